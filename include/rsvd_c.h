@@ -1,0 +1,132 @@
+/*
+ * rsvd_c.h -- C ABI of the MI355X-native randomized-SVD engine (librsvd_hip.so).
+ *
+ * Plain pointers and sizes only: no torch, Eigen or HIP types cross this boundary (streams are
+ * passed as `void*` = hipStream_t).  Every entry point returns an rsvd_status_t and never throws.
+ *
+ * Boundary mapping (reference = AMSC22-23/rSVD_Kamaneh_Raganato_Terrana @ 2024-10-08):
+ *   rsvd_run / rsvd_run_host_f64    <- void rSVD(Mat_m& A, Mat_m& U, Vec_v& S, Mat_m& V, int l,
+ *                                          SVDMethod)             include/rSVD.hpp:14, src/rSVD.cpp:72-133
+ *   rsvd_range_finder              <- void intermediate_step(const Mat_m& A, Mat_m& Q,
+ *                                          const Mat_m& Omega, int l, int q)
+ *                                                                  include/rSVD.hpp:13, src/rSVD.cpp:57-70
+ *   rsvd_generate_omega            <- Mat_m generateOmega(int n, int l)
+ *                                                                  include/rSVD.hpp:15, src/rSVD.cpp:12-55
+ *   rsvd_qr_reduced / rsvd_qr_full <- void qr_decomposition_reduced/full(const Mat_m& A, Mat_m& Q,
+ *                                          Mat_m& R)              include/QR.hpp:15-16, src/QR.cpp:22-80
+ *   rsvd_svd                       <- template<SVDMethod> SVD::compute()/getU/getS/getV
+ *                                                                  include/SVD_class.hpp:35-71,79-180
+ * The C++ drop-in headers include/rSVD.hpp, include/QR.hpp, include/SVD_class.hpp sit on top of
+ * these symbols with the reference's exact signatures.
+ *
+ * Layouts: every matrix is COLUMN-major (Eigen's default) with an explicit leading dimension.
+ * Device-pointer entry points are asynchronous on the handle's stream; *_host_* variants copy
+ * host buffers in and out and synchronise.
+ */
+#ifndef RSVD_C_H
+#define RSVD_C_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RSVD_ABI_VERSION 1
+
+typedef enum {
+    RSVD_OK = 0,
+    RSVD_ERR_INVALID_ARG = 1,    /* bad sizes / pointers (Eigen would assert)                      */
+    RSVD_ERR_UNSUPPORTED = 2,    /* e.g. SVD method not available; maps to std::invalid_argument     */
+    RSVD_ERR_HIP = 3,            /* a HIP runtime / launch error (see rsvd_last_error)              */
+    RSVD_ERR_NO_DEVICE = 4,
+    RSVD_ERR_NUMERICAL = 5,      /* non-finite result                                              */
+    RSVD_ERR_COMM = 6            /* the distributed all-reduce callback failed                      */
+} rsvd_status_t;
+
+/* Storage / compute type of A.  F64: fp64 end to end (bit-for-bit the reference's arithmetic
+ * class).  F32: fp32 MFMA projections, fp64 Gram/Cholesky/Jacobi. */
+typedef enum { RSVD_F64 = 0, RSVD_F32 = 1 } rsvd_dtype_t;
+
+/* Mirrors enum class SVDMethod { Jacobi, Power, ParallelJacobi } (include/SVD_class.hpp:28-32). */
+typedef enum { RSVD_SVD_JACOBI = 0, RSVD_SVD_POWER = 1, RSVD_SVD_PARALLEL_JACOBI = 2 } rsvd_svd_method_t;
+
+/* Orthonormalisation of the tall-skinny panels.  AUTO = CholeskyQR2 with the Householder
+ * TSQR fallback when the Cholesky flags ill-conditioning. */
+typedef enum { RSVD_QR_AUTO = 0, RSVD_QR_HOUSEHOLDER = 1, RSVD_QR_CHOLQR2 = 2 } rsvd_qr_mode_t;
+
+typedef struct {
+    int64_t m, n;              /* A is m x n                                                   */
+    int64_t lda;               /* >= m                                                         */
+    int32_t l;                 /* sketch width k + p (the reference's `l`)                     */
+    int32_t q;                 /* power iterations; the reference hard-codes 2 (src/rSVD.cpp:83) */
+    int32_t dtype;             /* rsvd_dtype_t                                                 */
+    int32_t method;            /* rsvd_svd_method_t                                            */
+    int32_t qr_mode;           /* rsvd_qr_mode_t                                               */
+    int32_t reserved;
+    uint64_t seed;             /* Philox key for Omega when no Omega is supplied               */
+} rsvd_desc_t;
+
+/* Diagnostics of the last run on a handle. */
+typedef struct {
+    int32_t cholqr_fallbacks;  /* panels re-orthonormalised by Householder TSQR                 */
+    int32_t jacobi_sweeps;     /* sweeps of the small SVD                                      */
+    int32_t splits_nn, splits_tn; /* K splits chosen for the projections                         */
+} rsvd_info_t;
+
+typedef struct rsvd_handle_s *rsvd_handle_t;
+
+/* Distributed exchange hook: sum `count` elements of `dtype` at device pointer `buf` over all
+ * ranks, in place, ordered after the work already enqueued on `stream`.  Return 0 on success.
+ * (The Python front end binds it to torch.distributed.all_reduce over RCCL.) */
+typedef int (*rsvd_allreduce_fn)(void *buf, int64_t count, int32_t dtype, void *stream, void *user);
+
+const char *rsvd_status_string(int status);
+int rsvd_abi_version(void);
+
+int rsvd_create(int device, rsvd_handle_t *out);
+int rsvd_destroy(rsvd_handle_t h);
+int rsvd_set_stream(rsvd_handle_t h, void *hip_stream);
+const char *rsvd_last_error(rsvd_handle_t h);
+int rsvd_get_info(rsvd_handle_t h, rsvd_info_t *info);
+/* Row-sharded runs: this handle owns rows [offset, offset + m_local) of a global m x n A; the
+ * hook sums the n x l partial products A_g^T Q_g and the l x l Grams across ranks. */
+int rsvd_set_comm(rsvd_handle_t h, int rank, int world, rsvd_allreduce_fn fn, void *user);
+
+/* Row partition of src/rSVD.cpp:20-23 / src/PM.cpp:31-35: rows of rank `rank` out of `world`.
+ * Host-only arithmetic (no device needed).  Returns the local row count, *offset = first row. */
+int64_t rsvd_row_partition(int64_t rows, int world, int rank, int64_t *offset);
+
+/* Device workspace bytes rsvd_run needs for `desc` (allocated lazily by the handle). */
+int rsvd_workspace_bytes(const rsvd_desc_t *desc, size_t *bytes);
+/* Use caller-owned device memory as the workspace (NULL reverts to handle-owned memory). */
+int rsvd_set_workspace(rsvd_handle_t h, void *ptr, size_t bytes);
+
+/* ---- device-pointer entry points (asynchronous on the handle stream) ---------------------- */
+
+/* rSVD: U (m x d, ldu), S (d), V (n x d, ldv), d = min(l, n); element type = desc->dtype.
+ * omega: optional n x l column-major (ld = ldo) sketch; NULL => Philox(desc->seed). */
+int rsvd_run(rsvd_handle_t h, const rsvd_desc_t *desc, const void *A, const void *omega, int64_t ldo,
+             void *U, int64_t ldu, void *S, void *V, int64_t ldv);
+
+/* intermediate_step: Q (m x l, ldq) orthonormal basis of the range of (A A^T)^q A Omega. */
+int rsvd_range_finder(rsvd_handle_t h, const rsvd_desc_t *desc, const void *A, const void *omega, int64_t ldo,
+                      void *Q, int64_t ldq);
+
+/* generateOmega: n x l N(0,1), column-major (ld = n), element (i,j) = Philox stream element i+n*j. */
+int rsvd_generate_omega(rsvd_handle_t h, int64_t n, int32_t l, uint64_t seed, int32_t dtype, void *omega);
+
+/* ---- host-pointer fp64 entry points used by the C++ drop-in headers (synchronous) --------- */
+int rsvd_run_host_f64(rsvd_handle_t h, int64_t m, int64_t n, const double *A, int64_t lda, int32_t l,
+                      int32_t q, int32_t method, const double *omega /* nullable, n x l, ld n */,
+                      uint64_t seed, double *U /* m x d */, double *S /* d */, double *V /* n x d */);
+int rsvd_range_finder_host_f64(rsvd_handle_t h, int64_t m, int64_t n, const double *A, int64_t lda,
+                               const double *omega /* n x l, ld n */, int32_t l, int32_t q,
+                               double *Q /* m x l */);
+int rsvd_generate_omega_host_f64(rsvd_handle_t h, int64_t n, int32_t l, uint64_t seed, double *omega);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RSVD_C_H */

@@ -1,0 +1,130 @@
+"""ctypes binding of the C ABI in include/rsvd_c.h (librsvd_hip.so, gfx950).
+
+The shared library is built in-tree (``build()``) so it travels with the repository; importing
+the package never falls back to a CPU implementation: if the library is missing or the GPU
+runtime is absent, the calls raise.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(PKG_DIR, "csrc")
+LIB_PATH = os.path.join(PKG_DIR, "librsvd_hip.so")
+REPO = os.path.dirname(PKG_DIR)
+
+RSVD_OK = 0
+STATUS = {
+    0: "ok",
+    1: "invalid argument",
+    2: "unsupported",
+    3: "HIP error",
+    4: "no HIP device",
+    5: "numerical failure",
+    6: "communication failure",
+}
+
+F64, F32 = 0, 1
+SVD_JACOBI, SVD_POWER, SVD_PARALLEL_JACOBI = 0, 1, 2
+QR_AUTO, QR_HOUSEHOLDER, QR_CHOLQR2 = 0, 1, 2
+
+# Every symbol include/rsvd_c.h declares (checked by tests/test_capi_exports.py).
+EXPORTS = (
+    "rsvd_status_string", "rsvd_abi_version", "rsvd_create", "rsvd_destroy", "rsvd_set_stream",
+    "rsvd_last_error", "rsvd_get_info", "rsvd_set_comm", "rsvd_row_partition",
+    "rsvd_workspace_bytes", "rsvd_set_workspace", "rsvd_run", "rsvd_range_finder",
+    "rsvd_generate_omega", "rsvd_run_host_f64", "rsvd_range_finder_host_f64",
+    "rsvd_generate_omega_host_f64",
+)
+
+
+class Desc(ctypes.Structure):
+    _fields_ = [
+        ("m", ctypes.c_int64), ("n", ctypes.c_int64), ("lda", ctypes.c_int64),
+        ("l", ctypes.c_int32), ("q", ctypes.c_int32), ("dtype", ctypes.c_int32),
+        ("method", ctypes.c_int32), ("qr_mode", ctypes.c_int32), ("reserved", ctypes.c_int32),
+        ("seed", ctypes.c_uint64),
+    ]
+
+
+class Info(ctypes.Structure):
+    _fields_ = [
+        ("cholqr_fallbacks", ctypes.c_int32), ("jacobi_sweeps", ctypes.c_int32),
+        ("splits_nn", ctypes.c_int32), ("splits_tn", ctypes.c_int32),
+    ]
+
+
+ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
+                                ctypes.c_void_p, ctypes.c_void_p)
+
+
+def build(jobs: int = 8, force: bool = False) -> str:
+    """Compile librsvd_hip.so for gfx950 with hipcc (cross-compiles without a GPU)."""
+    cmd = ["make", "-C", CSRC, f"-j{jobs}"]
+    if force:
+        subprocess.run(["make", "-C", CSRC, "clean"], check=True, capture_output=True)
+    subprocess.run(cmd, check=True)
+    return LIB_PATH
+
+
+_LIB = None
+
+
+def lib():
+    """Load librsvd_hip.so (raises if it has not been built)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} is missing: run rsvd_kamaneh_raganato_terrana_amd.build()")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, i32, i64, u64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64
+    dp = ctypes.POINTER(ctypes.c_double)
+    L.rsvd_status_string.restype = ctypes.c_char_p
+    L.rsvd_status_string.argtypes = [ctypes.c_int]
+    L.rsvd_last_error.restype = ctypes.c_char_p
+    L.rsvd_last_error.argtypes = [vp]
+    L.rsvd_create.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
+    L.rsvd_destroy.argtypes = [vp]
+    L.rsvd_set_stream.argtypes = [vp, vp]
+    L.rsvd_get_info.argtypes = [vp, ctypes.POINTER(Info)]
+    L.rsvd_set_comm.argtypes = [vp, ctypes.c_int, ctypes.c_int, ALLREDUCE_FN, vp]
+    L.rsvd_row_partition.restype = i64
+    L.rsvd_row_partition.argtypes = [i64, ctypes.c_int, ctypes.c_int, ctypes.POINTER(i64)]
+    L.rsvd_workspace_bytes.argtypes = [ctypes.POINTER(Desc), ctypes.POINTER(ctypes.c_size_t)]
+    L.rsvd_set_workspace.argtypes = [vp, vp, ctypes.c_size_t]
+    L.rsvd_run.argtypes = [vp, ctypes.POINTER(Desc), vp, vp, i64, vp, i64, vp, vp, i64]
+    L.rsvd_range_finder.argtypes = [vp, ctypes.POINTER(Desc), vp, vp, i64, vp, i64]
+    L.rsvd_generate_omega.argtypes = [vp, i64, i32, u64, i32, vp]
+    L.rsvd_run_host_f64.argtypes = [vp, i64, i64, dp, i64, i32, i32, i32, dp, u64, dp, dp, dp]
+    L.rsvd_range_finder_host_f64.argtypes = [vp, i64, i64, dp, i64, dp, i32, i32, dp]
+    L.rsvd_generate_omega_host_f64.argtypes = [vp, i64, i32, u64, dp]
+    _LIB = L
+    return L
+
+
+class RSVDError(RuntimeError):
+    def __init__(self, status: int, detail: str = ""):
+        self.status = status
+        super().__init__(f"{STATUS.get(status, status)}: {detail}")
+
+
+def check(status: int, handle=None) -> None:
+    if status != RSVD_OK:
+        detail = ""
+        if handle:
+            detail = (lib().rsvd_last_error(handle) or b"").decode()
+        if status == 2 and "Unsupported SVD method" in detail:
+            raise ValueError("Unsupported SVD method")  # std::invalid_argument, src/rSVD.cpp:123
+        raise RSVDError(status, detail)
+
+
+def row_partition(rows: int, world: int, rank: int):
+    """(local_rows, offset) per src/rSVD.cpp:20-23 -- host arithmetic, no GPU needed."""
+    off = ctypes.c_int64(0)
+    n = lib().rsvd_row_partition(rows, world, rank, ctypes.byref(off))
+    if n < 0:
+        raise ValueError("bad partition arguments")
+    return int(n), int(off.value)

@@ -1,0 +1,259 @@
+"""Python host mirror of the reference's rSVD interface, running on the MI355X engine.
+
+Reference signatures mirrored (AMSC22-23/rSVD_Kamaneh_Raganato_Terrana):
+
+* ``rSVD(A, l, method=SVDMethod.Jacobi)`` -> ``(U, S, V)``
+      void rSVD(Mat_m& A, Mat_m& U, Vec_v& S, Mat_m& V, int l, SVDMethod)  include/rSVD.hpp:14
+* ``intermediate_step(A, Omega, l, q)`` -> ``Q``
+      void intermediate_step(const Mat_m&, Mat_m& Q, const Mat_m& Omega, int l, int q)  :13
+* ``generateOmega(n, l)`` -> ``Omega``                    Mat_m generateOmega(int, int)  :15
+* ``SVDMethod`` (Jacobi, Power, ParallelJacobi)           include/SVD_class.hpp:28-32
+
+numpy float64 inputs take the synchronous fp64 host path (the drop-in the reference's Eigen
+callers see); torch CUDA tensors (float32 / float64) take the asynchronous device path on the
+current torch stream, with A resident in HBM.  There is no CPU fallback: without the HIP
+library or a GPU these functions raise.
+"""
+from __future__ import annotations
+
+import ctypes
+import enum
+from typing import Optional
+
+import numpy as np
+
+from . import _capi
+from ._capi import Desc, Info, check, lib
+
+
+class SVDMethod(enum.IntEnum):
+    Jacobi = 0
+    Power = 1
+    ParallelJacobi = 2
+
+
+class QRMode(enum.IntEnum):
+    Auto = 0
+    Householder = 1
+    CholQR2 = 2
+
+
+def _dp(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+
+
+def _torch():
+    import torch  # plumbing only: device memory, streams, torch.distributed
+
+    return torch
+
+
+def colmajor(t):
+    """A column-major (Fortran-order) view/copy of a 2-D torch tensor and its leading dim."""
+    if t.dim() != 2:
+        raise ValueError("expected a matrix")
+    if t.stride(0) == 1 and t.stride(1) >= max(1, t.shape[0]):
+        return t, t.stride(1)
+    c = t.t().contiguous().t()
+    return c, max(1, c.shape[0])
+
+
+def empty_colmajor(rows: int, cols: int, dtype, device):
+    torch = _torch()
+    return torch.empty((cols, rows), dtype=dtype, device=device).t()
+
+
+class Engine:
+    """One GPU handle (HIP stream + workspace); mirrors what a C++ caller gets from librsvd_hip."""
+
+    def __init__(self, device: int = 0):
+        self.device = device
+        h = ctypes.c_void_p()
+        check(lib().rsvd_create(device, ctypes.byref(h)))
+        self.h = h
+        self._ws = None
+        self._hook = None
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().rsvd_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- plumbing --------------------------------------------------------------------------
+    def _bind_stream(self):
+        torch = _torch()
+        s = torch.cuda.current_stream(self.device)
+        check(lib().rsvd_set_stream(self.h, ctypes.c_void_p(s.cuda_stream)), self.h)
+
+    def reserve(self, desc: Desc):
+        """Allocate the workspace from torch's allocator (outside any timed region)."""
+        torch = _torch()
+        nbytes = ctypes.c_size_t(0)
+        check(lib().rsvd_workspace_bytes(ctypes.byref(desc), ctypes.byref(nbytes)))
+        if self._ws is None or self._ws.numel() < nbytes.value:
+            self._ws = torch.empty(nbytes.value, dtype=torch.uint8, device=f"cuda:{self.device}")
+            check(lib().rsvd_set_workspace(self.h, ctypes.c_void_p(self._ws.data_ptr()), nbytes.value), self.h)
+        return self._ws
+
+    def set_comm(self, rank: int, world: int, group=None):
+        """Row-sharded runs: bind the exchange hook to torch.distributed.all_reduce (RCCL)."""
+        torch = _torch()
+        import torch.distributed as dist
+
+        eng = self
+
+        def _hook(buf, count, dtype, stream, user):
+            try:
+                ws = eng._ws
+                base = ws.data_ptr()
+                tdt = torch.float64 if dtype == _capi.F64 else torch.float32
+                esz = 8 if dtype == _capi.F64 else 4
+                off = buf - base
+                if off < 0 or off % esz or off + count * esz > ws.numel():
+                    return 1
+                view = ws[off: off + count * esz].view(tdt)
+                dist.all_reduce(view, op=dist.ReduceOp.SUM, group=group)
+                return 0
+            except Exception:  # never unwind through C
+                return 1
+
+        self._hook = _capi.ALLREDUCE_FN(_hook)
+        check(lib().rsvd_set_comm(self.h, rank, world, self._hook, None), self.h)
+
+    def info(self) -> dict:
+        inf = Info()
+        check(lib().rsvd_get_info(self.h, ctypes.byref(inf)), self.h)
+        return {k: getattr(inf, k) for k, _ in Info._fields_}
+
+    # -- device path -----------------------------------------------------------------------
+    def desc(self, A, l: int, q: int = 2, method: int = SVDMethod.Jacobi, seed: int = 0,
+             qr_mode: int = QRMode.Auto) -> Desc:
+        torch = _torch()
+        dt = {torch.float64: _capi.F64, torch.float32: _capi.F32}.get(A.dtype)
+        if dt is None:
+            raise TypeError(f"unsupported dtype {A.dtype}")
+        lda = A.stride(1) if A.stride(0) == 1 else None
+        if lda is None:
+            raise ValueError("A must be column-major (use colmajor())")
+        return Desc(m=A.shape[0], n=A.shape[1], lda=max(lda, A.shape[0]), l=l, q=q, dtype=dt,
+                    method=int(method), qr_mode=int(qr_mode), reserved=0, seed=seed)
+
+    def rsvd(self, A, l: int, q: int = 2, method: int = SVDMethod.Jacobi, omega=None, seed: int = 0,
+             qr_mode: int = QRMode.Auto, out=None):
+        """Device rSVD: A (m x n, CUDA, column-major f32/f64) -> U (m x l), S (l), V (n x l)."""
+        torch = _torch()
+        A, _ = colmajor(A)
+        d = self.desc(A, l, q, method, seed, qr_mode)
+        self.reserve(d)
+        self._bind_stream()
+        m, n = A.shape
+        dd = min(l, n)
+        if out is None:
+            U = empty_colmajor(m, dd, A.dtype, A.device)
+            S = torch.empty(dd, dtype=A.dtype, device=A.device)
+            V = empty_colmajor(n, dd, A.dtype, A.device)
+        else:
+            U, S, V = out
+        om, ldo = (None, 0)
+        if omega is not None:
+            om, ldo = colmajor(omega.to(device=A.device, dtype=A.dtype))
+        check(lib().rsvd_run(self.h, ctypes.byref(d), ctypes.c_void_p(A.data_ptr()),
+                             ctypes.c_void_p(om.data_ptr() if om is not None else 0), ldo,
+                             ctypes.c_void_p(U.data_ptr()), U.stride(1),
+                             ctypes.c_void_p(S.data_ptr()),
+                             ctypes.c_void_p(V.data_ptr()), V.stride(1)), self.h)
+        return U, S, V
+
+    def range_finder(self, A, omega, q: int = 2, qr_mode: int = QRMode.Auto):
+        torch = _torch()
+        A, _ = colmajor(A)
+        om, ldo = colmajor(omega.to(device=A.device, dtype=A.dtype))
+        l = om.shape[1]
+        d = self.desc(A, l, q, SVDMethod.Jacobi, 0, qr_mode)
+        self.reserve(d)
+        self._bind_stream()
+        Q = empty_colmajor(A.shape[0], l, A.dtype, A.device)
+        check(lib().rsvd_range_finder(self.h, ctypes.byref(d), ctypes.c_void_p(A.data_ptr()),
+                                      ctypes.c_void_p(om.data_ptr()), ldo, ctypes.c_void_p(Q.data_ptr()),
+                                      Q.stride(1)), self.h)
+        return Q
+
+    def generate_omega(self, n: int, l: int, seed: int = 0, dtype=None):
+        torch = _torch()
+        dtype = dtype or torch.float64
+        self._bind_stream()
+        Om = empty_colmajor(n, l, dtype, f"cuda:{self.device}")
+        check(lib().rsvd_generate_omega(self.h, n, l, seed, _capi.F64 if dtype == torch.float64 else _capi.F32,
+                                        ctypes.c_void_p(Om.data_ptr())), self.h)
+        return Om
+
+    # -- host fp64 path (the Eigen-callers' drop-in) ----------------------------------------
+    def rsvd_host(self, A: np.ndarray, l: int, q: int = 2, method: int = SVDMethod.Jacobi,
+                  omega: Optional[np.ndarray] = None, seed: int = 0):
+        A = np.asfortranarray(A, dtype=np.float64)
+        m, n = A.shape
+        dd = min(l, n)
+        U = np.zeros((m, dd), order="F")
+        S = np.zeros(dd)
+        V = np.zeros((n, dd), order="F")
+        om = None if omega is None else np.asfortranarray(omega, dtype=np.float64)
+        check(lib().rsvd_run_host_f64(self.h, m, n, _dp(A), m, l, q, int(method),
+                                      _dp(om) if om is not None else None, seed, _dp(U), _dp(S), _dp(V)),
+              self.h)
+        return U, S, V
+
+    def range_finder_host(self, A: np.ndarray, omega: np.ndarray, q: int = 2) -> np.ndarray:
+        A = np.asfortranarray(A, dtype=np.float64)
+        om = np.asfortranarray(omega, dtype=np.float64)
+        m, n = A.shape
+        l = om.shape[1]
+        Q = np.zeros((m, l), order="F")
+        check(lib().rsvd_range_finder_host_f64(self.h, m, n, _dp(A), m, _dp(om), l, q, _dp(Q)), self.h)
+        return Q
+
+    def generate_omega_host(self, n: int, l: int, seed: int = 0) -> np.ndarray:
+        om = np.zeros((n, l), order="F")
+        check(lib().rsvd_generate_omega_host_f64(self.h, n, l, seed, _dp(om)), self.h)
+        return om
+
+
+_DEFAULT: Optional[Engine] = None
+
+
+def default_engine() -> Engine:
+    global _DEFAULT
+    if _DEFAULT is None:
+        _DEFAULT = Engine(0)
+    return _DEFAULT
+
+
+def _is_torch(x) -> bool:
+    return type(x).__module__.startswith("torch")
+
+
+# ---- reference-named free functions ------------------------------------------------------------
+def rSVD(A, l: int, method: SVDMethod = SVDMethod.Jacobi, q: int = 2, omega=None, seed: int = 0):
+    """rSVD (src/rSVD.cpp:72-133). Returns (U, S, V); q defaults to the reference's hard-coded 2."""
+    eng = default_engine()
+    if _is_torch(A):
+        return eng.rsvd(A, l, q=q, method=method, omega=omega, seed=seed)
+    return eng.rsvd_host(A, l, q=q, method=method, omega=omega, seed=seed)
+
+
+def intermediate_step(A, Omega, l: int, q: int):
+    """intermediate_step (src/rSVD.cpp:57-70): the orthonormal range basis Q (m x l)."""
+    eng = default_engine()
+    if _is_torch(A):
+        return eng.range_finder(A, Omega[:, :l], q=q)
+    return eng.range_finder_host(A, np.asarray(Omega)[:, :l], q=q)
+
+
+def generateOmega(n: int, l: int, seed: int = 0):
+    """generateOmega (src/rSVD.cpp:12-55): n x l N(0,1), reproducible from `seed`."""
+    return default_engine().generate_omega_host(n, l, seed)

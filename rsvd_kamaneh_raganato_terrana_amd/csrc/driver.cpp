@@ -1,0 +1,490 @@
+// driver.cpp -- native host orchestration of the MI355X rSVD and the C ABI (include/rsvd_c.h).
+//
+// One handle = one GPU + one HIP stream + a lazily grown device workspace.  rsvd_run enqueues
+// the whole randomized SVD of src/rSVD.cpp:72-133 on the stream without host synchronisation:
+//
+//   Omega (Philox, util.hip)                            generateOmega        src/rSVD.cpp:81
+//   Y = A Omega (proj_nn) ; Q = orth(Y) (qr.hip)        intermediate_step    src/rSVD.cpp:59-61
+//   q x { Z = A^T Q ; Q_n = orth(Z) ; Y = A Q_n ; Q = orth(Y) }                src/rSVD.cpp:62-69
+//   B^T = A^T Q (proj_tn) ; B^T = Q_B R                 B = Q^T A + the QR   src/rSVD.cpp:89,
+//                                                       preconditioning of   SVD_class.hpp:116-123
+//   W = R^T = U_w S V_w^T (jacobi.hip)                  SVD<Jacobi>          SVD_class.hpp:126-178
+//   U = Q U_w ; V = Q_B V_w (panel_small)               U = Q * Utilde       src/rSVD.cpp:128
+//
+// Row sharding (world > 1): the handle holds rows [off, off + m_local) of A (src/rSVD.cpp:20-23
+// split).  The m-side panels stay sharded (their l x l Grams are summed through the all-reduce
+// hook), the n-side panels A^T Q = sum_g A_g^T Q_g are summed through the hook and then
+// orthonormalised redundantly on every rank, so every rank ends with the same Q_B, S, V and
+// its own rows of U.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/rsvd_c.h"
+#include "kernels.hpp"
+
+using namespace rsvd;
+
+struct rsvd_handle_s {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    std::string err;
+    char* ws = nullptr;
+    size_t ws_bytes = 0;
+    bool ws_external = false;  // workspace supplied by the caller (rsvd_set_workspace)
+    int* dflags = nullptr;  // [0] cholqr breakdown count, [1] jacobi sweeps
+    rsvd_info_t info{};
+    int rank = 0, world = 1;
+    rsvd_allreduce_fn allreduce = nullptr;
+    void* ar_user = nullptr;
+};
+
+namespace {
+
+#define RSVD_CK(expr)                                                                         \
+    do {                                                                                      \
+        hipError_t _e = (expr);                                                               \
+        if (_e != hipSuccess) {                                                               \
+            h->err = std::string(#expr) + ": " + hipGetErrorString(_e);                       \
+            return RSVD_ERR_HIP;                                                              \
+        }                                                                                     \
+    } while (0)
+
+#define RSVD_TRY(expr)                   \
+    do {                                 \
+        int _s = (expr);                 \
+        if (_s != RSVD_OK) return _s;    \
+    } while (0)
+
+inline int lp_of(int l) { return (l + 15) / 16 * 16; }
+inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
+
+template <typename T>
+struct Layout {
+    int64_t m, n;
+    int l, LP;
+    ProjPlan pnn, ptn;
+    int gram_m, gram_n;
+    size_t off_Xn, off_Zn, off_Ym, off_Qm, off_T1, off_slab, off_gram, off_small, total;
+
+    Layout(int64_t m_, int64_t n_, int l_) : m(m_), n(n_), l(l_), LP(lp_of(l_)) {
+        pnn = plan_proj_nn<T>(m, n, LP);
+        ptn = plan_proj_tn<T>(m, n, LP);
+        gram_m = plan_gram_blocks(m);
+        gram_n = plan_gram_blocks(n);
+        const int64_t mx = std::max(m, n);
+        size_t o = 0;
+        off_Xn = o; o = align256(o + sizeof(T) * n * LP);
+        off_Zn = o; o = align256(o + sizeof(T) * n * LP);
+        off_Ym = o; o = align256(o + sizeof(T) * m * LP);
+        off_Qm = o; o = align256(o + sizeof(T) * m * LP);
+        off_T1 = o; o = align256(o + sizeof(T) * mx * LP);
+        const int64_t slab_elems = std::max<int64_t>(pnn.splits > 1 ? pnn.splits * m : 0,
+                                                     ptn.splits > 1 ? ptn.splits * n : 0);
+        off_slab = o; o = align256(o + sizeof(T) * std::max<int64_t>(slab_elems, 1) * LP);
+        off_gram = o; o = align256(o + sizeof(double) * 64 * LP * LP);
+        off_small = o; o = align256(o + sizeof(double) * 8 * LP * LP);  // R1, R2, Rinv, Uw, Vw, Gsum
+        total = o;
+    }
+};
+
+int ensure_ws(rsvd_handle_t h, size_t bytes) {
+    if (bytes <= h->ws_bytes) return RSVD_OK;
+    if (h->ws_external) {
+        h->err = "caller workspace too small: need " + std::to_string(bytes) + " bytes";
+        return RSVD_ERR_INVALID_ARG;
+    }
+    if (h->ws) {
+        RSVD_CK(hipStreamSynchronize(h->stream));
+        RSVD_CK(hipFree(h->ws));
+        h->ws = nullptr;
+        h->ws_bytes = 0;
+    }
+    RSVD_CK(hipMalloc(&h->ws, bytes));
+    h->ws_bytes = bytes;
+    return RSVD_OK;
+}
+
+int check_desc(rsvd_handle_t h, const rsvd_desc_t* d) {
+    if (!d) { h->err = "null descriptor"; return RSVD_ERR_INVALID_ARG; }
+    if (d->m <= 0 || d->n <= 0 || d->l <= 0 || d->q < 0 || d->lda < d->m) {
+        h->err = "invalid sizes (need m, n, l > 0, q >= 0, lda >= m)";
+        return RSVD_ERR_INVALID_ARG;
+    }
+    if (d->dtype != RSVD_F64 && d->dtype != RSVD_F32) { h->err = "unsupported dtype"; return RSVD_ERR_UNSUPPORTED; }
+    if (d->method != RSVD_SVD_JACOBI && d->method != RSVD_SVD_PARALLEL_JACOBI) {
+        h->err = "Unsupported SVD method";  // src/rSVD.cpp:123 wording
+        return RSVD_ERR_UNSUPPORTED;
+    }
+    if (d->l > 64) { h->err = "l > 64 not supported yet"; return RSVD_ERR_UNSUPPORTED; }
+    if (d->l > d->n || d->l > d->m) { h->err = "l > min(m, n) not supported"; return RSVD_ERR_UNSUPPORTED; }
+    return RSVD_OK;
+}
+
+// ---- the pipeline ---------------------------------------------------------------------------
+template <typename T>
+struct Engine {
+    rsvd_handle_t h;
+    const Layout<T>& L;
+    hipStream_t s;
+    T *Xn, *Zn, *Ym, *Qm, *T1, *slab;
+    double *gram, *R1, *R2, *Rinv, *Uw, *Vw, *Gsum;
+
+    Engine(rsvd_handle_t h_, const Layout<T>& L_) : h(h_), L(L_), s(h_->stream) {
+        char* b = h->ws;
+        Xn = reinterpret_cast<T*>(b + L.off_Xn);
+        Zn = reinterpret_cast<T*>(b + L.off_Zn);
+        Ym = reinterpret_cast<T*>(b + L.off_Ym);
+        Qm = reinterpret_cast<T*>(b + L.off_Qm);
+        T1 = reinterpret_cast<T*>(b + L.off_T1);
+        slab = reinterpret_cast<T*>(b + L.off_slab);
+        gram = reinterpret_cast<double*>(b + L.off_gram);
+        double* sm = reinterpret_cast<double*>(b + L.off_small);
+        const int64_t q2 = (int64_t)L.LP * L.LP;
+        R1 = sm; R2 = sm + q2; Rinv = sm + 2 * q2; Uw = sm + 3 * q2; Vw = sm + 4 * q2; Gsum = sm + 5 * q2;
+    }
+
+    int allreduce(void* buf, int64_t count, int32_t dtype) {
+        if (h->world <= 1 || !h->allreduce) return RSVD_OK;
+        if (h->allreduce(buf, count, dtype, (void*)s, h->ar_user) != 0) {
+            h->err = "all-reduce hook failed";
+            return RSVD_ERR_COMM;
+        }
+        return RSVD_OK;
+    }
+
+    // One CholeskyQR pass: R = chol(P^T P) (summed over ranks when `sharded`), Out = P R^-1.
+    int cholqr_pass(const T* P, int64_t rows, T* Out, double* Rdst, double* Racc, int accumulate, bool sharded) {
+        const int nb = plan_gram_blocks(rows);
+        RSVD_CK(launch_gram_partial<T>(P, rows, L.LP, nb, gram, s));
+        const double* gsrc = gram;
+        int nsl = nb;
+        if (sharded && h->world > 1) {
+            RSVD_CK(launch_sum_slabs<double>(gram, (int64_t)L.LP * L.LP, nb, (int64_t)L.LP * L.LP, Gsum, s));
+            RSVD_TRY(allreduce(Gsum, (int64_t)L.LP * L.LP, RSVD_F64));
+            gsrc = Gsum;
+            nsl = 1;
+        }
+        RSVD_CK(launch_chol_inv(gsrc, nsl, L.l, L.LP, Rdst, Rinv, Racc, accumulate, h->dflags, s));
+        RSVD_CK(launch_panel_small<T>(P, rows, L.LP, Rinv, Out, 0, 0, 0, s));
+        return RSVD_OK;
+    }
+
+    // CholeskyQR2: Q = orth(P); R1 <- R2 * R1 (the panel's R) when want_r.
+    int orth(const T* P, int64_t rows, T* Q, bool sharded) {
+        RSVD_TRY(cholqr_pass(P, rows, T1, R1, nullptr, 0, sharded));
+        RSVD_TRY(cholqr_pass(T1, rows, Q, R2, R1, 1, sharded));
+        return RSVD_OK;
+    }
+
+    int proj_nn(const T* A, int64_t lda, const T* X, T* Y) {
+        RSVD_CK(launch_proj_nn<T>(A, lda, L.m, L.n, X, L.LP, L.pnn, slab, Y, s));
+        return RSVD_OK;
+    }
+    int proj_tn(const T* A, int64_t lda, const T* Q, T* Z) {
+        RSVD_CK(launch_proj_tn<T>(A, lda, L.m, L.n, Q, L.LP, L.ptn, slab, Z, s));
+        // Z = sum_g A_g^T Q_g over the row shards
+        return allreduce(Z, L.n * L.LP, sizeof(T) == 8 ? RSVD_F64 : RSVD_F32);
+    }
+
+    int load_omega(const void* omega, int64_t ldo, uint64_t seed) {
+        if (omega) {
+            RSVD_CK(launch_colmajor_to_panel<T>(reinterpret_cast<const T*>(omega), ldo, L.n, L.l, L.LP, Xn, s));
+        } else {
+            RSVD_CK(launch_philox_omega<T>(Xn, L.n, L.l, L.LP, seed, s));
+        }
+        return RSVD_OK;
+    }
+
+    // intermediate_step (src/rSVD.cpp:57-70): leaves Q (m x LP panel) in Qm.
+    int range_finder(const T* A, int64_t lda, int q) {
+        RSVD_TRY(proj_nn(A, lda, Xn, Ym));
+        RSVD_TRY(orth(Ym, L.m, Qm, true));
+        for (int i = 0; i < q; ++i) {
+            RSVD_TRY(proj_tn(A, lda, Qm, Zn));
+            RSVD_TRY(orth(Zn, L.n, Xn, false));
+            RSVD_TRY(proj_nn(A, lda, Xn, Ym));
+            RSVD_TRY(orth(Ym, L.m, Qm, true));
+        }
+        return RSVD_OK;
+    }
+
+    int run(const rsvd_desc_t* d, const T* A, void* U, int64_t ldu, T* S, void* V, int64_t ldv) {
+        RSVD_TRY(range_finder(A, d->lda, d->q));
+        // Stage B: B^T = A^T Q, QR-preconditioned as in SVD_class.hpp:116-123.
+        RSVD_TRY(proj_tn(A, d->lda, Qm, Zn));
+        RSVD_TRY(orth(Zn, L.n, Xn, false));  // Xn = Q_B, R1 = R
+        RSVD_CK(launch_small_svd<T>(R1, L.l, L.LP, Uw, Vw, S, h->dflags + 1, s));
+        const int dcols = L.l;  // d = min(l, n) = l (l <= n enforced)
+        RSVD_CK(launch_panel_small<T>(Qm, L.m, L.LP, Uw, reinterpret_cast<T*>(U), 1, dcols, ldu, s));
+        RSVD_CK(launch_panel_small<T>(Xn, L.n, L.LP, Vw, reinterpret_cast<T*>(V), 1, dcols, ldv, s));
+        return RSVD_OK;
+    }
+};
+
+template <typename T>
+int run_typed(rsvd_handle_t h, const rsvd_desc_t* d, const void* A, const void* omega, int64_t ldo, void* U,
+              int64_t ldu, void* S, void* V, int64_t ldv, void* Qout, int64_t ldq) {
+    Layout<T> L(d->m, d->n, d->l);
+    RSVD_TRY(ensure_ws(h, L.total));
+    RSVD_CK(hipMemsetAsync(h->dflags, 0, 4 * sizeof(int), h->stream));
+    h->info.splits_nn = L.pnn.splits;
+    h->info.splits_tn = L.ptn.splits;
+    Engine<T> E(h, L);
+    RSVD_TRY(E.load_omega(omega, ldo, d->seed));
+    if (Qout) {
+        RSVD_TRY(E.range_finder(reinterpret_cast<const T*>(A), d->lda, d->q));
+        RSVD_CK(launch_panel_to_colmajor<T>(E.Qm, L.m, L.l, L.LP, reinterpret_cast<T*>(Qout), ldq, h->stream));
+        return RSVD_OK;
+    }
+    return E.run(d, reinterpret_cast<const T*>(A), U, ldu, reinterpret_cast<T*>(S), V, ldv);
+}
+
+int set_device(rsvd_handle_t h) {
+    RSVD_CK(hipSetDevice(h->device));
+    return RSVD_OK;
+}
+
+}  // namespace
+
+// =============================================================================================
+// C ABI
+// =============================================================================================
+extern "C" {
+
+const char* rsvd_status_string(int status) {
+    switch (status) {
+        case RSVD_OK: return "ok";
+        case RSVD_ERR_INVALID_ARG: return "invalid argument";
+        case RSVD_ERR_UNSUPPORTED: return "unsupported";
+        case RSVD_ERR_HIP: return "HIP error";
+        case RSVD_ERR_NO_DEVICE: return "no HIP device";
+        case RSVD_ERR_NUMERICAL: return "numerical failure";
+        case RSVD_ERR_COMM: return "communication failure";
+        default: return "unknown status";
+    }
+}
+
+int rsvd_abi_version(void) { return RSVD_ABI_VERSION; }
+
+int64_t rsvd_row_partition(int64_t rows, int world, int rank, int64_t* offset) {
+    // src/rSVD.cpp:20-23: rows_per_proc = rows / P, remainder spread over the first ranks.
+    if (world <= 0 || rank < 0 || rank >= world || rows < 0) {
+        if (offset) *offset = 0;
+        return -1;
+    }
+    const int64_t per = rows / world, rem = rows % world;
+    const int64_t local = (rank < rem) ? per + 1 : per;
+    if (offset) *offset = rank * per + std::min<int64_t>(rank, rem);
+    return local;
+}
+
+int rsvd_create(int device, rsvd_handle_t* out) {
+    if (!out) return RSVD_ERR_INVALID_ARG;
+    *out = nullptr;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) return RSVD_ERR_NO_DEVICE;
+    if (device < 0 || device >= count) return RSVD_ERR_INVALID_ARG;
+    rsvd_handle_t h = new rsvd_handle_s();
+    h->device = device;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc(&h->dflags, 16 * sizeof(int)) != hipSuccess) {
+        delete h;
+        return RSVD_ERR_HIP;
+    }
+    h->own_stream = true;
+    *out = h;
+    return RSVD_OK;
+}
+
+int rsvd_destroy(rsvd_handle_t h) {
+    if (!h) return RSVD_OK;
+    (void)hipSetDevice(h->device);
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    if (h->ws && !h->ws_external) (void)hipFree(h->ws);
+    if (h->dflags) (void)hipFree(h->dflags);
+    if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
+    delete h;
+    return RSVD_OK;
+}
+
+int rsvd_set_stream(rsvd_handle_t h, void* stream) {
+    if (!h) return RSVD_ERR_INVALID_ARG;
+    if (h->own_stream && h->stream) {
+        (void)hipStreamSynchronize(h->stream);
+        (void)hipStreamDestroy(h->stream);
+    }
+    h->stream = reinterpret_cast<hipStream_t>(stream);
+    h->own_stream = false;
+    return RSVD_OK;
+}
+
+const char* rsvd_last_error(rsvd_handle_t h) { return h ? h->err.c_str() : "null handle"; }
+
+int rsvd_get_info(rsvd_handle_t h, rsvd_info_t* info) {
+    if (!h || !info) return RSVD_ERR_INVALID_ARG;
+    RSVD_TRY(set_device(h));
+    int flags[2] = {0, 0};
+    RSVD_CK(hipMemcpyAsync(flags, h->dflags, 2 * sizeof(int), hipMemcpyDeviceToHost, h->stream));
+    RSVD_CK(hipStreamSynchronize(h->stream));
+    h->info.cholqr_fallbacks = flags[0];
+    h->info.jacobi_sweeps = flags[1];
+    *info = h->info;
+    return RSVD_OK;
+}
+
+int rsvd_set_workspace(rsvd_handle_t h, void* ptr, size_t bytes) {
+    if (!h || (!ptr && bytes)) return RSVD_ERR_INVALID_ARG;
+    if (h->ws && !h->ws_external) {
+        (void)hipStreamSynchronize(h->stream);
+        (void)hipFree(h->ws);
+    }
+    h->ws = reinterpret_cast<char*>(ptr);
+    h->ws_bytes = ptr ? bytes : 0;
+    h->ws_external = ptr != nullptr;
+    return RSVD_OK;
+}
+
+int rsvd_set_comm(rsvd_handle_t h, int rank, int world, rsvd_allreduce_fn fn, void* user) {
+    if (!h || world < 1 || rank < 0 || rank >= world || (world > 1 && !fn)) return RSVD_ERR_INVALID_ARG;
+    h->rank = rank;
+    h->world = world;
+    h->allreduce = fn;
+    h->ar_user = user;
+    return RSVD_OK;
+}
+
+int rsvd_workspace_bytes(const rsvd_desc_t* d, size_t* bytes) {
+    if (!d || !bytes) return RSVD_ERR_INVALID_ARG;
+    if (d->dtype == RSVD_F64)
+        *bytes = Layout<double>(d->m, d->n, d->l).total;
+    else
+        *bytes = Layout<float>(d->m, d->n, d->l).total;
+    return RSVD_OK;
+}
+
+int rsvd_run(rsvd_handle_t h, const rsvd_desc_t* d, const void* A, const void* omega, int64_t ldo, void* U,
+             int64_t ldu, void* S, void* V, int64_t ldv) {
+    if (!h) return RSVD_ERR_INVALID_ARG;
+    RSVD_TRY(check_desc(h, d));
+    if (!A || !U || !S || !V || ldu < d->m || ldv < d->n || (omega && ldo < d->n)) {
+        h->err = "null pointer or bad leading dimension";
+        return RSVD_ERR_INVALID_ARG;
+    }
+    RSVD_TRY(set_device(h));
+    if (d->dtype == RSVD_F64) return run_typed<double>(h, d, A, omega, ldo, U, ldu, S, V, ldv, nullptr, 0);
+    return run_typed<float>(h, d, A, omega, ldo, U, ldu, S, V, ldv, nullptr, 0);
+}
+
+int rsvd_range_finder(rsvd_handle_t h, const rsvd_desc_t* d, const void* A, const void* omega, int64_t ldo, void* Q,
+                      int64_t ldq) {
+    if (!h) return RSVD_ERR_INVALID_ARG;
+    RSVD_TRY(check_desc(h, d));
+    if (!A || !Q || ldq < d->m) {
+        h->err = "null pointer or bad leading dimension";
+        return RSVD_ERR_INVALID_ARG;
+    }
+    RSVD_TRY(set_device(h));
+    if (d->dtype == RSVD_F64) return run_typed<double>(h, d, A, omega, ldo, nullptr, 0, nullptr, nullptr, 0, Q, ldq);
+    return run_typed<float>(h, d, A, omega, ldo, nullptr, 0, nullptr, nullptr, 0, Q, ldq);
+}
+
+int rsvd_generate_omega(rsvd_handle_t h, int64_t n, int32_t l, uint64_t seed, int32_t dtype, void* omega) {
+    if (!h || n <= 0 || l <= 0 || !omega) return RSVD_ERR_INVALID_ARG;
+    RSVD_TRY(set_device(h));
+    // Generate the row-major panel in the workspace, then write it out column-major:
+    // Omega(i, j) is stream element i + n*j in both layouts.
+    const int LP = lp_of(l);
+    size_t bytes = (size_t)n * LP * (dtype == RSVD_F64 ? 8 : 4);
+    RSVD_TRY(ensure_ws(h, bytes));
+    if (dtype == RSVD_F64) {
+        RSVD_CK(launch_philox_omega<double>(reinterpret_cast<double*>(h->ws), n, l, LP, seed, h->stream));
+        RSVD_CK(launch_panel_to_colmajor<double>(reinterpret_cast<double*>(h->ws), n, l, LP,
+                                                 reinterpret_cast<double*>(omega), n, h->stream));
+    } else if (dtype == RSVD_F32) {
+        RSVD_CK(launch_philox_omega<float>(reinterpret_cast<float*>(h->ws), n, l, LP, seed, h->stream));
+        RSVD_CK(launch_panel_to_colmajor<float>(reinterpret_cast<float*>(h->ws), n, l, LP,
+                                                reinterpret_cast<float*>(omega), n, h->stream));
+    } else {
+        return RSVD_ERR_UNSUPPORTED;
+    }
+    return RSVD_OK;
+}
+
+// ---- host fp64 variants ----------------------------------------------------------------------
+namespace {
+struct DevBuf {
+    void* p = nullptr;
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+};
+}  // namespace
+
+int rsvd_run_host_f64(rsvd_handle_t h, int64_t m, int64_t n, const double* A, int64_t lda, int32_t l, int32_t q,
+                      int32_t method, const double* omega, uint64_t seed, double* U, double* S, double* V) {
+    if (!h || !A || !U || !S || !V) return RSVD_ERR_INVALID_ARG;
+    rsvd_desc_t d{};
+    d.m = m; d.n = n; d.lda = m; d.l = l; d.q = q; d.dtype = RSVD_F64; d.method = method;
+    d.qr_mode = RSVD_QR_AUTO; d.seed = seed;
+    RSVD_TRY(check_desc(h, &d));
+    if (lda < m) return RSVD_ERR_INVALID_ARG;
+    RSVD_TRY(set_device(h));
+    const int64_t dd = std::min<int64_t>(l, n);
+    DevBuf dA, dO, dU, dS, dV;
+    RSVD_CK(hipMalloc(&dA.p, sizeof(double) * m * n));
+    RSVD_CK(hipMalloc(&dU.p, sizeof(double) * m * dd));
+    RSVD_CK(hipMalloc(&dS.p, sizeof(double) * dd));
+    RSVD_CK(hipMalloc(&dV.p, sizeof(double) * n * dd));
+    RSVD_CK(hipMemcpy2DAsync(dA.p, sizeof(double) * m, A, sizeof(double) * lda, sizeof(double) * m, n,
+                             hipMemcpyHostToDevice, h->stream));
+    if (omega) {
+        RSVD_CK(hipMalloc(&dO.p, sizeof(double) * n * l));
+        RSVD_CK(hipMemcpyAsync(dO.p, omega, sizeof(double) * n * l, hipMemcpyHostToDevice, h->stream));
+    }
+    RSVD_TRY(rsvd_run(h, &d, dA.p, dO.p, n, dU.p, m, dS.p, dV.p, n));
+    RSVD_CK(hipMemcpyAsync(U, dU.p, sizeof(double) * m * dd, hipMemcpyDeviceToHost, h->stream));
+    RSVD_CK(hipMemcpyAsync(S, dS.p, sizeof(double) * dd, hipMemcpyDeviceToHost, h->stream));
+    RSVD_CK(hipMemcpyAsync(V, dV.p, sizeof(double) * n * dd, hipMemcpyDeviceToHost, h->stream));
+    RSVD_CK(hipStreamSynchronize(h->stream));
+    return RSVD_OK;
+}
+
+int rsvd_range_finder_host_f64(rsvd_handle_t h, int64_t m, int64_t n, const double* A, int64_t lda,
+                               const double* omega, int32_t l, int32_t q, double* Q) {
+    if (!h || !A || !Q || !omega) return RSVD_ERR_INVALID_ARG;
+    rsvd_desc_t d{};
+    d.m = m; d.n = n; d.lda = m; d.l = l; d.q = q; d.dtype = RSVD_F64; d.method = RSVD_SVD_JACOBI;
+    RSVD_TRY(check_desc(h, &d));
+    if (lda < m) return RSVD_ERR_INVALID_ARG;
+    RSVD_TRY(set_device(h));
+    DevBuf dA, dO, dQ;
+    RSVD_CK(hipMalloc(&dA.p, sizeof(double) * m * n));
+    RSVD_CK(hipMalloc(&dO.p, sizeof(double) * n * l));
+    RSVD_CK(hipMalloc(&dQ.p, sizeof(double) * m * l));
+    RSVD_CK(hipMemcpy2DAsync(dA.p, sizeof(double) * m, A, sizeof(double) * lda, sizeof(double) * m, n,
+                             hipMemcpyHostToDevice, h->stream));
+    RSVD_CK(hipMemcpyAsync(dO.p, omega, sizeof(double) * n * l, hipMemcpyHostToDevice, h->stream));
+    RSVD_TRY(rsvd_range_finder(h, &d, dA.p, dO.p, n, dQ.p, m));
+    RSVD_CK(hipMemcpyAsync(Q, dQ.p, sizeof(double) * m * l, hipMemcpyDeviceToHost, h->stream));
+    RSVD_CK(hipStreamSynchronize(h->stream));
+    return RSVD_OK;
+}
+
+int rsvd_generate_omega_host_f64(rsvd_handle_t h, int64_t n, int32_t l, uint64_t seed, double* omega) {
+    if (!h || !omega || n <= 0 || l <= 0) return RSVD_ERR_INVALID_ARG;
+    RSVD_TRY(set_device(h));
+    DevBuf dO;
+    RSVD_CK(hipMalloc(&dO.p, sizeof(double) * n * l));
+    RSVD_TRY(rsvd_generate_omega(h, n, l, seed, RSVD_F64, dO.p));
+    RSVD_CK(hipMemcpyAsync(omega, dO.p, sizeof(double) * n * l, hipMemcpyDeviceToHost, h->stream));
+    RSVD_CK(hipStreamSynchronize(h->stream));
+    return RSVD_OK;
+}
+
+}  // extern "C"

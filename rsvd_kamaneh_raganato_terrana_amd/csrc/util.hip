@@ -1,0 +1,144 @@
+// util.hip -- Omega generation, panel layout conversions, slab reduction.
+//
+// Omega: the reference draws an n x l Gaussian from std::mt19937(random_device()+rank)
+// (src/rSVD.cpp:26-37) and ships it with MPI_Gatherv + MPI_Bcast (:49,52).  Here every GPU
+// regenerates the identical matrix from a counter-based Philox4x32-10 stream keyed by the
+// seed, so Omega needs no communication and the CPU oracle (oracle/rsvd_oracle.c,
+// orc_philox_gaussian) can draw the same numbers.  Element (i, j) is stream element i + n*j.
+#include "common.hpp"
+#include "kernels.hpp"
+
+namespace rsvd {
+
+namespace {
+
+__device__ __forceinline__ void philox4x32_10(uint64_t ctr, uint64_t seed, uint32_t out[4]) {
+    uint32_t c0 = (uint32_t)ctr, c1 = (uint32_t)(ctr >> 32), c2 = 0x52535644u, c3 = 0u;
+    uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
+        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+        const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+__device__ __forceinline__ double gauss_elem(uint64_t e, uint64_t seed) {
+    uint32_t x[4];
+    philox4x32_10(e >> 1, seed, x);
+    const double two_m53 = 1.1102230246251565404e-16;
+    const double u1 = ((double)(((uint64_t)(x[0] >> 5) << 26) | (x[1] >> 6)) + 0.5) * two_m53;
+    const double u2 = ((double)(((uint64_t)(x[2] >> 5) << 26) | (x[3] >> 6)) + 0.5) * two_m53;
+    const double rr = sqrt(-2.0 * log(u1));
+    const double th = 6.283185307179586476925286766559 * u2;
+    return (e & 1) ? rr * sin(th) : rr * cos(th);
+}
+
+template <typename T>
+__global__ void philox_omega_kernel(T* __restrict__ out, int64_t n, int l, int LP, uint64_t seed) {
+    const int64_t total = n * LP;
+    for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
+         idx += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = idx / LP;
+        const int j = (int)(idx - i * LP);
+        out[idx] = (j < l) ? (T)gauss_elem((uint64_t)(i + n * (int64_t)j), seed) : T(0);
+    }
+}
+
+template <typename T>
+__global__ void colmajor_to_panel_kernel(const T* __restrict__ in, int64_t ld, int64_t m, int l, int LP,
+                                         T* __restrict__ out) {
+    const int64_t total = m * LP;
+    for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
+         idx += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = idx / LP;
+        const int j = (int)(idx - i * LP);
+        out[idx] = (j < l) ? in[i + (int64_t)j * ld] : T(0);
+    }
+}
+
+template <typename T>
+__global__ void panel_to_colmajor_kernel(const T* __restrict__ in, int64_t m, int cols, int LP,
+                                         T* __restrict__ out, int64_t ld) {
+    const int64_t total = m * cols;
+    for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
+         idx += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t j = idx / m;
+        const int64_t i = idx - j * m;
+        out[i + j * ld] = in[i * LP + j];
+    }
+}
+
+template <typename T>
+__global__ void sum_slabs_kernel(const T* __restrict__ slabs, int64_t stride, int nslab, int64_t count,
+                                 T* __restrict__ out) {
+    typedef typename Vec16<T>::type V;
+    constexpr int VW = Vec16<T>::N;
+    const int64_t nv = count / VW;
+    for (int64_t v = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; v < nv;
+         v += (int64_t)gridDim.x * blockDim.x) {
+        V acc = *reinterpret_cast<const V*>(slabs + v * VW);
+        T* a = reinterpret_cast<T*>(&acc);
+        for (int s = 1; s < nslab; ++s) {
+            const V o = *reinterpret_cast<const V*>(slabs + s * stride + v * VW);
+            const T* b = reinterpret_cast<const T*>(&o);
+#pragma unroll
+            for (int t = 0; t < VW; ++t) a[t] += b[t];
+        }
+        *reinterpret_cast<V*>(out + v * VW) = acc;
+    }
+}
+
+inline int grid_for(int64_t work, int block) {
+    int64_t g = (work + block - 1) / block;
+    if (g > 4096) g = 4096;
+    if (g < 1) g = 1;
+    return (int)g;
+}
+
+}  // namespace
+
+template <typename T>
+hipError_t launch_philox_omega(T* out, int64_t n, int l, int LP, uint64_t seed, hipStream_t s) {
+    hipLaunchKernelGGL((philox_omega_kernel<T>), dim3(grid_for(n * LP, 256)), dim3(256), 0, s, out, n, l, LP,
+                       seed);
+    return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_colmajor_to_panel(const T* in, int64_t ld, int64_t m, int l, int LP, T* out, hipStream_t s) {
+    hipLaunchKernelGGL((colmajor_to_panel_kernel<T>), dim3(grid_for(m * LP, 256)), dim3(256), 0, s, in, ld, m,
+                       l, LP, out);
+    return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_panel_to_colmajor(const T* in, int64_t m, int cols, int LP, T* out, int64_t ld, hipStream_t s) {
+    hipLaunchKernelGGL((panel_to_colmajor_kernel<T>), dim3(grid_for(m * cols, 256)), dim3(256), 0, s, in, m,
+                       cols, LP, out, ld);
+    return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_sum_slabs(const T* slabs, int64_t slab_stride, int nslab, int64_t count, T* out,
+                            hipStream_t s) {
+    // count and slab_stride are multiples of LP (>= 16) -> multiples of the 16-B vector width.
+    hipLaunchKernelGGL((sum_slabs_kernel<T>), dim3(grid_for(count / Vec16<T>::N, 256)), dim3(256), 0, s, slabs,
+                       slab_stride, nslab, count, out);
+    return hipGetLastError();
+}
+
+#define RSVD_INST(T)                                                                                    \
+    template hipError_t launch_philox_omega<T>(T*, int64_t, int, int, uint64_t, hipStream_t);           \
+    template hipError_t launch_colmajor_to_panel<T>(const T*, int64_t, int64_t, int, int, T*, hipStream_t); \
+    template hipError_t launch_panel_to_colmajor<T>(const T*, int64_t, int, int, T*, int64_t, hipStream_t); \
+    template hipError_t launch_sum_slabs<T>(const T*, int64_t, int, int64_t, T*, hipStream_t);
+RSVD_INST(float)
+RSVD_INST(double)
+#undef RSVD_INST
+
+}  // namespace rsvd
