@@ -100,6 +100,15 @@ int64_t rsvd_row_partition(int64_t rows, int world, int rank, int64_t *offset);
 
 /* Device workspace bytes rsvd_run needs for `desc` (allocated lazily by the handle). */
 int rsvd_workspace_bytes(const rsvd_desc_t *desc, size_t *bytes);
+/* Timing mode (benchmarking): hipEvent pairs bracket every projection GEMM kernel launch
+ * (A*X and A^T*Q; not their slab reductions).  rsvd_set_timing resets the accumulators;
+ * rsvd_get_timing synchronises the stream and returns totals since the reset. */
+typedef struct {
+    int32_t nn_launches, tn_launches;
+    double nn_ms, tn_ms;
+} rsvd_timing_t;
+int rsvd_set_timing(rsvd_handle_t h, int enable);
+int rsvd_get_timing(rsvd_handle_t h, rsvd_timing_t *t);
 /* Use caller-owned device memory as the workspace (NULL reverts to handle-owned memory). */
 int rsvd_set_workspace(rsvd_handle_t h, void *ptr, size_t bytes);
 

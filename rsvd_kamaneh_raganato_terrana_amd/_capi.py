@@ -34,7 +34,7 @@ QR_AUTO, QR_HOUSEHOLDER, QR_CHOLQR2 = 0, 1, 2
 EXPORTS = (
     "rsvd_status_string", "rsvd_abi_version", "rsvd_create", "rsvd_destroy", "rsvd_set_stream",
     "rsvd_last_error", "rsvd_get_info", "rsvd_set_comm", "rsvd_row_partition",
-    "rsvd_workspace_bytes", "rsvd_set_workspace", "rsvd_run", "rsvd_range_finder",
+    "rsvd_workspace_bytes", "rsvd_set_workspace", "rsvd_set_timing", "rsvd_get_timing", "rsvd_run", "rsvd_range_finder",
     "rsvd_generate_omega", "rsvd_run_host_f64", "rsvd_range_finder_host_f64",
     "rsvd_generate_omega_host_f64",
 )
@@ -56,12 +56,30 @@ class Info(ctypes.Structure):
     ]
 
 
+class Timing(ctypes.Structure):
+    _fields_ = [
+        ("nn_launches", ctypes.c_int32), ("tn_launches", ctypes.c_int32),
+        ("nn_ms", ctypes.c_double), ("tn_ms", ctypes.c_double),
+    ]
+
+
 ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
                                 ctypes.c_void_p, ctypes.c_void_p)
 
 
+def _up_to_date() -> bool:
+    if not os.path.exists(LIB_PATH):
+        return False
+    t = os.path.getmtime(LIB_PATH)
+    srcs = [os.path.join(CSRC, f) for f in os.listdir(CSRC)]
+    srcs.append(os.path.join(REPO, "include", "rsvd_c.h"))
+    return all(os.path.getmtime(p) <= t for p in srcs if os.path.isfile(p))
+
+
 def build(jobs: int = 8, force: bool = False) -> str:
     """Compile librsvd_hip.so for gfx950 with hipcc (cross-compiles without a GPU)."""
+    if not force and _up_to_date():
+        return LIB_PATH
     cmd = ["make", "-C", CSRC, f"-j{jobs}"]
     if force:
         subprocess.run(["make", "-C", CSRC, "clean"], check=True, capture_output=True)
@@ -95,6 +113,8 @@ def lib():
     L.rsvd_row_partition.argtypes = [i64, ctypes.c_int, ctypes.c_int, ctypes.POINTER(i64)]
     L.rsvd_workspace_bytes.argtypes = [ctypes.POINTER(Desc), ctypes.POINTER(ctypes.c_size_t)]
     L.rsvd_set_workspace.argtypes = [vp, vp, ctypes.c_size_t]
+    L.rsvd_set_timing.argtypes = [vp, ctypes.c_int]
+    L.rsvd_get_timing.argtypes = [vp, ctypes.POINTER(Timing)]
     L.rsvd_run.argtypes = [vp, ctypes.POINTER(Desc), vp, vp, i64, vp, i64, vp, vp, i64]
     L.rsvd_range_finder.argtypes = [vp, ctypes.POINTER(Desc), vp, vp, i64, vp, i64]
     L.rsvd_generate_omega.argtypes = [vp, i64, i32, u64, i32, vp]

@@ -23,7 +23,7 @@ from typing import Optional
 import numpy as np
 
 from . import _capi
-from ._capi import Desc, Info, check, lib
+from ._capi import Desc, Info, Timing, check, lib
 
 
 class SVDMethod(enum.IntEnum):
@@ -93,12 +93,16 @@ class Engine:
 
     def reserve(self, desc: Desc):
         """Allocate the workspace from torch's allocator (outside any timed region)."""
-        torch = _torch()
         nbytes = ctypes.c_size_t(0)
         check(lib().rsvd_workspace_bytes(ctypes.byref(desc), ctypes.byref(nbytes)))
-        if self._ws is None or self._ws.numel() < nbytes.value:
-            self._ws = torch.empty(nbytes.value, dtype=torch.uint8, device=f"cuda:{self.device}")
-            check(lib().rsvd_set_workspace(self.h, ctypes.c_void_p(self._ws.data_ptr()), nbytes.value), self.h)
+        return self._reserve_bytes(nbytes.value)
+
+    def _reserve_bytes(self, nbytes: int):
+        torch = _torch()
+        if self._ws is None or self._ws.numel() < nbytes:
+            self._ws = None
+            self._ws = torch.empty(nbytes, dtype=torch.uint8, device=f"cuda:{self.device}")
+            check(lib().rsvd_set_workspace(self.h, ctypes.c_void_p(self._ws.data_ptr()), nbytes), self.h)
         return self._ws
 
     def set_comm(self, rank: int, world: int, group=None):
@@ -125,6 +129,15 @@ class Engine:
 
         self._hook = _capi.ALLREDUCE_FN(_hook)
         check(lib().rsvd_set_comm(self.h, rank, world, self._hook, None), self.h)
+
+    def set_timing(self, enable: bool = True):
+        """hipEvent timing of every projection GEMM launch (benchmarking only)."""
+        check(lib().rsvd_set_timing(self.h, int(enable)), self.h)
+
+    def timing(self) -> dict:
+        t = Timing()
+        check(lib().rsvd_get_timing(self.h, ctypes.byref(t)), self.h)
+        return {k: getattr(t, k) for k, _ in Timing._fields_}
 
     def info(self) -> dict:
         inf = Info()
@@ -187,6 +200,7 @@ class Engine:
     def generate_omega(self, n: int, l: int, seed: int = 0, dtype=None):
         torch = _torch()
         dtype = dtype or torch.float64
+        self._reserve_bytes(n * ((l + 15) // 16 * 16) * 8)
         self._bind_stream()
         Om = empty_colmajor(n, l, dtype, f"cuda:{self.device}")
         check(lib().rsvd_generate_omega(self.h, n, l, seed, _capi.F64 if dtype == torch.float64 else _capi.F32,
@@ -203,6 +217,8 @@ class Engine:
         S = np.zeros(dd)
         V = np.zeros((n, dd), order="F")
         om = None if omega is None else np.asfortranarray(omega, dtype=np.float64)
+        self.reserve(Desc(m=m, n=n, lda=m, l=l, q=q, dtype=_capi.F64, method=int(method)))
+        self._bind_stream()
         check(lib().rsvd_run_host_f64(self.h, m, n, _dp(A), m, l, q, int(method),
                                       _dp(om) if om is not None else None, seed, _dp(U), _dp(S), _dp(V)),
               self.h)
@@ -214,11 +230,15 @@ class Engine:
         m, n = A.shape
         l = om.shape[1]
         Q = np.zeros((m, l), order="F")
+        self.reserve(Desc(m=m, n=n, lda=m, l=l, q=q, dtype=_capi.F64))
+        self._bind_stream()
         check(lib().rsvd_range_finder_host_f64(self.h, m, n, _dp(A), m, _dp(om), l, q, _dp(Q)), self.h)
         return Q
 
     def generate_omega_host(self, n: int, l: int, seed: int = 0) -> np.ndarray:
         om = np.zeros((n, l), order="F")
+        self._reserve_bytes(n * ((l + 15) // 16 * 16) * 8)
+        self._bind_stream()
         check(lib().rsvd_generate_omega_host_f64(self.h, n, l, seed, _dp(om)), self.h)
         return om
 

@@ -42,6 +42,13 @@ struct rsvd_handle_s {
     int rank = 0, world = 1;
     rsvd_allreduce_fn allreduce = nullptr;
     void* ar_user = nullptr;
+    // timing mode: hipEvent pairs around every projection kernel (kind 0 = A*X, 1 = A^T*Q)
+    bool timing = false;
+    std::vector<hipEvent_t> ev_pool;
+    std::vector<std::pair<int, int>> ev_used;  // (kind, first event index)
+    size_t ev_next = 0;
+    double acc_ms[2] = {0.0, 0.0};
+    int acc_n[2] = {0, 0};
 };
 
 namespace {
@@ -70,7 +77,7 @@ struct Layout {
     int l, LP;
     ProjPlan pnn, ptn;
     int gram_m, gram_n;
-    size_t off_Xn, off_Zn, off_Ym, off_Qm, off_T1, off_slab, off_gram, off_small, total;
+    size_t off_Xn, off_Zn, off_Ym, off_Qm, off_T1, off_slab, off_gram, off_small, off_ctr, total;
 
     Layout(int64_t m_, int64_t n_, int l_) : m(m_), n(n_), l(l_), LP(lp_of(l_)) {
         pnn = plan_proj_nn<T>(m, n, LP);
@@ -87,8 +94,9 @@ struct Layout {
         const int64_t slab_elems = std::max<int64_t>(pnn.splits > 1 ? pnn.splits * m : 0,
                                                      ptn.splits > 1 ? ptn.splits * n : 0);
         off_slab = o; o = align256(o + sizeof(T) * std::max<int64_t>(slab_elems, 1) * LP);
-        off_gram = o; o = align256(o + sizeof(double) * 64 * LP * LP);
+        off_gram = o; o = align256(o + sizeof(double) * 33 * LP * LP);  // <= 32 Gram slabs + reduced tiles
         off_small = o; o = align256(o + sizeof(double) * 8 * LP * LP);  // R1, R2, Rinv, Uw, Vw, Gsum
+        off_ctr = o; o = align256(o + 64 * sizeof(unsigned));           // arrival counters
         total = o;
     }
 };
@@ -134,6 +142,11 @@ struct Engine {
     hipStream_t s;
     T *Xn, *Zn, *Ym, *Qm, *T1, *slab;
     double *gram, *R1, *R2, *Rinv, *Uw, *Vw, *Gsum;
+    unsigned* ctr;
+    unsigned tgt0 = 0, tgt1 = 0;  // run-cumulative arrival targets of gram_chol (counters zeroed per run)
+    // fp32 panels that only carry a subspace (power-iteration intermediates) get one CholeskyQR
+    // pass; panels whose basis is an output (final Q, Q_B) and every fp64 panel get two.
+    int inter_passes = sizeof(T) == 4 ? 1 : 2;
 
     Engine(rsvd_handle_t h_, const Layout<T>& L_) : h(h_), L(L_), s(h_->stream) {
         char* b = h->ws;
@@ -147,6 +160,7 @@ struct Engine {
         double* sm = reinterpret_cast<double*>(b + L.off_small);
         const int64_t q2 = (int64_t)L.LP * L.LP;
         R1 = sm; R2 = sm + q2; Rinv = sm + 2 * q2; Uw = sm + 3 * q2; Vw = sm + 4 * q2; Gsum = sm + 5 * q2;
+        ctr = reinterpret_cast<unsigned*>(b + L.off_ctr);
     }
 
     int allreduce(void* buf, int64_t count, int32_t dtype) {
@@ -158,36 +172,88 @@ struct Engine {
         return RSVD_OK;
     }
 
-    // One CholeskyQR pass: R = chol(P^T P) (summed over ranks when `sharded`), Out = P R^-1.
-    int cholqr_pass(const T* P, int64_t rows, T* Out, double* Rdst, double* Racc, int accumulate, bool sharded) {
+    // Per-orth breakdown flags live at dflags[4 + k] (k = orth index within the run, < 12).
+    int orth_index = 0;
+    int* cur_flag = nullptr;
+
+    // One CholeskyQR pass: R = chol(P^T P) (Gram summed over ranks when `sharded`), Out = P R^-1.
+    // The factorisation runs in fp32 on the fp32 path (see qr.hip), in fp64 on the fp64 path.
+    int cholqr_pass(const T* P, int64_t rows, T* Out, bool sharded) {
         const int nb = plan_gram_blocks(rows);
-        RSVD_CK(launch_gram_partial<T>(P, rows, L.LP, nb, gram, s));
-        const double* gsrc = gram;
-        int nsl = nb;
+        double* tiles = gram + 32 * (size_t)L.LP * L.LP;
+        const int f32 = sizeof(T) == 4;
+        tgt0 += nb;
+        tgt1 += gram_tiles(L.LP, 0);
         if (sharded && h->world > 1) {
-            RSVD_CK(launch_sum_slabs<double>(gram, (int64_t)L.LP * L.LP, nb, (int64_t)L.LP * L.LP, Gsum, s));
+            RSVD_CK(launch_gram_chol<T>(P, rows, L.LP, nb, gram, tiles, ctr, tgt0, tgt1, 0, f32, Gsum, L.l, nullptr,
+                                        nullptr, cur_flag, s));
             RSVD_TRY(allreduce(Gsum, (int64_t)L.LP * L.LP, RSVD_F64));
-            gsrc = Gsum;
-            nsl = 1;
+            RSVD_CK(launch_chol(Gsum, L.l, L.LP, f32, R1, Rinv, cur_flag, s));
+        } else {
+            RSVD_CK(launch_gram_chol<T>(P, rows, L.LP, nb, gram, tiles, ctr, tgt0, tgt1, 1, f32, nullptr, L.l, R1, Rinv,
+                                        cur_flag, s));
         }
-        RSVD_CK(launch_chol_inv(gsrc, nsl, L.l, L.LP, Rdst, Rinv, Racc, accumulate, h->dflags, s));
         RSVD_CK(launch_panel_small<T>(P, rows, L.LP, Rinv, Out, 0, 0, 0, s));
         return RSVD_OK;
     }
 
-    // CholeskyQR2: Q = orth(P); R1 <- R2 * R1 (the panel's R) when want_r.
-    int orth(const T* P, int64_t rows, T* Q, bool sharded) {
-        RSVD_TRY(cholqr_pass(P, rows, T1, R1, nullptr, 0, sharded));
-        RSVD_TRY(cholqr_pass(T1, rows, Q, R2, R1, 1, sharded));
+    // CholeskyQR (passes = 1) or CholeskyQR2 (passes = 2): Q = orth(P).  If any pass flags a bad
+    // pivot, the predicated fallback rebuilds Q from P (CGS2 + random completion, util.hip).
+    int orth(const T* P, int64_t rows, T* Q, bool sharded, int passes) {
+        cur_flag = h->dflags + 4 + (orth_index < 12 ? orth_index : 11);
+        ++orth_index;
+        if (passes <= 1) {
+            RSVD_TRY(cholqr_pass(P, rows, Q, sharded));
+        } else {
+            RSVD_TRY(cholqr_pass(P, rows, T1, sharded));
+            RSVD_TRY(cholqr_pass(T1, rows, Q, sharded));
+        }
+        if (!(sharded && h->world > 1)) {  // the sharded fallback is not implemented: the flag reports it
+            RSVD_CK(launch_robust_orth<T>(P, rows, L.l, L.LP, Q, cur_flag, 0x5EEDull + orth_index, s));
+        }
+        return RSVD_OK;
+    }
+
+    // Gout = P^T P2 (fp64), e.g. R = Q_B^T B^T for the small SVD.
+    int cross_gram(const T* P, const T* P2, int64_t rows, double* Gout) {
+        const int nb = plan_gram_blocks(rows);
+        double* tiles = gram + 32 * (size_t)L.LP * L.LP;
+        tgt0 += nb;
+        tgt1 += gram_tiles(L.LP, 1);
+        RSVD_CK(launch_cross_gram<T>(P, P2, rows, L.LP, nb, gram, tiles, ctr, tgt0, tgt1, Gout, L.l, h->dflags, s));
+        return RSVD_OK;
+    }
+
+    // Timing mode: bracket the projection GEMM kernel (not its slab reduction) with events.
+    int ev_begin(int kind, int& idx) {
+        idx = -1;
+        if (!h->timing) return RSVD_OK;
+        while (h->ev_pool.size() < h->ev_next + 2) {
+            hipEvent_t e;
+            RSVD_CK(hipEventCreate(&e));
+            h->ev_pool.push_back(e);
+        }
+        idx = (int)h->ev_next;
+        h->ev_next += 2;
+        h->ev_used.push_back({kind, idx});
+        RSVD_CK(hipEventRecord(h->ev_pool[idx], s));
+        return RSVD_OK;
+    }
+    int ev_end(int idx) {
+        if (idx >= 0) RSVD_CK(hipEventRecord(h->ev_pool[idx + 1], s));
         return RSVD_OK;
     }
 
     int proj_nn(const T* A, int64_t lda, const T* X, T* Y) {
-        RSVD_CK(launch_proj_nn<T>(A, lda, L.m, L.n, X, L.LP, L.pnn, slab, Y, s));
+        int ev;
+        RSVD_TRY(ev_begin(0, ev));
+        RSVD_CK(launch_proj_nn<T>(A, lda, L.m, L.n, X, L.LP, L.pnn, slab, Y, s, ev >= 0 ? h->ev_pool[ev + 1] : nullptr));
         return RSVD_OK;
     }
     int proj_tn(const T* A, int64_t lda, const T* Q, T* Z) {
-        RSVD_CK(launch_proj_tn<T>(A, lda, L.m, L.n, Q, L.LP, L.ptn, slab, Z, s));
+        int ev;
+        RSVD_TRY(ev_begin(1, ev));
+        RSVD_CK(launch_proj_tn<T>(A, lda, L.m, L.n, Q, L.LP, L.ptn, slab, Z, s, ev >= 0 ? h->ev_pool[ev + 1] : nullptr));
         // Z = sum_g A_g^T Q_g over the row shards
         return allreduce(Z, L.n * L.LP, sizeof(T) == 8 ? RSVD_F64 : RSVD_F32);
     }
@@ -204,12 +270,12 @@ struct Engine {
     // intermediate_step (src/rSVD.cpp:57-70): leaves Q (m x LP panel) in Qm.
     int range_finder(const T* A, int64_t lda, int q) {
         RSVD_TRY(proj_nn(A, lda, Xn, Ym));
-        RSVD_TRY(orth(Ym, L.m, Qm, true));
+        RSVD_TRY(orth(Ym, L.m, Qm, true, q == 0 ? 2 : inter_passes));
         for (int i = 0; i < q; ++i) {
             RSVD_TRY(proj_tn(A, lda, Qm, Zn));
-            RSVD_TRY(orth(Zn, L.n, Xn, false));
+            RSVD_TRY(orth(Zn, L.n, Xn, false, inter_passes));
             RSVD_TRY(proj_nn(A, lda, Xn, Ym));
-            RSVD_TRY(orth(Ym, L.m, Qm, true));
+            RSVD_TRY(orth(Ym, L.m, Qm, true, i == q - 1 ? 2 : inter_passes));
         }
         return RSVD_OK;
     }
@@ -218,7 +284,8 @@ struct Engine {
         RSVD_TRY(range_finder(A, d->lda, d->q));
         // Stage B: B^T = A^T Q, QR-preconditioned as in SVD_class.hpp:116-123.
         RSVD_TRY(proj_tn(A, d->lda, Qm, Zn));
-        RSVD_TRY(orth(Zn, L.n, Xn, false));  // Xn = Q_B, R1 = R
+        RSVD_TRY(orth(Zn, L.n, Xn, false, 2));  // Xn = Q_B
+        RSVD_TRY(cross_gram(Xn, Zn, L.n, R1));    // R = Q_B^T B^T exactly (fp64), W = R^T
         RSVD_CK(launch_small_svd<T>(R1, L.l, L.LP, Uw, Vw, S, h->dflags + 1, s));
         const int dcols = L.l;  // d = min(l, n) = l (l <= n enforced)
         RSVD_CK(launch_panel_small<T>(Qm, L.m, L.LP, Uw, reinterpret_cast<T*>(U), 1, dcols, ldu, s));
@@ -232,7 +299,8 @@ int run_typed(rsvd_handle_t h, const rsvd_desc_t* d, const void* A, const void* 
               int64_t ldu, void* S, void* V, int64_t ldv, void* Qout, int64_t ldq) {
     Layout<T> L(d->m, d->n, d->l);
     RSVD_TRY(ensure_ws(h, L.total));
-    RSVD_CK(hipMemsetAsync(h->dflags, 0, 4 * sizeof(int), h->stream));
+    RSVD_CK(hipMemsetAsync(h->dflags, 0, 16 * sizeof(int), h->stream));
+    RSVD_CK(hipMemsetAsync(h->ws + L.off_ctr, 0, 64 * sizeof(unsigned), h->stream));
     h->info.splits_nn = L.pnn.splits;
     h->info.splits_tn = L.ptn.splits;
     Engine<T> E(h, L);
@@ -308,6 +376,7 @@ int rsvd_destroy(rsvd_handle_t h) {
     if (h->stream) (void)hipStreamSynchronize(h->stream);
     if (h->ws && !h->ws_external) (void)hipFree(h->ws);
     if (h->dflags) (void)hipFree(h->dflags);
+    for (auto e : h->ev_pool) (void)hipEventDestroy(e);
     if (h->own_stream && h->stream) (void)hipStreamDestroy(h->stream);
     delete h;
     return RSVD_OK;
@@ -329,12 +398,49 @@ const char* rsvd_last_error(rsvd_handle_t h) { return h ? h->err.c_str() : "null
 int rsvd_get_info(rsvd_handle_t h, rsvd_info_t* info) {
     if (!h || !info) return RSVD_ERR_INVALID_ARG;
     RSVD_TRY(set_device(h));
-    int flags[2] = {0, 0};
-    RSVD_CK(hipMemcpyAsync(flags, h->dflags, 2 * sizeof(int), hipMemcpyDeviceToHost, h->stream));
+    int flags[16] = {0};
+    RSVD_CK(hipMemcpyAsync(flags, h->dflags, 16 * sizeof(int), hipMemcpyDeviceToHost, h->stream));
     RSVD_CK(hipStreamSynchronize(h->stream));
-    h->info.cholqr_fallbacks = flags[0];
+    if (flags[2]) {
+        h->err = "a Gram reduction timed out waiting for its producers";
+        return RSVD_ERR_HIP;
+    }
+    int fallbacks = 0;
+    for (int k = 4; k < 16; ++k) fallbacks += flags[k] != 0;
+    h->info.cholqr_fallbacks = fallbacks;
     h->info.jacobi_sweeps = flags[1];
     *info = h->info;
+    return RSVD_OK;
+}
+
+int rsvd_set_timing(rsvd_handle_t h, int enable) {
+    if (!h) return RSVD_ERR_INVALID_ARG;
+    RSVD_TRY(set_device(h));
+    RSVD_CK(hipStreamSynchronize(h->stream));
+    h->timing = enable != 0;
+    h->ev_used.clear();
+    h->ev_next = 0;
+    h->acc_ms[0] = h->acc_ms[1] = 0.0;
+    h->acc_n[0] = h->acc_n[1] = 0;
+    return RSVD_OK;
+}
+
+int rsvd_get_timing(rsvd_handle_t h, rsvd_timing_t* t) {
+    if (!h || !t) return RSVD_ERR_INVALID_ARG;
+    RSVD_TRY(set_device(h));
+    RSVD_CK(hipStreamSynchronize(h->stream));
+    for (auto& u : h->ev_used) {
+        float ms = 0.f;
+        RSVD_CK(hipEventElapsedTime(&ms, h->ev_pool[u.second], h->ev_pool[u.second + 1]));
+        h->acc_ms[u.first] += ms;
+        h->acc_n[u.first] += 1;
+    }
+    h->ev_used.clear();
+    h->ev_next = 0;
+    t->nn_launches = h->acc_n[0];
+    t->tn_launches = h->acc_n[1];
+    t->nn_ms = h->acc_ms[0];
+    t->tn_ms = h->acc_ms[1];
     return RSVD_OK;
 }
 

@@ -23,6 +23,12 @@ hipError_t launch_sum_slabs(const T* slabs, int64_t slab_stride, int nslab, int6
 template <typename T>
 hipError_t launch_panel_to_colmajor(const T* in, int64_t m, int cols, int LP, T* out, int64_t ld, hipStream_t s);
 
+// Fallback re-orthonormalisation of P into Q (CGS2 + deterministic random completion) when
+// *flag != 0; returns immediately otherwise.  One workgroup.
+template <typename T>
+hipError_t launch_robust_orth(const T* P, int64_t rows, int l, int LP, T* Q, const int* flag, uint64_t seed,
+                              hipStream_t s);
+
 // ---- proj.hip: the projections (MFMA) ----------------------------------------------------------
 struct ProjPlan {
     int splits;      // K-splits (slabs); 1 => written straight into the output panel
@@ -32,25 +38,37 @@ struct ProjPlan {
 // Y (m x LP panel) = A (m x n, col-major) * X (n x LP panel)        [src/rSVD.cpp:59,66]
 template <typename T>
 ProjPlan plan_proj_nn(int64_t m, int64_t n, int LP);
+// `done` (optional) is recorded right after the GEMM kernel, before the slab reduction.
 template <typename T>
 hipError_t launch_proj_nn(const T* A, int64_t lda, int64_t m, int64_t n, const T* X, int LP,
-                          const ProjPlan& p, T* slabs, T* Y, hipStream_t s);
+                          const ProjPlan& p, T* slabs, T* Y, hipStream_t s, hipEvent_t done = nullptr);
 // Z (n x LP panel) = A^T * Q (m x LP panel)                           [src/rSVD.cpp:63,89]
 template <typename T>
 ProjPlan plan_proj_tn(int64_t m, int64_t n, int LP);
 template <typename T>
 hipError_t launch_proj_tn(const T* A, int64_t lda, int64_t m, int64_t n, const T* Q, int LP,
-                          const ProjPlan& p, T* slabs, T* Z, hipStream_t s);
+                          const ProjPlan& p, T* slabs, T* Z, hipStream_t s, hipEvent_t done = nullptr);
 
-// ---- qr.hip: CholeskyQR2 with fp64 Gram / Cholesky ----------------------------------------------
-// Partial Gram slabs of the first l columns of a rows x LP panel; returns slab count via plan.
+// ---- qr.hip: CholeskyQR with fp64 Gram ----------------------------------------------------------
+// Workgroups for the partial Gram of a `rows`-row panel; Gram tiles (16x16) per slab.
 int plan_gram_blocks(int64_t rows);
+int gram_tiles(int LP, int cross);
+// One launch: partial Grams of P (rows x LP) -> nb slabs -> per-tile reductions (fixed order)
+// -> mode 1: R = chol(G) (upper, LP x LP zero-padded) and Rinv = R^-1, factored in fp32 when
+// compute_f32 else fp64; mode 0: the summed Gram to Gsum (distributed path).  flag[0] += 1 on a
+// bad pivot.  ctr[0..1] are run-cumulative arrival counters (zeroed per run): t0 = ctr[0] after
+// this launch's nb arrivals, t1 = ctr[1] after its tile reducers (gram_tiles(LP, 0)).
 template <typename T>
-hipError_t launch_gram_partial(const T* P, int64_t rows, int LP, int nblk, double* gslabs, hipStream_t s);
-// G = sum of slabs; R = chol(G) (upper, l x l, LP-padded);  Rinv = R^-1; Racc = R * Racc_in
-// (if accumulate).  Sets *flag |= 1 when a pivot is not safely positive (breakdown / rank loss).
-hipError_t launch_chol_inv(const double* gslabs, int nslab, int l, int LP, double* R, double* Rinv,
-                           double* Racc, int accumulate, int* flag, hipStream_t s);
+hipError_t launch_gram_chol(const T* P, int64_t rows, int LP, int nb, double* slabs, double* tiles, unsigned* ctr,
+                            unsigned t0, unsigned t1, int mode, int compute_f32, double* Gsum, int l, double* R,
+                            double* Rinv, int* flag, hipStream_t s);
+// Cross-Gram Gout = P^T P2 (LP x LP fp64, zero outside l x l); t1 advances by gram_tiles(LP, 1).
+template <typename T>
+hipError_t launch_cross_gram(const T* P, const T* P2, int64_t rows, int LP, int nb, double* slabs, double* tiles,
+                             unsigned* ctr, unsigned t0, unsigned t1, double* Gout, int l, int* flag, hipStream_t s);
+// Factor an already-summed Gram G (LP x LP) -- same outputs as mode 1 above.
+hipError_t launch_chol(const double* G, int l, int LP, int compute_f32, double* R, double* Rinv, int* flag,
+                       hipStream_t s);
 // Out (rows x LP) = In (rows x LP) * M (LP x LP, fp64, applied in T precision).
 // out_colmajor: write Out's first `cols` columns col-major with leading dim ld instead.
 template <typename T>

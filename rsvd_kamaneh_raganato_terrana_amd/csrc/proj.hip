@@ -231,7 +231,7 @@ ProjPlan make_plan(int64_t K, int blocks, int64_t kstep_wg) {
 
 template <typename T, int LP>
 hipError_t nn_dispatch(const T* A, int64_t lda, int64_t m, int64_t n, const T* X, const ProjPlan& p,
-                       T* slabs, T* Y, hipStream_t s) {
+                       T* slabs, T* Y, hipStream_t s, hipEvent_t done) {
     constexpr int VW = Vec16<T>::N;
     constexpr int WR = 16 * VW;
     const size_t lds = (size_t)kWaves * WR * LP * sizeof(T);
@@ -241,13 +241,14 @@ hipError_t nn_dispatch(const T* A, int64_t lda, int64_t m, int64_t n, const T* X
     hipLaunchKernelGGL((proj_nn_kernel<T, LP>), dim3(p.blocks * p.splits), dim3(kWave * kWaves), lds, s, A,
                        lda, m, n, X, out, stride, p.chunk, p.blocks, vec_ok);
     hipError_t e = hipGetLastError();
+    if (e == hipSuccess && done) e = hipEventRecord(done, s);
     if (e != hipSuccess || p.splits == 1) return e;
     return launch_sum_slabs<T>(slabs, stride, p.splits, m * LP, Y, s);
 }
 
 template <typename T, int LP>
 hipError_t tn_dispatch(const T* A, int64_t lda, int64_t m, int64_t n, const T* Q, const ProjPlan& p,
-                       T* slabs, T* Z, hipStream_t s) {
+                       T* slabs, T* Z, hipStream_t s, hipEvent_t done) {
     constexpr int VW = Vec16<T>::N;
     constexpr int JT = 2;
     constexpr int WJ = 16 * JT;
@@ -258,6 +259,7 @@ hipError_t tn_dispatch(const T* A, int64_t lda, int64_t m, int64_t n, const T* Q
     hipLaunchKernelGGL((proj_tn_kernel<T, LP, JT>), dim3(p.blocks * p.splits), dim3(kWave * kWaves), lds, s,
                        A, lda, m, n, Q, out, stride, p.chunk, p.blocks, vec_ok);
     hipError_t e = hipGetLastError();
+    if (e == hipSuccess && done) e = hipEventRecord(done, s);
     if (e != hipSuccess || p.splits == 1) return e;
     return launch_sum_slabs<T>(slabs, stride, p.splits, n * LP, Z, s);
 }
@@ -279,24 +281,24 @@ ProjPlan plan_proj_tn(int64_t m, int64_t n, int LP) {
 
 template <typename T>
 hipError_t launch_proj_nn(const T* A, int64_t lda, int64_t m, int64_t n, const T* X, int LP,
-                          const ProjPlan& p, T* slabs, T* Y, hipStream_t s) {
+                          const ProjPlan& p, T* slabs, T* Y, hipStream_t s, hipEvent_t done) {
     switch (LP) {
-        case 16: return nn_dispatch<T, 16>(A, lda, m, n, X, p, slabs, Y, s);
-        case 32: return nn_dispatch<T, 32>(A, lda, m, n, X, p, slabs, Y, s);
-        case 48: return nn_dispatch<T, 48>(A, lda, m, n, X, p, slabs, Y, s);
-        case 64: return nn_dispatch<T, 64>(A, lda, m, n, X, p, slabs, Y, s);
+        case 16: return nn_dispatch<T, 16>(A, lda, m, n, X, p, slabs, Y, s, done);
+        case 32: return nn_dispatch<T, 32>(A, lda, m, n, X, p, slabs, Y, s, done);
+        case 48: return nn_dispatch<T, 48>(A, lda, m, n, X, p, slabs, Y, s, done);
+        case 64: return nn_dispatch<T, 64>(A, lda, m, n, X, p, slabs, Y, s, done);
         default: return hipErrorInvalidValue;
     }
 }
 
 template <typename T>
 hipError_t launch_proj_tn(const T* A, int64_t lda, int64_t m, int64_t n, const T* Q, int LP,
-                          const ProjPlan& p, T* slabs, T* Z, hipStream_t s) {
+                          const ProjPlan& p, T* slabs, T* Z, hipStream_t s, hipEvent_t done) {
     switch (LP) {
-        case 16: return tn_dispatch<T, 16>(A, lda, m, n, Q, p, slabs, Z, s);
-        case 32: return tn_dispatch<T, 32>(A, lda, m, n, Q, p, slabs, Z, s);
-        case 48: return tn_dispatch<T, 48>(A, lda, m, n, Q, p, slabs, Z, s);
-        case 64: return tn_dispatch<T, 64>(A, lda, m, n, Q, p, slabs, Z, s);
+        case 16: return tn_dispatch<T, 16>(A, lda, m, n, Q, p, slabs, Z, s, done);
+        case 32: return tn_dispatch<T, 32>(A, lda, m, n, Q, p, slabs, Z, s, done);
+        case 48: return tn_dispatch<T, 48>(A, lda, m, n, Q, p, slabs, Z, s, done);
+        case 64: return tn_dispatch<T, 64>(A, lda, m, n, Q, p, slabs, Z, s, done);
         default: return hipErrorInvalidValue;
     }
 }
@@ -305,9 +307,9 @@ hipError_t launch_proj_tn(const T* A, int64_t lda, int64_t m, int64_t n, const T
     template ProjPlan plan_proj_nn<T>(int64_t, int64_t, int);                                          \
     template ProjPlan plan_proj_tn<T>(int64_t, int64_t, int);                                          \
     template hipError_t launch_proj_nn<T>(const T*, int64_t, int64_t, int64_t, const T*, int,          \
-                                          const ProjPlan&, T*, T*, hipStream_t);                       \
+                                          const ProjPlan&, T*, T*, hipStream_t, hipEvent_t);           \
     template hipError_t launch_proj_tn<T>(const T*, int64_t, int64_t, int64_t, const T*, int,          \
-                                          const ProjPlan&, T*, T*, hipStream_t);
+                                          const ProjPlan&, T*, T*, hipStream_t, hipEvent_t);
 RSVD_INST(float)
 RSVD_INST(double)
 #undef RSVD_INST

@@ -1,16 +1,28 @@
-// qr.hip -- tall-skinny orthonormalisation by CholeskyQR2 with an fp64 Gram, plus the
-// "panel x small matrix" MFMA kernel used for Q = Y R^-1 and the back-projections
-// U = Q * U_w (src/rSVD.cpp:128) and V = Q_B * V_w.
+// qr.hip -- tall-skinny orthonormalisation by CholeskyQR with an fp64 Gram, the cross-Gram used
+// for the small SVD's input, and the "panel x small matrix" MFMA kernel used for Q = Y R^-1 and
+// the back-projections U = Q U_w (src/rSVD.cpp:128) and V = Q_B V_w.
 //
 // The reference orthonormalises with Eigen::HouseholderQR + householderQ()*Identity
 // (src/rSVD.cpp:60-61,64-65,67-68).  rSVD's outputs depend only on span(Q), so
-// any numerically orthonormal basis of span(Y) is a drop-in.  CholeskyQR2 needs two streaming
-// passes over the panel and an l x l Cholesky:
-//     G = Y^T Y (fp64, exact products of f32/f64 entries), R1 = chol(G), Q1 = Y R1^-1,
-//     G' = Q1^T Q1, R2 = chol(G'), Q = Q1 R2^-1, R = R2 R1.
-// It is accurate while cond(Y) << 1/sqrt(u_64); the Cholesky raises a device flag when a pivot
-// falls below 1e-10 of its original diagonal (cond(Y) >~ 1e5 or rank loss), and the driver then
-// re-runs that panel through the Householder TSQR path (tsqr.hip).
+// any numerically orthonormal basis of span(Y) is a drop-in.  One CholeskyQR pass is
+//     G = Y^T Y (fp64 MFMA on exactly up-converted entries), R = chol(G), Q = Y R^-1 (fp64 MFMA)
+// and CholeskyQR2 repeats it on Q.  Because Q is applied in fp64, span(Q) = span(Y) to working
+// accuracy for ANY well-conditioned triangular R: the factorisation itself only has to make Q
+// well conditioned, so on the fp32 path it runs in fp32 (4x shorter dependent-latency chains
+// than fp64 on gfx950); the fp64 path factors in fp64.  A pivot below 1e-10 (fp64) / 1e-6 (fp32)
+// of its original diagonal raises a device flag (rank loss / cond(Y) beyond the method's range).
+// The small SVD does not use this R: it factors W = (Q_B^T B^T)^T computed exactly by the
+// cross-Gram mode below, so its accuracy does not depend on the Cholesky precision.
+//
+// gram_kernel does the whole small side of a pass in ONE launch: every workgroup reduces its
+// row block to partial 16x16 Gram tiles and publishes them (cdna_hip_programming.md §6
+// Guideline 16: plain stores, per-wave vmcnt(0), barrier, agent release, relaxed counter add);
+// one workgroup per tile waits for all slabs (bounded spin, agent acquire), sums its tile over
+// the slabs in a FIXED order (bitwise reproducible) and publishes it; the last tile reducer
+// assembles the Gram and (mode 1) factors it: R and R^-1 together by symmetric elimination on
+// [G | I], register-tiled over 256 threads, one barrier per step.
+#include <algorithm>
+
 #include "common.hpp"
 #include "kernels.hpp"
 
@@ -20,209 +32,435 @@ namespace {
 
 constexpr int kGramWaves = 4;
 
-// Partial Gram of the panel rows [b*chunk, (b+1)*chunk): f64 MFMA on (exactly) up-converted
-// entries.  Lane (r, h) holds P[i0 + h][16 g + r] for every column group g; that value is both
-// the A operand (P^T[16 g1 + r][i0 + h]) and the B operand (P[i0 + h][16 g2 + r]).
-template <typename T, int LP>
-__global__ __launch_bounds__(kWave* kGramWaves) void gram_partial_kernel(const T* __restrict__ P,
-                                                                        int64_t rows, int64_t chunk,
-                                                                        double* __restrict__ gslabs) {
-    constexpr int G = LP / 16;
+template <int LP, bool FULL>
+struct Tiles {
+    static constexpr int G = LP / 16;
+    static constexpr int NT = FULL ? G * G : G * (G + 1) / 2;  // full (cross) or upper tiles
+};
+
+__device__ __forceinline__ double rsqrt_c(double d) {
+    const double y = __builtin_amdgcn_rsq(d);
+    return y * (1.5 - 0.5 * d * y * y);
+}
+__device__ __forceinline__ float rsqrt_c(float d) {
+    const float y = __builtin_amdgcn_rsqf(d);
+    return y * (1.5f - 0.5f * d * y * y);
+}
+template <typename C> struct PivTol;
+template <> struct PivTol<double> { static constexpr double v = 1e-10; };
+template <> struct PivTol<float> { static constexpr double v = 1e-6; };
+
+// ---- R = chol(G) and R^-1 together, all 256 threads, one barrier per step ---------------------
+// Symmetric Gaussian elimination on [G | I]: after step k, row k of G is row k of D L^T and row k
+// of the identity block is row k of L^-1 (G = L D L^T, L unit lower), so
+//     R[k][j]     = M[k][j] / sqrt(M[k][k])        (j >= k)
+//     R^-1[j][k]  = W[k][j] / sqrt(M[k][k])        (j <= k).
+// Thread (ti, tj) of a 16 x 16 grid keeps M[i][j] and W[i][j] for i = ti + 16a, j = tj + 16b in
+// registers (compute type C); row k is published through a double-buffered LDS row.  The padding
+// is treated as [G_ll 0; 0 I]; outputs are zeroed outside the leading l x l block.
+// LDS: rows (4*LP of C), d0 (LP of C), Rs and RIs (LP*LP doubles each).
+template <typename C, int LP>
+__device__ __forceinline__ bool tile_cholesky_inverse(const double* Gs, C* rows, C* d0, double* Rs, double* RIs,
+                                                      int l) {
+    constexpr int NB = LP / 16;
+    const int tid = threadIdx.x;
+    const int ti = tid >> 4, tj = tid & 15;
+    C M[NB][NB], W[NB][NB];
+#pragma unroll
+    for (int a = 0; a < NB; ++a)
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+            const int i = ti + 16 * a, j = tj + 16 * b;
+            M[a][b] = (i < l && j < l) ? (C)Gs[i * LP + j] : ((i == j) ? C(1) : C(0));
+            W[a][b] = (i == j) ? C(1) : C(0);
+        }
+    for (int e = tid; e < LP * LP; e += blockDim.x) {
+        Rs[e] = 0.0;
+        RIs[e] = 0.0;
+    }
+    for (int k = tid; k < LP; k += blockDim.x) d0[k] = (k < l) ? (C)Gs[k * LP + k] : C(1);
+    bool bad = false;
+    for (int k = 0; k < l; ++k) {
+        C* rowM = rows + (k & 1) * 2 * LP;
+        C* rowW = rowM + LP;
+        const int ak = k >> 4, tk = k & 15;
+        if (ti == tk) {
+#pragma unroll
+            for (int b = 0; b < NB; ++b) {
+                C mv = M[0][b], wv = W[0][b];
+#pragma unroll
+                for (int a = 1; a < NB; ++a) {
+                    mv = (ak == a) ? M[a][b] : mv;
+                    wv = (ak == a) ? W[a][b] : wv;
+                }
+                rowM[tj + 16 * b] = mv;
+                rowW[tj + 16 * b] = wv;
+            }
+        }
+        __syncthreads();
+        C piv = rowM[k];
+        const C d0k = d0[k];
+        const bool ok = (piv > (C)PivTol<C>::v * d0k) && (d0k > C(0)) && isfinite(piv);
+        bad |= !ok;
+        piv = ok ? piv : ((d0k > C(0) && isfinite(d0k)) ? d0k : C(1));  // keep going without NaNs; flagged
+        const C inv = rsqrt_c(piv);
+        const C ipiv = inv * inv;
+        C rj[NB], wj[NB], fi[NB];
+#pragma unroll
+        for (int b = 0; b < NB; ++b) {
+            rj[b] = rowM[tj + 16 * b];
+            wj[b] = rowW[tj + 16 * b];
+            fi[b] = rowM[ti + 16 * b] * ipiv;  // m_ik = M[i][k] / M[k][k] (M symmetric)
+        }
+        if (ti == tk) {
+#pragma unroll
+            for (int b = 0; b < NB; ++b) {
+                const int j = tj + 16 * b;
+                Rs[k * LP + j] = (j >= k) ? (double)(rj[b] * inv) : 0.0;
+                RIs[j * LP + k] = (j <= k) ? (double)(wj[b] * inv) : 0.0;
+            }
+        }
+#pragma unroll
+        for (int a = 0; a < NB; ++a) {
+            const int i = ti + 16 * a;
+            const C f = (i > k) ? fi[a] : C(0);
+#pragma unroll
+            for (int b = 0; b < NB; ++b) {
+                const int j = tj + 16 * b;
+                M[a][b] -= (j > k) ? f * rj[b] : C(0);
+                W[a][b] -= f * wj[b];
+            }
+        }
+    }
+    __syncthreads();
+    return bad;
+}
+
+template <int LP>
+__device__ __forceinline__ void write_factor(const double* Rs, const double* RIs, int l, double* __restrict__ Rout,
+                                             double* __restrict__ Rinv) {
+    for (int e = threadIdx.x; e < LP * LP; e += blockDim.x) {
+        const int i = e / LP, j = e % LP;
+        const bool in = i < l && j < l;
+        if (Rout) Rout[e] = in ? Rs[e] : 0.0;
+        Rinv[e] = in ? RIs[e] : 0.0;
+    }
+}
+
+__device__ __forceinline__ bool spin_until(unsigned* ctr, unsigned target, int* flag) {
+    unsigned spins = 0;
+    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > (1u << 26)) {  // ~seconds: never expected; report instead of hanging
+            atomicOr(flag + 2, 1);
+            return false;
+        }
+    }
+    return true;
+}
+
+// Doubles of LDS the factorisation phase needs (Gs + Rs + RIs, rows + d0).
+template <int LP>
+constexpr size_t factor_lds_doubles() { return (size_t)3 * LP * LP + 5 * LP; }
+
+// ------------------------------------------------------------------------------------------------
+// grid = max(nb, NT) workgroups.  Phase 1 (blocks < nb): partial Gram of a row block -> slab
+// (CROSS: P^T P2, all G x G tiles; else P^T P, upper tiles).  Phase 2 (blocks < NT): wait for all
+// nb slabs (cumulative counter ctr[0] >= target0), reduce tile `blockIdx.x` over the slabs in fixed
+// order.  Phase 3 (the last tile reducer, ctr[1] == target1 - 1): mode 1 factors (R, R^-1), mode 0
+// writes the Gram (zero outside l x l) to Gsum.  Counters are zeroed by the driver at the start of
+// every run; targets are run-cumulative (no in-kernel reset).
+template <typename T, typename C, int LP, bool CROSS>
+__global__ __launch_bounds__(kWave* kGramWaves) void gram_kernel(
+    const T* __restrict__ P, const T* __restrict__ P2, int64_t rows, int64_t chunk, int nb,
+    double* __restrict__ slabs, double* __restrict__ tiles, unsigned* __restrict__ ctr, unsigned target0,
+    unsigned target1, int mode, double* __restrict__ Gsum, int l, double* __restrict__ Rout,
+    double* __restrict__ Rinv, int* __restrict__ flag) {
+    constexpr int G = Tiles<LP, CROSS>::G, NT = Tiles<LP, CROSS>::NT;
     typedef Mfma<double> M;
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-    double* red = reinterpret_cast<double*>(smem_raw);  // [kGramWaves][LP][LP]
+    double* red = reinterpret_cast<double*>(smem_raw);  // [kGramWaves][NT][256]
+    constexpr size_t red_doubles = (size_t)kGramWaves * NT * 256;
+    constexpr size_t area = red_doubles > factor_lds_doubles<LP>() ? red_doubles : factor_lds_doubles<LP>();
+    int* ticket = reinterpret_cast<int*>(red + area);
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int r = lane & 15, h = lane >> 4;
-    const int64_t rbeg = (int64_t)blockIdx.x * chunk;
-    const int64_t rend = (rbeg + chunk < rows) ? rbeg + chunk : rows;
+    const int b = blockIdx.x;
 
-    f64x4 acc[G][G];
+    if (b < nb) {
+        const int64_t rbeg = (int64_t)b * chunk;
+        const int64_t rend = (rbeg + chunk < rows) ? rbeg + chunk : rows;
+        f64x4 acc[NT];
 #pragma unroll
-    for (int a = 0; a < G; ++a)
+        for (int t = 0; t < NT; ++t) acc[t] = M::zero();
+        constexpr int U = CROSS ? 2 : 4;  // k-steps (4 rows each) per wave per iteration, loads first
+        for (int64_t i0 = rbeg + 4 * w; i0 < rend; i0 += 4 * kGramWaves * U) {
+            double y[U][G], z[U][G];
 #pragma unroll
-        for (int b = 0; b < G; ++b) acc[a][b] = M::zero();
-
-    for (int64_t i0 = rbeg + 4 * w; i0 < rend; i0 += 4 * kGramWaves) {
-        const int64_t i = i0 + h;
-        double y[G];
+            for (int u = 0; u < U; ++u) {
+                const int64_t i = i0 + 4 * kGramWaves * u + h;
 #pragma unroll
-        for (int g = 0; g < G; ++g) y[g] = (i < rend) ? (double)P[i * LP + 16 * g + r] : 0.0;
-#pragma unroll
-        for (int a = 0; a < G; ++a)
-#pragma unroll
-            for (int b = a; b < G; ++b) acc[a][b] = M::mma(y[a], y[b], acc[a][b]);
-    }
-    double* mine = red + (size_t)w * LP * LP;
-#pragma unroll
-    for (int a = 0; a < G; ++a)
-#pragma unroll
-        for (int b = a; b < G; ++b)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int row = 16 * a + M::row(h, j), col = 16 * b + r;
-                mine[row * LP + col] = acc[a][b][j];
+                for (int g = 0; g < G; ++g) {
+                    y[u][g] = (i < rend) ? (double)P[i * LP + 16 * g + r] : 0.0;
+                    z[u][g] = (CROSS && i < rend) ? (double)P2[i * LP + 16 * g + r] : 0.0;
+                }
             }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                int t = 0;
+#pragma unroll
+                for (int a = 0; a < G; ++a)
+#pragma unroll
+                    for (int bb = (CROSS ? 0 : a); bb < G; ++bb, ++t)
+                        acc[t] = M::mma(y[u][a], CROSS ? z[u][bb] : y[u][bb], acc[t]);
+            }
+        }
+        // tile (a, bb) element (row 16a + R, col 16bb + C) sits at red[w][t][R*16 + C]
+        double* mine = red + (size_t)w * NT * 256;
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+            for (int jj = 0; jj < 4; ++jj) mine[t * 256 + M::row(h, jj) * 16 + r] = acc[t][jj];
+        __syncthreads();
+        double* myslab = slabs + (size_t)b * NT * 256;
+        for (int e = threadIdx.x; e < NT * 256; e += blockDim.x) {
+            double s = 0.0;
+#pragma unroll
+            for (int ww = 0; ww < kGramWaves; ++ww) s += red[(size_t)ww * NT * 256 + e];
+            myslab[e] = s;
+        }
+        // publish (cdna_hip_programming.md §6 Guideline 16, counter form)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    if (b >= NT) return;
+    // ---- phase 2: tile reducer ----
+    if (threadIdx.x == 0) {
+        *ticket = spin_until(ctr, target0, flag) ? 1 : 0;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     __syncthreads();
-    double* dst = gslabs + (size_t)blockIdx.x * LP * LP;
+    if (*ticket == 0) return;
+    {
+        const int e = threadIdx.x;  // 256 elements per tile, one per thread
+        double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+        int sb = 0;
+        for (; sb + 4 <= nb; sb += 4) {  // 4 independent loads in flight, fixed summation order
+            const double v0 = slabs[(size_t)(sb + 0) * NT * 256 + b * 256 + e];
+            const double v1 = slabs[(size_t)(sb + 1) * NT * 256 + b * 256 + e];
+            const double v2 = slabs[(size_t)(sb + 2) * NT * 256 + b * 256 + e];
+            const double v3 = slabs[(size_t)(sb + 3) * NT * 256 + b * 256 + e];
+            s0 += v0; s1 += v1; s2 += v2; s3 += v3;
+        }
+        for (; sb < nb; ++sb) s0 += slabs[(size_t)sb * NT * 256 + b * 256 + e];
+        tiles[b * 256 + e] = (s0 + s1) + (s2 + s3);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned tk = __hip_atomic_fetch_add(ctr + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *ticket = (tk == target1 - 1) ? 1 : 0;
+        if (*ticket) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+    }
+    __syncthreads();
+    if (*ticket == 0) return;
+    // ---- phase 3: the last tile reducer assembles the Gram ----
+    double* Gs = red;                    // [LP][LP]   (reuses the reduction area)
+    double* Rs = Gs + LP * LP;           // [LP][LP]
+    double* RIs = Rs + LP * LP;          // [LP][LP]
+    C* prow = reinterpret_cast<C*>(RIs + LP * LP);  // [2][2][LP]
+    C* d0 = prow + 4 * LP;                          // [LP]
+    for (int e = threadIdx.x; e < NT * 256; e += blockDim.x) {
+        const double s = tiles[e];
+        int t = e >> 8, a = 0, bb;
+        if (CROSS) {
+            a = t / G;
+            bb = t % G;
+        } else {
+            while (t >= G - a) { t -= G - a; ++a; }
+            bb = a + t;
+        }
+        const int R_ = (e & 255) >> 4, C_ = e & 15;
+        const int row = 16 * a + R_, col = 16 * bb + C_;
+        Gs[row * LP + col] = s;
+        if (!CROSS) Gs[col * LP + row] = s;
+    }
+    __syncthreads();
+    if (mode == 0) {
+        for (int e = threadIdx.x; e < LP * LP; e += blockDim.x) {
+            const int row = e / LP, col = e % LP;
+            Gsum[e] = (row < l && col < l) ? Gs[e] : 0.0;
+        }
+        return;
+    }
+    const bool bad = tile_cholesky_inverse<C, LP>(Gs, prow, d0, Rs, RIs, l);
+    write_factor<LP>(Rs, RIs, l, Rout, Rinv);
+    if (threadIdx.x == 0 && bad) atomicAdd(flag, 1);
+}
+
+// Factor an already-summed Gram (distributed path: after the all-reduce).
+template <typename C, int LP>
+__global__ __launch_bounds__(256) void chol_kernel(const double* __restrict__ Gin, int l, double* __restrict__ Rout,
+                                                   double* __restrict__ Rinv, int* __restrict__ flag) {
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    double* Gs = reinterpret_cast<double*>(smem_raw);
+    double* Rs = Gs + LP * LP;
+    double* RIs = Rs + LP * LP;
+    C* prow = reinterpret_cast<C*>(RIs + LP * LP);
+    C* d0 = prow + 4 * LP;
     for (int e = threadIdx.x; e < LP * LP; e += blockDim.x) {
         const int row = e / LP, col = e % LP;
-        const int a = row / 16, b = col / 16;
-        // only the upper tile blocks were produced; mirror the lower ones
-        const int src = (a <= b) ? e : col * LP + row;
-        double s = 0.0;
-#pragma unroll
-        for (int ww = 0; ww < kGramWaves; ++ww) s += red[(size_t)ww * LP * LP + src];
-        dst[e] = s;
+        Gs[e] = (row < l && col < l) ? Gin[e] : 0.0;
     }
+    __syncthreads();
+    const bool bad = tile_cholesky_inverse<C, LP>(Gs, prow, d0, Rs, RIs, l);
+    write_factor<LP>(Rs, RIs, l, Rout, Rinv);
+    if (threadIdx.x == 0 && bad) atomicAdd(flag, 1);
 }
 
-// One workgroup: G = sum(slabs); R = chol(G) upper; Rinv = R^-1; Racc = R * Racc (optional).
-__global__ __launch_bounds__(256) void chol_inv_kernel(const double* __restrict__ gslabs, int nslab, int l,
-                                                       int LP, double* __restrict__ Rout,
-                                                       double* __restrict__ Rinv_out, double* __restrict__ Racc,
-                                                       int accumulate, int* __restrict__ flag) {
-    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-    double* Gs = reinterpret_cast<double*>(smem_raw);  // [LP][LP]
-    double* Ri = Gs + LP * LP;                          // [LP][LP]
-    double* d0 = Ri + LP * LP;                          // [LP] original diagonal
-    int& bad = *reinterpret_cast<int*>(d0 + LP);        // kept in the dynamic region (Guideline 17)
-    const int tid = threadIdx.x, nt = blockDim.x;
-    if (tid == 0) bad = 0;
-    for (int e = tid; e < LP * LP; e += nt) {
-        double s = 0.0;
-        for (int b = 0; b < nslab; ++b) s += gslabs[(size_t)b * LP * LP + e];
-        Gs[e] = s;
-        Ri[e] = 0.0;
-    }
-    __syncthreads();
-    for (int k = tid; k < l; k += nt) d0[k] = Gs[k * LP + k];
-    __syncthreads();
-    // right-looking Cholesky on the upper triangle
-    for (int k = 0; k < l; ++k) {
-        if (tid == 0) {
-            double d = Gs[k * LP + k];
-            const double ref = d0[k];
-            if (!(d > 1e-10 * ref) || !(ref > 0.0) || !isfinite(d)) {
-                bad = 1;
-                d = (ref > 0.0 && isfinite(ref)) ? ref : 1.0;  // keep going without NaNs; result flagged
-            }
-            Gs[k * LP + k] = sqrt(d);
-        }
-        __syncthreads();
-        const double inv = 1.0 / Gs[k * LP + k];
-        for (int j = k + 1 + tid; j < l; j += nt) Gs[k * LP + j] *= inv;
-        __syncthreads();
-        const int rem = l - k - 1;
-        for (int e = tid; e < rem * rem; e += nt) {
-            const int i = k + 1 + e / rem, j = k + 1 + e % rem;
-            if (j >= i) Gs[i * LP + j] -= Gs[k * LP + i] * Gs[k * LP + j];
-        }
-        __syncthreads();
-    }
-    // Rinv: bottom-up rows, Rinv[i][j] = -(1/R_ii) * sum_{p=i+1..j} R[i][p] Rinv[p][j]
-    for (int i = l - 1; i >= 0; --i) {
-        const double rii = Gs[i * LP + i];
-        for (int j = i + tid; j < l; j += nt) {
-            if (j == i) {
-                Ri[i * LP + i] = 1.0 / rii;
-            } else {
-                double s = 0.0;
-                for (int p = i + 1; p <= j; ++p) s += Gs[i * LP + p] * Ri[p * LP + j];
-                Ri[i * LP + j] = -s / rii;
-            }
-        }
-        __syncthreads();
-    }
-    // outputs (zero the strictly-lower part and the padding)
-    for (int e = tid; e < LP * LP; e += nt) {
-        const int i = e / LP, j = e % LP;
-        const bool in = (i < l && j < l && j >= i);
-        Rout[e] = in ? Gs[e] : 0.0;
-        Rinv_out[e] = in ? Ri[e] : 0.0;
-    }
-    if (accumulate) {
-        // Racc <- R * Racc  (both upper triangular); stage old Racc in Ri (Rinv already written)
-        __syncthreads();
-        for (int e = tid; e < LP * LP; e += nt) Ri[e] = Racc[e];
-        __syncthreads();
-        for (int e = tid; e < LP * LP; e += nt) {
-            const int i = e / LP, j = e % LP;
-            double s = 0.0;
-            if (i < l && j < l && j >= i)
-                for (int p = i; p <= j; ++p) s += Gs[i * LP + p] * Ri[p * LP + j];
-            Racc[e] = s;
-        }
-    }
-    __syncthreads();
-    if (tid == 0 && bad) atomicOr(flag, 1);
-}
-
-// Out = In * M: 16 rows per wave, 4 waves per workgroup; In tile and M staged in LDS.
+// Out = In * M: 16 rows per wave, 4 waves per workgroup; In tile and M staged in LDS as fp64 and
+// multiplied on the f64 MFMA, so applying R^-1 does not amplify storage rounding by cond(R);
+// only the result is rounded to T.
 template <typename T, int LP>
 __global__ __launch_bounds__(256) void panel_small_kernel(const T* __restrict__ In, int64_t rows,
                                                           const double* __restrict__ Mg, T* __restrict__ Out,
                                                           int out_colmajor, int cols, int64_t ld) {
-    typedef Mfma<T> M;
-    typedef typename M::acc_t acc_t;
+    typedef Mfma<double> M;
     constexpr int G = LP / 16;
     constexpr int RPB = 64;  // rows per block
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-    T* Ms = reinterpret_cast<T*>(smem_raw);  // [LP][LP]
-    T* Is = Ms + LP * LP;                    // [RPB][LP + 1] (padded: fragment reads are column-wise)
+    double* Ms = reinterpret_cast<double*>(smem_raw);  // [LP][LP]
+    double* Is = Ms + LP * LP;                         // [RPB][LP + 1] (padded: fragment reads are column-wise)
     constexpr int IS = LP + 1;
     const int tid = threadIdx.x;
     const int lane = tid & 63, w = tid >> 6;
     const int r = lane & 15, h = lane >> 4;
     const int64_t row0 = (int64_t)blockIdx.x * RPB;
-    for (int e = tid; e < LP * LP; e += blockDim.x) Ms[e] = (T)Mg[e];
+    for (int e = tid; e < LP * LP; e += blockDim.x) Ms[e] = Mg[e];
     for (int e = tid; e < RPB * LP; e += blockDim.x) {
         const int lr = e / LP, c = e % LP;
-        Is[lr * IS + c] = (row0 + lr < rows) ? In[(row0 + lr) * LP + c] : T(0);
+        Is[lr * IS + c] = (row0 + lr < rows) ? (double)In[(row0 + lr) * LP + c] : 0.0;
     }
     __syncthreads();
-    acc_t acc[G];
+    f64x4 acc[G];
 #pragma unroll
     for (int g = 0; g < G; ++g) acc[g] = M::zero();
     const int lr0 = w * 16;
 #pragma unroll
     for (int k0 = 0; k0 < LP; k0 += 4) {
-        const T a = Is[(lr0 + r) * IS + k0 + h];
+        const double a = Is[(lr0 + r) * IS + k0 + h];
 #pragma unroll
         for (int g = 0; g < G; ++g) acc[g] = M::mma(a, Ms[(k0 + h) * LP + 16 * g + r], acc[g]);
     }
+    if (!out_colmajor) {
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int64_t row = row0 + lr0 + M::row(h, j);
+                if (row < rows) Out[row * LP + 16 * g + r] = (T)acc[g][j];
+            }
+        return;
+    }
+    // column-major output: transpose through LDS so each column segment is stored contiguously
+    __syncthreads();
+    double* Ts = Is;  // [LP][RPB + 1]
+    constexpr int TS = RPB + 1;
 #pragma unroll
     for (int g = 0; g < G; ++g)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int64_t row = row0 + lr0 + M::row(h, j);
-            const int col = 16 * g + r;
-            if (row < rows) {
-                if (!out_colmajor)
-                    Out[row * LP + col] = acc[g][j];
-                else if (col < cols)
-                    Out[row + (int64_t)col * ld] = acc[g][j];
-            }
-        }
+        for (int j = 0; j < 4; ++j) Ts[(16 * g + r) * TS + lr0 + M::row(h, j)] = acc[g][j];
+    __syncthreads();
+    for (int e = tid; e < cols * RPB; e += blockDim.x) {
+        const int c = e / RPB, lr = e % RPB;
+        if (row0 + lr < rows) Out[row0 + lr + (int64_t)c * ld] = (T)Ts[c * TS + lr];
+    }
+}
+
+template <int LP, bool CROSS>
+size_t gram_lds_bytes() {
+    const size_t red = (size_t)kGramWaves * Tiles<LP, CROSS>::NT * 256;
+    return std::max(red, factor_lds_doubles<LP>()) * sizeof(double) + 16;
+}
+
+template <typename T, typename C, int LP, bool CROSS>
+hipError_t gram_launch(const T* P, const T* P2, int64_t rows, int nb, double* slabs, double* tiles, unsigned* ctr,
+                       unsigned t0, unsigned t1, int mode, double* Gsum, int l, double* R, double* Rinv, int* flag,
+                       hipStream_t s) {
+    const int64_t chunk = (rows + nb - 1) / nb;
+    const int NT = Tiles<LP, CROSS>::NT;
+    const int grid = nb > NT ? nb : NT;
+    hipLaunchKernelGGL((gram_kernel<T, C, LP, CROSS>), dim3(grid), dim3(kWave * kGramWaves), (gram_lds_bytes<LP, CROSS>()),
+                       s, P, P2, rows, chunk, nb, slabs, tiles, ctr, t0, t1, mode, Gsum, l, R, Rinv, flag);
+    return hipGetLastError();
 }
 
 }  // namespace
 
 int plan_gram_blocks(int64_t rows) {
-    int64_t blocks = (rows + 1023) / 1024;  // >= 1024 rows per workgroup
-    if (blocks > 64) blocks = 64;
+    int64_t blocks = (rows + 127) / 128;  // >= 128 rows per workgroup
+    if (blocks > 32) blocks = 32;
     if (blocks < 1) blocks = 1;
     return (int)blocks;
 }
 
+int gram_tiles(int LP, int cross) {
+    const int G = LP / 16;
+    return cross ? G * G : G * (G + 1) / 2;
+}
+
 template <typename T>
-hipError_t launch_gram_partial(const T* P, int64_t rows, int LP, int nblk, double* gslabs, hipStream_t s) {
-    const int64_t chunk = (rows + nblk - 1) / nblk;
-    const size_t lds = (size_t)kGramWaves * LP * LP * sizeof(double);
+hipError_t launch_gram_chol(const T* P, int64_t rows, int LP, int nb, double* slabs, double* tiles, unsigned* ctr,
+                            unsigned t0, unsigned t1, int mode, int compute_f32, double* Gsum, int l, double* R,
+                            double* Rinv, int* flag, hipStream_t s) {
     switch (LP) {
-#define CASE(L)                                                                                            \
-    case L:                                                                                                \
-        hipLaunchKernelGGL((gram_partial_kernel<T, L>), dim3(nblk), dim3(kWave * kGramWaves), lds, s, P, rows, \
-                           chunk, gslabs);                                                                 \
+#define CASE(L)                                                                                                   \
+    case L:                                                                                                       \
+        return compute_f32 ? gram_launch<T, float, L, false>(P, nullptr, rows, nb, slabs, tiles, ctr, t0, t1, mode, \
+                                                              Gsum, l, R, Rinv, flag, s)                           \
+                           : gram_launch<T, double, L, false>(P, nullptr, rows, nb, slabs, tiles, ctr, t0, t1, mode, \
+                                                               Gsum, l, R, Rinv, flag, s);
+        CASE(16) CASE(32) CASE(48) CASE(64)
+#undef CASE
+        default: return hipErrorInvalidValue;
+    }
+}
+
+template <typename T>
+hipError_t launch_cross_gram(const T* P, const T* P2, int64_t rows, int LP, int nb, double* slabs, double* tiles,
+                             unsigned* ctr, unsigned t0, unsigned t1, double* Gout, int l, int* flag, hipStream_t s) {
+    switch (LP) {
+#define CASE(L)                                                                                                 \
+    case L:                                                                                                     \
+        return gram_launch<T, double, L, true>(P, P2, rows, nb, slabs, tiles, ctr, t0, t1, 0, Gout, l, nullptr, \
+                                               nullptr, flag, s);
+        CASE(16) CASE(32) CASE(48) CASE(64)
+#undef CASE
+        default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_chol(const double* G, int l, int LP, int compute_f32, double* R, double* Rinv, int* flag,
+                       hipStream_t s) {
+    const size_t lds = factor_lds_doubles<64>() * sizeof(double) + 16;
+    switch (LP) {
+#define CASE(L)                                                                                                    \
+    case L:                                                                                                        \
+        if (compute_f32)                                                                                           \
+            hipLaunchKernelGGL((chol_kernel<float, L>), dim3(1), dim3(256), lds, s, G, l, R, Rinv, flag);          \
+        else                                                                                                       \
+            hipLaunchKernelGGL((chol_kernel<double, L>), dim3(1), dim3(256), lds, s, G, l, R, Rinv, flag);         \
         break;
         CASE(16) CASE(32) CASE(48) CASE(64)
 #undef CASE
@@ -231,19 +469,11 @@ hipError_t launch_gram_partial(const T* P, int64_t rows, int LP, int nblk, doubl
     return hipGetLastError();
 }
 
-hipError_t launch_chol_inv(const double* gslabs, int nslab, int l, int LP, double* R, double* Rinv, double* Racc,
-                           int accumulate, int* flag, hipStream_t s) {
-    const size_t lds = (size_t)(2 * LP * LP + LP) * sizeof(double) + 16;
-    hipLaunchKernelGGL(chol_inv_kernel, dim3(1), dim3(256), lds, s, gslabs, nslab, l, LP, R, Rinv, Racc,
-                       accumulate, flag);
-    return hipGetLastError();
-}
-
 template <typename T>
 hipError_t launch_panel_small(const T* In, int64_t rows, int LP, const double* Mat, T* Out, int out_colmajor,
                               int cols, int64_t ld, hipStream_t s) {
     const int blocks = (int)((rows + 63) / 64);
-    const size_t lds = (size_t)(LP * LP + 64 * (LP + 1)) * sizeof(T);
+    const size_t lds = (size_t)(LP * LP + std::max(64 * (LP + 1), LP * 65)) * sizeof(double);
     switch (LP) {
 #define CASE(L)                                                                                          \
     case L:                                                                                              \
@@ -257,9 +487,12 @@ hipError_t launch_panel_small(const T* In, int64_t rows, int LP, const double* M
     return hipGetLastError();
 }
 
-#define RSVD_INST(T)                                                                                       \
-    template hipError_t launch_gram_partial<T>(const T*, int64_t, int, int, double*, hipStream_t);         \
-    template hipError_t launch_panel_small<T>(const T*, int64_t, int, const double*, T*, int, int, int64_t, \
+#define RSVD_INST(T)                                                                                             \
+    template hipError_t launch_gram_chol<T>(const T*, int64_t, int, int, double*, double*, unsigned*, unsigned,    \
+                                            unsigned, int, int, double*, int, double*, double*, int*, hipStream_t); \
+    template hipError_t launch_cross_gram<T>(const T*, const T*, int64_t, int, int, double*, double*, unsigned*,   \
+                                             unsigned, unsigned, double*, int, int*, hipStream_t);               \
+    template hipError_t launch_panel_small<T>(const T*, int64_t, int, const double*, T*, int, int, int64_t,       \
                                               hipStream_t);
 RSVD_INST(float)
 RSVD_INST(double)

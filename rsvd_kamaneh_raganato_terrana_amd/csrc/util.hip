@@ -142,3 +142,106 @@ RSVD_INST(double)
 #undef RSVD_INST
 
 }  // namespace rsvd
+
+// ================================================================================================
+// Robust re-orthonormalisation (fallback for a panel whose CholeskyQR flagged a bad pivot:
+// rank-deficient or too ill-conditioned Y).  Predicated on *flag: one early-exit launch otherwise.
+// One workgroup, classical Gram-Schmidt with re-orthogonalisation ("twice is enough", a third pass
+// when a column lost more than half its norm) on the ORIGINAL panel P.  A column whose residual is
+// at the rounding-noise level (relative 1e-13 fp64 / 1e-6 fp32) is replaced by a Philox Gaussian
+// vector and orthogonalised: like the reference's Householder Q (src/rSVD.cpp:60-61), the result is
+// an orthonormal basis of span(Y) completed by arbitrary orthonormal directions.
+// ================================================================================================
+namespace rsvd {
+namespace {
+
+constexpr int kRobustThreads = 256;
+
+__device__ __forceinline__ double block_sum(double v, double* red) {
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    __syncthreads();
+    if (lane == 0) red[w] = v;
+    __syncthreads();
+    double s = 0.0;
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) s += red[i];
+    return s;
+}
+
+template <typename T>
+__global__ __launch_bounds__(kRobustThreads) void robust_orth_kernel(const T* __restrict__ P, int64_t rows, int l,
+                                                                    int LP, T* __restrict__ Q,
+                                                                    const int* __restrict__ flag, uint64_t seed) {
+    if (*flag == 0) return;
+    __shared__ double dots[64 + 8];
+    __shared__ double red[8];
+    const int tid = threadIdx.x, nt = blockDim.x;
+    const double tiny = sizeof(T) == 4 ? 1e-6 : 1e-13;
+    // zero the padding columns, copy P into Q (columns are orthogonalised in place)
+    for (int64_t e = tid; e < rows * LP; e += nt) Q[e] = ((e % LP) < l) ? P[e] : T(0);
+    __syncthreads();
+    for (int j = 0; j < l; ++j) {
+        double n0 = 0.0;
+        for (int64_t r = tid; r < rows; r += nt) n0 += (double)Q[r * LP + j] * (double)Q[r * LP + j];
+        n0 = sqrt(block_sum(n0, red));
+        bool replaced = false;
+        for (int attempt = 0; attempt < 2; ++attempt) {
+            double nprev = n0;
+            for (int pass = 0; pass < 3; ++pass) {
+                // d_i = <q_i, v>, i < j  (256 threads x up to 64 partial sums, reduced per i)
+                for (int i = 0; i < j; ++i) {
+                    double d = 0.0;
+                    for (int64_t r = tid; r < rows; r += nt) d += (double)Q[r * LP + i] * (double)Q[r * LP + j];
+                    d = block_sum(d, red);
+                    if (tid == 0) dots[i] = d;
+                }
+                __syncthreads();
+                double nn = 0.0;
+                for (int64_t r = tid; r < rows; r += nt) {
+                    double x = (double)Q[r * LP + j];
+                    for (int i = 0; i < j; ++i) x -= dots[i] * (double)Q[r * LP + i];
+                    Q[r * LP + j] = (T)x;
+                    nn += x * x;
+                }
+                nn = sqrt(block_sum(nn, red));
+                const bool again = nn < 0.5 * nprev;
+                nprev = nn;
+                if (pass >= 1 && !again) break;
+            }
+            if (nprev > tiny * n0 && nprev > 0.0 && isfinite(nprev)) {
+                const double inv = 1.0 / nprev;
+                for (int64_t r = tid; r < rows; r += nt) Q[r * LP + j] = (T)((double)Q[r * LP + j] * inv);
+                __syncthreads();
+                break;
+            }
+            // rounding-noise residual: replace by a deterministic Gaussian vector and retry
+            replaced = true;
+            for (int64_t r = tid; r < rows; r += nt) {
+                uint32_t x[4];
+                philox4x32_10((uint64_t)r * 64 + j, seed ^ 0xC0FFEE1234ull, x);
+                Q[r * LP + j] = (T)((double)x[0] * 2.3283064365386963e-10 - 0.5);
+            }
+            __syncthreads();
+            n0 = 0.0;
+            for (int64_t r = tid; r < rows; r += nt) n0 += (double)Q[r * LP + j] * (double)Q[r * LP + j];
+            n0 = sqrt(block_sum(n0, red));
+        }
+        (void)replaced;
+        __syncthreads();
+    }
+}
+
+}  // namespace
+
+template <typename T>
+hipError_t launch_robust_orth(const T* P, int64_t rows, int l, int LP, T* Q, const int* flag, uint64_t seed,
+                              hipStream_t s) {
+    hipLaunchKernelGGL((robust_orth_kernel<T>), dim3(1), dim3(kRobustThreads), 0, s, P, rows, l, LP, Q, flag, seed);
+    return hipGetLastError();
+}
+
+template hipError_t launch_robust_orth<float>(const float*, int64_t, int, int, float*, const int*, uint64_t, hipStream_t);
+template hipError_t launch_robust_orth<double>(const double*, int64_t, int, int, double*, const int*, uint64_t,
+                                               hipStream_t);
+
+}  // namespace rsvd

@@ -81,3 +81,50 @@ def test_rsvd_f32_device_matches_oracle(engine):
     k = 32
     assert rel_fro(sign_align(U[:, :k], Uo[:, :k]), Uo[:, :k]) < 1e-4
     assert rel_fro(sign_align(V[:, :k], Vo[:, :k]), Vo[:, :k]) < 1e-4
+
+
+def _ref_rank2(n=100):
+    """input/sparse_matrix.mtx (python/matrix_maker.py): A[i][j] = i*n + j + 1, rank 2."""
+    return np.asfortranarray(np.arange(1, n * n + 1, dtype=np.float64).reshape(n, n))
+
+
+@pytest.mark.parametrize("l", [4, 16])
+def test_rank_deficient_rank2_known_answer(engine, l):
+    """Y = A Omega has rank 2 < l: CholeskyQR breaks down and the robust path must take over."""
+    A = _ref_rank2()
+    U, S, V = engine.rsvd_host(A, l, seed=0x5EED0001)
+    Uo, So, Vo = oracle.rsvd(A, l, q=2, seed=0x5EED0001)
+    sv = np.linalg.svd(A, compute_uv=False)
+    assert abs(S[0] - sv[0]) < 1e-10 * sv[0] and abs(S[1] - sv[1]) < 1e-8 * sv[0]
+    assert np.max(np.abs(S[2:])) < 1e-9 * sv[0]
+    assert rel_fro(S, So) < 1e-10
+    assert np.linalg.norm(U.T @ U - np.eye(l)) < 1e-10
+    assert np.linalg.norm(V.T @ V - np.eye(l)) < 1e-10
+    assert np.linalg.norm(A - (U * S) @ V.T) < 1e-9 * np.linalg.norm(A)
+    assert engine.info()["cholqr_fallbacks"] > 0
+
+
+def test_zero_matrix(engine):
+    A = np.zeros((64, 48), order="F")
+    U, S, V = engine.rsvd_host(A, 8)
+    assert np.all(S == 0.0)
+    assert np.linalg.norm(U.T @ U - np.eye(8)) < 1e-10
+    assert np.linalg.norm(V.T @ V - np.eye(8)) < 1e-10
+
+
+def test_duplicate_columns_f32_device(engine):
+    import torch
+
+    rng = np.random.default_rng(11)
+    B = rng.standard_normal((512, 6))
+    A = np.asfortranarray(np.repeat(B, 40, axis=1)[:, :200])  # rank 6, l = 32
+    At = torch.from_numpy(A.astype(np.float32)).cuda().t().contiguous().t()
+    U, S, V = engine.rsvd(At, 32, q=2, seed=3)
+    torch.cuda.synchronize()
+    U, S, V = U.cpu().double().numpy(), S.cpu().double().numpy(), V.cpu().double().numpy()
+    sv = np.linalg.svd(A, compute_uv=False)
+    assert rel_fro(S[:6], sv[:6]) < 1e-5
+    assert np.max(np.abs(S[6:])) < 1e-4 * sv[0]
+    assert np.linalg.norm(U.T @ U - np.eye(32)) < 1e-4
+    assert np.linalg.norm(V.T @ V - np.eye(32)) < 1e-4
+    assert np.linalg.norm(A - (U * S) @ V.T) < 1e-5 * np.linalg.norm(A)
