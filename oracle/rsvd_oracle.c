@@ -27,7 +27,7 @@ int orc_set_threads(int nthreads) {
 }
 
 /* ------------------------------------------------------------------------------------------ */
-/* Philox4x32-10 (Salmon et al., SC'11).  The device twin lives in csrc/rsvd_kernels.hip.       */
+/* Philox4x32-10 (Salmon et al., SC'11).  The device twin lives in csrc/util.hip.                */
 /* ------------------------------------------------------------------------------------------ */
 static inline void philox_round(uint32_t c[4], const uint32_t k[2]) {
     const uint64_t p0 = (uint64_t)0xD2511F53u * c[0];

@@ -14,10 +14,11 @@ from .api import (  # noqa: F401
     empty_colmajor,
     generateOmega,
     intermediate_step,
+    make_allreduce_hook,
     rSVD,
 )
 
 __all__ = [
     "build", "row_partition", "RSVDError", "Engine", "QRMode", "SVDMethod", "colmajor",
-    "default_engine", "empty_colmajor", "generateOmega", "intermediate_step", "rSVD",
+    "default_engine", "empty_colmajor", "generateOmega", "intermediate_step", "make_allreduce_hook", "rSVD",
 ]

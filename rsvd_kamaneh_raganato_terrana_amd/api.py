@@ -63,6 +63,39 @@ def empty_colmajor(rows: int, cols: int, dtype, device):
     return torch.empty((cols, rows), dtype=dtype, device=device).t()
 
 
+def make_allreduce_hook(get_buffer, group=None):
+    """The C ABI's rsvd_allreduce_fn (include/rsvd_c.h) over torch.distributed.
+
+    The engine only ever exchanges slices of its workspace (the Gram matrix of a CholeskyQR pass
+    and the n x l panel Z = A^T Q); ``get_buffer()`` returns that workspace as a
+    uint8 tensor and the hook sums the (pointer, count, dtype) slice in place across ranks.  It
+    returns non-zero (never raises through C) for a slice outside the buffer or a failed
+    collective.  With a CUDA workspace and the "nccl" backend this is an RCCL all-reduce over
+    xGMI; with a CPU buffer and "gloo" it is the same code path the CPU tests exercise.
+    """
+    torch = _torch()
+    import torch.distributed as dist
+
+    def _hook(buf, count, dtype, stream, user):
+        try:
+            ws = get_buffer()
+            if ws is None or buf is None:
+                return 1
+            base = ws.data_ptr()
+            tdt = torch.float64 if dtype == _capi.F64 else torch.float32
+            esz = 8 if dtype == _capi.F64 else 4
+            off = buf - base
+            if count < 0 or off < 0 or off % esz or off + count * esz > ws.numel():
+                return 1
+            view = ws[off: off + count * esz].view(tdt)
+            dist.all_reduce(view, op=dist.ReduceOp.SUM, group=group)
+            return 0
+        except Exception:  # never unwind through C
+            return 1
+
+    return _capi.ALLREDUCE_FN(_hook)
+
+
 class Engine:
     """One GPU handle (HIP stream + workspace); mirrors what a C++ caller gets from librsvd_hip."""
 
@@ -107,27 +140,7 @@ class Engine:
 
     def set_comm(self, rank: int, world: int, group=None):
         """Row-sharded runs: bind the exchange hook to torch.distributed.all_reduce (RCCL)."""
-        torch = _torch()
-        import torch.distributed as dist
-
-        eng = self
-
-        def _hook(buf, count, dtype, stream, user):
-            try:
-                ws = eng._ws
-                base = ws.data_ptr()
-                tdt = torch.float64 if dtype == _capi.F64 else torch.float32
-                esz = 8 if dtype == _capi.F64 else 4
-                off = buf - base
-                if off < 0 or off % esz or off + count * esz > ws.numel():
-                    return 1
-                view = ws[off: off + count * esz].view(tdt)
-                dist.all_reduce(view, op=dist.ReduceOp.SUM, group=group)
-                return 0
-            except Exception:  # never unwind through C
-                return 1
-
-        self._hook = _capi.ALLREDUCE_FN(_hook)
+        self._hook = make_allreduce_hook(lambda: self._ws, group)
         check(lib().rsvd_set_comm(self.h, rank, world, self._hook, None), self.h)
 
     def set_timing(self, enable: bool = True):

@@ -118,20 +118,27 @@ int ensure_ws(rsvd_handle_t h, size_t bytes) {
     return RSVD_OK;
 }
 
-int check_desc(rsvd_handle_t h, const rsvd_desc_t* d) {
-    if (!d) { h->err = "null descriptor"; return RSVD_ERR_INVALID_ARG; }
+int check_desc_msg(const rsvd_desc_t* d, const char** err) {
+    if (!d) { *err = "null descriptor"; return RSVD_ERR_INVALID_ARG; }
     if (d->m <= 0 || d->n <= 0 || d->l <= 0 || d->q < 0 || d->lda < d->m) {
-        h->err = "invalid sizes (need m, n, l > 0, q >= 0, lda >= m)";
+        *err = "invalid sizes (need m, n, l > 0, q >= 0, lda >= m)";
         return RSVD_ERR_INVALID_ARG;
     }
-    if (d->dtype != RSVD_F64 && d->dtype != RSVD_F32) { h->err = "unsupported dtype"; return RSVD_ERR_UNSUPPORTED; }
+    if (d->dtype != RSVD_F64 && d->dtype != RSVD_F32) { *err = "unsupported dtype"; return RSVD_ERR_UNSUPPORTED; }
     if (d->method != RSVD_SVD_JACOBI && d->method != RSVD_SVD_PARALLEL_JACOBI) {
-        h->err = "Unsupported SVD method";  // src/rSVD.cpp:123 wording
+        *err = "Unsupported SVD method";  // src/rSVD.cpp:123 wording
         return RSVD_ERR_UNSUPPORTED;
     }
-    if (d->l > 64) { h->err = "l > 64 not supported yet"; return RSVD_ERR_UNSUPPORTED; }
-    if (d->l > d->n || d->l > d->m) { h->err = "l > min(m, n) not supported"; return RSVD_ERR_UNSUPPORTED; }
+    if (d->l > 64) { *err = "l > 64 not supported yet"; return RSVD_ERR_UNSUPPORTED; }
+    if (d->l > d->n || d->l > d->m) { *err = "l > min(m, n) not supported"; return RSVD_ERR_UNSUPPORTED; }
     return RSVD_OK;
+}
+
+int check_desc(rsvd_handle_t h, const rsvd_desc_t* d) {
+    const char* err = "";
+    const int st = check_desc_msg(d, &err);
+    if (st != RSVD_OK) h->err = err;
+    return st;
 }
 
 // ---- the pipeline ---------------------------------------------------------------------------
@@ -467,6 +474,8 @@ int rsvd_set_comm(rsvd_handle_t h, int rank, int world, rsvd_allreduce_fn fn, vo
 
 int rsvd_workspace_bytes(const rsvd_desc_t* d, size_t* bytes) {
     if (!d || !bytes) return RSVD_ERR_INVALID_ARG;
+    const char* err = "";
+    RSVD_TRY(check_desc_msg(d, &err));
     if (d->dtype == RSVD_F64)
         *bytes = Layout<double>(d->m, d->n, d->l).total;
     else
