@@ -45,16 +45,20 @@ typedef enum {
     RSVD_ERR_COMM = 6            /* the distributed all-reduce callback failed                      */
 } rsvd_status_t;
 
-/* Storage / compute type of A.  F64: fp64 end to end (bit-for-bit the reference's arithmetic
- * class).  F32: fp32 MFMA projections, fp64 Gram/Cholesky/Jacobi. */
+/* Storage / compute type of A.  F64: fp64 end to end (the reference's arithmetic class).
+ * F32: fp32 MFMA projections and fp32 panels; Grams accumulated in fp64 (f64 MFMA), the panel
+ * products by R^-1 in fp64, Cholesky factor and small Jacobi SVD in fp32. */
 typedef enum { RSVD_F64 = 0, RSVD_F32 = 1 } rsvd_dtype_t;
 
 /* Mirrors enum class SVDMethod { Jacobi, Power, ParallelJacobi } (include/SVD_class.hpp:28-32). */
 typedef enum { RSVD_SVD_JACOBI = 0, RSVD_SVD_POWER = 1, RSVD_SVD_PARALLEL_JACOBI = 2 } rsvd_svd_method_t;
 
-/* Orthonormalisation of the tall-skinny panels.  AUTO = CholeskyQR2 with the Householder
- * TSQR fallback when the Cholesky flags ill-conditioning. */
-typedef enum { RSVD_QR_AUTO = 0, RSVD_QR_HOUSEHOLDER = 1, RSVD_QR_CHOLQR2 = 2 } rsvd_qr_mode_t;
+/* Orthonormalisation of the tall-skinny panels.  AUTO = CholeskyQR (one pass for fp32 power-
+ * iteration intermediates, two otherwise) with a predicated Gram-Schmidt (CGS2) re-
+ * orthonormalisation of the panel when a Cholesky pivot breaks down (rank-deficient or too
+ * ill-conditioned sketch).  GS2 = always the CGS2 path (single-GPU panels).
+ * CHOLQR2 = two CholeskyQR passes on every panel. */
+typedef enum { RSVD_QR_AUTO = 0, RSVD_QR_GS2 = 1, RSVD_QR_CHOLQR2 = 2 } rsvd_qr_mode_t;
 
 typedef struct {
     int64_t m, n;              /* A is m x n                                                   */
@@ -70,7 +74,7 @@ typedef struct {
 
 /* Diagnostics of the last run on a handle. */
 typedef struct {
-    int32_t cholqr_fallbacks;  /* panels re-orthonormalised by Householder TSQR                 */
+    int32_t cholqr_fallbacks;  /* panels re-orthonormalised by the CGS2 fallback                 */
     int32_t jacobi_sweeps;     /* sweeps of the small SVD                                      */
     int32_t splits_nn, splits_tn; /* K splits chosen for the projections                         */
 } rsvd_info_t;

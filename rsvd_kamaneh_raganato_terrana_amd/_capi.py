@@ -28,7 +28,7 @@ STATUS = {
 
 F64, F32 = 0, 1
 SVD_JACOBI, SVD_POWER, SVD_PARALLEL_JACOBI = 0, 1, 2
-QR_AUTO, QR_HOUSEHOLDER, QR_CHOLQR2 = 0, 1, 2
+QR_AUTO, QR_GS2, QR_CHOLQR2 = 0, 1, 2
 
 # Every symbol include/rsvd_c.h declares (checked by tests/test_capi_exports.py).
 EXPORTS = (

@@ -33,9 +33,9 @@ class SVDMethod(enum.IntEnum):
 
 
 class QRMode(enum.IntEnum):
-    Auto = 0
-    Householder = 1
-    CholQR2 = 2
+    Auto = 0      # CholeskyQR(2) + predicated CGS2 fallback
+    GS2 = 1       # always CGS2 (robust, slow: one workgroup)
+    CholQR2 = 2   # two CholeskyQR passes on every panel
 
 
 def _dp(a: np.ndarray):

@@ -125,6 +125,7 @@ int check_desc_msg(const rsvd_desc_t* d, const char** err) {
         return RSVD_ERR_INVALID_ARG;
     }
     if (d->dtype != RSVD_F64 && d->dtype != RSVD_F32) { *err = "unsupported dtype"; return RSVD_ERR_UNSUPPORTED; }
+    if (d->qr_mode < RSVD_QR_AUTO || d->qr_mode > RSVD_QR_CHOLQR2) { *err = "bad qr_mode"; return RSVD_ERR_INVALID_ARG; }
     if (d->method != RSVD_SVD_JACOBI && d->method != RSVD_SVD_PARALLEL_JACOBI) {
         *err = "Unsupported SVD method";  // src/rSVD.cpp:123 wording
         return RSVD_ERR_UNSUPPORTED;
@@ -154,6 +155,7 @@ struct Engine {
     // fp32 panels that only carry a subspace (power-iteration intermediates) get one CholeskyQR
     // pass; panels whose basis is an output (final Q, Q_B) and every fp64 panel get two.
     int inter_passes = sizeof(T) == 4 ? 1 : 2;
+    int qr_mode = RSVD_QR_AUTO;
 
     Engine(rsvd_handle_t h_, const Layout<T>& L_) : h(h_), L(L_), s(h_->stream) {
         char* b = h->ws;
@@ -209,6 +211,12 @@ struct Engine {
     int orth(const T* P, int64_t rows, T* Q, bool sharded, int passes) {
         cur_flag = h->dflags + 4 + (orth_index < 12 ? orth_index : 11);
         ++orth_index;
+        if (qr_mode == RSVD_QR_GS2 && !(sharded && h->world > 1)) {  // always the Gram-Schmidt path
+            RSVD_CK(hipMemsetAsync(cur_flag, 0xFF, sizeof(int), s));
+            RSVD_CK(launch_robust_orth<T>(P, rows, L.l, L.LP, Q, cur_flag, 0x5EEDull + orth_index, s));
+            return RSVD_OK;
+        }
+        if (qr_mode == RSVD_QR_CHOLQR2) passes = 2;
         if (passes <= 1) {
             RSVD_TRY(cholqr_pass(P, rows, Q, sharded));
         } else {
@@ -311,6 +319,7 @@ int run_typed(rsvd_handle_t h, const rsvd_desc_t* d, const void* A, const void* 
     h->info.splits_nn = L.pnn.splits;
     h->info.splits_tn = L.ptn.splits;
     Engine<T> E(h, L);
+    E.qr_mode = d->qr_mode;
     RSVD_TRY(E.load_omega(omega, ldo, d->seed));
     if (Qout) {
         RSVD_TRY(E.range_finder(reinterpret_cast<const T*>(A), d->lda, d->q));

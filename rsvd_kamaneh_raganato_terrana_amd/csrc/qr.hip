@@ -20,7 +20,7 @@
 // one workgroup per tile waits for all slabs (bounded spin, agent acquire), sums its tile over
 // the slabs in a FIXED order (bitwise reproducible) and publishes it; the last tile reducer
 // assembles the Gram and (mode 1) factors it: R and R^-1 together by symmetric elimination on
-// [G | I], register-tiled over 256 threads, one barrier per step.
+// [G | I], register-tiled over 256 threads, one barrier per block of 4 pivots.
 #include <algorithm>
 
 #include "common.hpp"
@@ -50,15 +50,141 @@ template <typename C> struct PivTol;
 template <> struct PivTol<double> { static constexpr double v = 1e-10; };
 template <> struct PivTol<float> { static constexpr double v = 1e-6; };
 
-// ---- R = chol(G) and R^-1 together, all 256 threads, one barrier per step ---------------------
+// ---- R = chol(G) and R^-1 together, all 256 threads, one barrier per 4 pivots ----------------
 // Symmetric Gaussian elimination on [G | I]: after step k, row k of G is row k of D L^T and row k
 // of the identity block is row k of L^-1 (G = L D L^T, L unit lower), so
 //     R[k][j]     = M[k][j] / sqrt(M[k][k])        (j >= k)
 //     R^-1[j][k]  = W[k][j] / sqrt(M[k][k])        (j <= k).
 // Thread (ti, tj) of a 16 x 16 grid keeps M[i][j] and W[i][j] for i = ti + 16a, j = tj + 16b in
-// registers (compute type C); row k is published through a double-buffered LDS row.  The padding
-// is treated as [G_ll 0; 0 I]; outputs are zeroed outside the leading l x l block.
-// LDS: rows (4*LP of C), d0 (LP of C), Rs and RIs (LP*LP doubles each).
+// registers (compute type C).  Pivots go in blocks of PB = 4: the owners publish the PB raw block
+// rows (double-buffered LDS), then EVERY thread replays the PB elimination steps of the block on
+// just the columns it needs -- its NB columns j, its NB rows i (by symmetry M[i][k] = M[k][i]) and
+// the PB diagonal-block columns -- and applies the rank-PB update to its registers.  One barrier
+// per block instead of per pivot; the replay is a few dozen redundant FMAs per thread.
+// The padding is treated as [G_ll 0; 0 I]; outputs are zeroed outside the leading l x l block.
+// LDS: rows (2 x 2 x PB x LP of C), d0 (LP of C), Rs and RIs (LP*LP doubles each).
+constexpr int kPivBlock = 4;
+
+// Pivots 16*AK .. 16*AK+15 (four blocks of PB).  AK is a compile-time constant, so the live
+// register tiles are known: rows a < AK are finished, M's columns b < AK are dead, and W's rows
+// are lower triangular (W[k][j] = 0 for j > k) so W only changes in columns b <= AK.
+template <typename C, int LP, int AK>
+__device__ __forceinline__ void chol_group(C (&M)[LP / 16][LP / 16], C (&W)[LP / 16][LP / 16], C* rows,
+                                           const C* d0, double* Rs, double* RIs, int lend, int& buf, bool& bad) {
+    constexpr int NB = LP / 16, PB = kPivBlock;
+    const int tid = threadIdx.x;
+    const int ti = tid >> 4, tj = tid & 15;
+    for (int tk0 = 0; tk0 < 16; tk0 += PB, buf ^= 1) {
+        const int k0 = 16 * AK + tk0;
+        if (k0 >= lend) break;
+        C* PMr = rows + buf * (2 * PB * LP);  // [PB][LP] raw block rows of M
+        C* PWr = PMr + PB * LP;               // [PB][LP] raw block rows of W
+        if (ti >= tk0 && ti < tk0 + PB) {
+            const int t = ti - tk0;
+#pragma unroll
+            for (int b = AK; b < NB; ++b) PMr[t * LP + tj + 16 * b] = M[AK][b];
+#pragma unroll
+            for (int b = 0; b <= AK; ++b) PWr[t * LP + tj + 16 * b] = W[AK][b];
+        }
+        __syncthreads();
+        // replay the block's PB steps on the needed columns (indices b / a below AK are dead)
+        C pm[PB][NB], pr[PB][NB], pd[PB][PB], pw[PB][NB];
+#pragma unroll
+        for (int t = 0; t < PB; ++t) {
+#pragma unroll
+            for (int b = AK; b < NB; ++b) {
+                pm[t][b] = PMr[t * LP + tj + 16 * b];
+                pr[t][b] = PMr[t * LP + ti + 16 * b];
+            }
+#pragma unroll
+            for (int b = 0; b <= AK; ++b) pw[t][b] = PWr[t * LP + tj + 16 * b];
+#pragma unroll
+            for (int u = 0; u < PB; ++u) pd[t][u] = PMr[t * LP + k0 + u];
+        }
+        C fr[PB][NB];
+#pragma unroll
+        for (int t = 0; t < PB; ++t) {
+            const int k = k0 + t;
+            C piv = pd[t][t];
+            const C d0k = d0[k];
+            const bool ok = (piv > (C)PivTol<C>::v * d0k) && (d0k > C(0)) && isfinite(piv);
+            bad |= !ok;
+            piv = ok ? piv : ((d0k > C(0) && isfinite(d0k)) ? d0k : C(1));  // keep going without NaNs; flagged
+            const C inv = rsqrt_c(piv);
+            const C ipiv = inv * inv;
+            if (ti == t) {  // 16 writer threads per pivot row
+                if (Rs) {
+#pragma unroll
+                    for (int b = AK; b < NB; ++b) {
+                        const int j = tj + 16 * b;
+                        Rs[k * LP + j] = (j >= k) ? (double)(pm[t][b] * inv) : 0.0;
+                    }
+                }
+#pragma unroll
+                for (int b = 0; b <= AK; ++b) {
+                    const int j = tj + 16 * b;
+                    RIs[j * LP + k] = (j <= k) ? (double)(pw[t][b] * inv) : 0.0;
+                }
+            }
+            // multipliers of this thread's rows (i > k) for step t
+#pragma unroll
+            for (int a = AK; a < NB; ++a) fr[t][a] = (a > AK || ti > tk0 + t) ? pr[t][a] * ipiv : C(0);
+            // eliminate column k from the later block rows s > t
+#pragma unroll
+            for (int s2 = t + 1; s2 < PB; ++s2) {
+                const C f = pd[t][s2] * ipiv;
+#pragma unroll
+                for (int u = t + 1; u < PB; ++u) pd[s2][u] -= f * pd[t][u];
+                pm[s2][AK] -= (tj > tk0 + t) ? f * pm[t][AK] : C(0);
+                pr[s2][AK] -= (ti > tk0 + t) ? f * pr[t][AK] : C(0);
+#pragma unroll
+                for (int b = AK + 1; b < NB; ++b) {
+                    pm[s2][b] -= f * pm[t][b];
+                    pr[s2][b] -= f * pr[t][b];
+                }
+#pragma unroll
+                for (int b = 0; b <= AK; ++b) pw[s2][b] -= f * pw[t][b];
+            }
+        }
+        // rank-PB update of the live trailing registers
+#pragma unroll
+        for (int a = AK; a < NB; ++a) {
+            {
+                C mv = M[a][AK];
+#pragma unroll
+                for (int t = 0; t < PB; ++t) mv -= (tj > tk0 + t) ? fr[t][a] * pm[t][AK] : C(0);
+                M[a][AK] = mv;
+            }
+#pragma unroll
+            for (int b = AK + 1; b < NB; ++b) {
+                C mv = M[a][b];
+#pragma unroll
+                for (int t = 0; t < PB; ++t) mv -= fr[t][a] * pm[t][b];
+                M[a][b] = mv;
+            }
+#pragma unroll
+            for (int b = 0; b <= AK; ++b) {
+                C wv = W[a][b];
+#pragma unroll
+                for (int t = 0; t < PB; ++t) wv -= fr[t][a] * pw[t][b];
+                W[a][b] = wv;
+            }
+        }
+    }
+}
+
+template <typename C, int LP, int AK>
+__device__ __forceinline__ void chol_groups(C (&M)[LP / 16][LP / 16], C (&W)[LP / 16][LP / 16], C* rows,
+                                            const C* d0, double* Rs, double* RIs, int lend, int& buf, bool& bad) {
+    if constexpr (AK < LP / 16) {
+        if (16 * AK < lend) {
+            chol_group<C, LP, AK>(M, W, rows, d0, Rs, RIs, lend, buf, bad);
+            chol_groups<C, LP, AK + 1>(M, W, rows, d0, Rs, RIs, lend, buf, bad);
+        }
+    }
+}
+
+// Rs may be null (R itself not wanted); RIs always receives R^-1.
 template <typename C, int LP>
 __device__ __forceinline__ bool tile_cholesky_inverse(const double* Gs, C* rows, C* d0, double* Rs, double* RIs,
                                                       int l) {
@@ -75,63 +201,14 @@ __device__ __forceinline__ bool tile_cholesky_inverse(const double* Gs, C* rows,
             W[a][b] = (i == j) ? C(1) : C(0);
         }
     for (int e = tid; e < LP * LP; e += blockDim.x) {
-        Rs[e] = 0.0;
+        if (Rs) Rs[e] = 0.0;
         RIs[e] = 0.0;
     }
     for (int k = tid; k < LP; k += blockDim.x) d0[k] = (k < l) ? (C)Gs[k * LP + k] : C(1);
     bool bad = false;
-    for (int k = 0; k < l; ++k) {
-        C* rowM = rows + (k & 1) * 2 * LP;
-        C* rowW = rowM + LP;
-        const int ak = k >> 4, tk = k & 15;
-        if (ti == tk) {
-#pragma unroll
-            for (int b = 0; b < NB; ++b) {
-                C mv = M[0][b], wv = W[0][b];
-#pragma unroll
-                for (int a = 1; a < NB; ++a) {
-                    mv = (ak == a) ? M[a][b] : mv;
-                    wv = (ak == a) ? W[a][b] : wv;
-                }
-                rowM[tj + 16 * b] = mv;
-                rowW[tj + 16 * b] = wv;
-            }
-        }
-        __syncthreads();
-        C piv = rowM[k];
-        const C d0k = d0[k];
-        const bool ok = (piv > (C)PivTol<C>::v * d0k) && (d0k > C(0)) && isfinite(piv);
-        bad |= !ok;
-        piv = ok ? piv : ((d0k > C(0) && isfinite(d0k)) ? d0k : C(1));  // keep going without NaNs; flagged
-        const C inv = rsqrt_c(piv);
-        const C ipiv = inv * inv;
-        C rj[NB], wj[NB], fi[NB];
-#pragma unroll
-        for (int b = 0; b < NB; ++b) {
-            rj[b] = rowM[tj + 16 * b];
-            wj[b] = rowW[tj + 16 * b];
-            fi[b] = rowM[ti + 16 * b] * ipiv;  // m_ik = M[i][k] / M[k][k] (M symmetric)
-        }
-        if (ti == tk) {
-#pragma unroll
-            for (int b = 0; b < NB; ++b) {
-                const int j = tj + 16 * b;
-                Rs[k * LP + j] = (j >= k) ? (double)(rj[b] * inv) : 0.0;
-                RIs[j * LP + k] = (j <= k) ? (double)(wj[b] * inv) : 0.0;
-            }
-        }
-#pragma unroll
-        for (int a = 0; a < NB; ++a) {
-            const int i = ti + 16 * a;
-            const C f = (i > k) ? fi[a] : C(0);
-#pragma unroll
-            for (int b = 0; b < NB; ++b) {
-                const int j = tj + 16 * b;
-                M[a][b] -= (j > k) ? f * rj[b] : C(0);
-                W[a][b] -= f * wj[b];
-            }
-        }
-    }
+    int buf = 0;
+    const int lend = (l + kPivBlock - 1) / kPivBlock * kPivBlock;  // padded pivots beyond are exact 1s
+    chol_groups<C, LP, 0>(M, W, rows, d0, Rs, RIs, lend, buf, bad);
     __syncthreads();
     return bad;
 }
@@ -161,7 +238,7 @@ __device__ __forceinline__ bool spin_until(unsigned* ctr, unsigned target, int* 
 
 // Doubles of LDS the factorisation phase needs (Gs + Rs + RIs, rows + d0).
 template <int LP>
-constexpr size_t factor_lds_doubles() { return (size_t)3 * LP * LP + 5 * LP; }
+constexpr size_t factor_lds_doubles() { return (size_t)3 * LP * LP + (4 * kPivBlock + 1) * LP; }
 
 // ------------------------------------------------------------------------------------------------
 // grid = max(nb, NT) workgroups.  Phase 1 (blocks < nb): partial Gram of a row block -> slab
@@ -279,8 +356,8 @@ __global__ __launch_bounds__(kWave* kGramWaves) void gram_kernel(
     double* Gs = red;                    // [LP][LP]   (reuses the reduction area)
     double* Rs = Gs + LP * LP;           // [LP][LP]
     double* RIs = Rs + LP * LP;          // [LP][LP]
-    C* prow = reinterpret_cast<C*>(RIs + LP * LP);  // [2][2][LP]
-    C* d0 = prow + 4 * LP;                          // [LP]
+    C* prow = reinterpret_cast<C*>(RIs + LP * LP);  // [2][2][PB][LP]
+    C* d0 = prow + 4 * kPivBlock * LP;              // [LP]
     for (int e = threadIdx.x; e < NT * 256; e += blockDim.x) {
         const double s = tiles[e];
         int t = e >> 8, a = 0, bb;
@@ -304,7 +381,7 @@ __global__ __launch_bounds__(kWave* kGramWaves) void gram_kernel(
         }
         return;
     }
-    const bool bad = tile_cholesky_inverse<C, LP>(Gs, prow, d0, Rs, RIs, l);
+    const bool bad = tile_cholesky_inverse<C, LP>(Gs, prow, d0, Rout ? Rs : nullptr, RIs, l);
     write_factor<LP>(Rs, RIs, l, Rout, Rinv);
     if (threadIdx.x == 0 && bad) atomicAdd(flag, 1);
 }
@@ -318,13 +395,13 @@ __global__ __launch_bounds__(256) void chol_kernel(const double* __restrict__ Gi
     double* Rs = Gs + LP * LP;
     double* RIs = Rs + LP * LP;
     C* prow = reinterpret_cast<C*>(RIs + LP * LP);
-    C* d0 = prow + 4 * LP;
+    C* d0 = prow + 4 * kPivBlock * LP;
     for (int e = threadIdx.x; e < LP * LP; e += blockDim.x) {
         const int row = e / LP, col = e % LP;
         Gs[e] = (row < l && col < l) ? Gin[e] : 0.0;
     }
     __syncthreads();
-    const bool bad = tile_cholesky_inverse<C, LP>(Gs, prow, d0, Rs, RIs, l);
+    const bool bad = tile_cholesky_inverse<C, LP>(Gs, prow, d0, Rout ? Rs : nullptr, RIs, l);
     write_factor<LP>(Rs, RIs, l, Rout, Rinv);
     if (threadIdx.x == 0 && bad) atomicAdd(flag, 1);
 }

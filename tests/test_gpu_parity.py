@@ -128,3 +128,21 @@ def test_duplicate_columns_f32_device(engine):
     assert np.linalg.norm(U.T @ U - np.eye(32)) < 1e-4
     assert np.linalg.norm(V.T @ V - np.eye(32)) < 1e-4
     assert np.linalg.norm(A - (U * S) @ V.T) < 1e-5 * np.linalg.norm(A)
+
+
+@pytest.mark.parametrize("mode", [1, 2])  # QRMode.GS2, QRMode.CholQR2
+def test_qr_modes_agree_with_oracle(engine, mode):
+    import torch
+
+    m, n, l = 400, 300, 24
+    A = gapped_matrix(m, n, 3 * l, decay=0.85, seed=17)
+    Om = oracle.generate_omega(n, l, 4)
+    Uo, So, Vo = oracle.rsvd(A, l, q=2, Omega=Om)
+    At = torch.from_numpy(A).cuda().t().contiguous().t()
+    U, S, V = engine.rsvd(At, l, q=2, omega=torch.from_numpy(Om), qr_mode=mode)
+    torch.cuda.synchronize()
+    U, S, V = U.cpu().numpy(), S.cpu().numpy(), V.cpu().numpy()
+    assert rel_fro(S, So) < 1e-10
+    k = l // 2
+    assert rel_fro(sign_align(U[:, :k], Uo[:, :k]), Uo[:, :k]) < 1e-8
+    assert rel_fro(sign_align(V[:, :k], Vo[:, :k]), Vo[:, :k]) < 1e-8
