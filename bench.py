@@ -54,6 +54,26 @@ def make_A(torch, m_local, n, rank, dtype, rank_cols=128, seed=0x5EED0002):
     return At.to(dtype).t()                                    # m_local x n, column-major view
 
 
+def pmc_traffic(key, kernel_prefix):
+    """HBM bytes per launch of the kernel from the committed rocprofv3 PMC summary for this
+    workload (profiles/*_traffic.json, written by tools/profile.sh + tools/traffic.py; FETCH_SIZE
+    doubled per the gfx950 correction).  None when no summary for this workload exists."""
+    import glob
+
+    best = None
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_traffic.json"))):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if d.get("workload") != key:
+            continue
+        for k, v in d.get("kernels", {}).items():
+            if k.startswith(kernel_prefix):
+                best = (v["hbm_bytes"], os.path.relpath(f, REPO))
+    return best
+
+
 def cpu_baseline(A_host, l, q, flops_total, budget_s, threads):
     import oracle
 
@@ -159,6 +179,8 @@ def main():
     flop_launch = 2.0 * m_local * n * l
     a_bytes = m_local * n * (4 if args.dtype == "f32" else 8)
     achieved = flop_launch / (avg_ms * 1e-3) / 1e12
+    key = f"c2_{args.dtype}_{m_local}x{n}_l{l}_q{q}"
+    tr = pmc_traffic(key, "proj_tn_kernel" if kname.startswith("proj_tn") else "proj_nn_kernel")
     roof = {
         "bound": "mfma",
         "kernel": kname,
@@ -166,7 +188,9 @@ def main():
         "peak": PEAK_TFLOPS[args.dtype],
         "unit": "TFLOP/s",
         "frac": achieved / PEAK_TFLOPS[args.dtype],
-        "traffic": None,
+        "traffic": tr[0] if tr else None,
+        "traffic_unit": "bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)",
+        "traffic_source": tr[1] if tr else None,
         "avg_launch_us": avg_ms * 1e3,
         "algorithmic_flop_per_launch": flop_launch,
         "algorithmic_bytes_per_launch": a_bytes,
