@@ -1,20 +1,26 @@
 #!/usr/bin/env python
 """bench.py -- BASELINE.json metric: "rSVD wall-clock + achieved TFLOP/s, dense m x n rank-k".
 
-Workload (BASELINE.json configs[1], "C2"): dense 4096 x 4096 fp32 A, l = 64, q = 2 power
-iterations, SVDMethod::Jacobi small SVD -- one full rSVD() (src/rSVD.cpp:72-133) per step, A
-resident in HBM before the timed region.  Synthetic A = X diag(0.9^t) Y^T / sqrt(n) + 1e-3 N
-(SURVEY.md §8(d)), X, Y Gaussian with 128 columns.
+One step = one full rSVD() (src/rSVD.cpp:72-133: sketch, q power iterations with a QR after every
+projection, B = Q^T A, its small SVD, U = Q Utilde) on a synthetic A already resident in HBM.
+Synthetic A = X diag(0.9^t) Y^T / sqrt(n) + 1e-3 N, X, Y Gaussian.
 
-N GPUs (torchrun, one process per GPU, RCCL): weak scaling by rows -- rank g owns
-m_per_gpu = 4096 rows of a (4096 N) x 4096 matrix (src/rSVD.cpp:20-23 split); the n-side panels
-are summed with all_reduce and orthonormalised redundantly, U stays row-sharded.
+Configurations (BASELINE.json "configs"; --config, default c2):
+  c2  dense 4096 x 4096 fp32, l = 64, q = 2                       (configs[1], the default line)
+  c3  tall-skinny 1048576 x 1024 bf16, l = 128, q = 1             (configs[2])
+  c4  dense 65536 x 65536 bf16, l = 256, q = 2, rows sharded      (configs[3])
+  c5  131072 x 8192 e4m3 (per-tensor scale), l = 512, q = 2       (configs[4])
+Scaling over N GPUs (torchrun, one process per GPU, RCCL): c2 / c3 are weak-scaled (each rank
+owns m rows, the global matrix is N m x n); c4 / c5 are strong-scaled (the global m x n matrix is
+row-partitioned, src/rSVD.cpp:20-23).  The n-side panels are summed with all_reduce and
+orthonormalised redundantly, U stays row-sharded.
 value = whole-job algorithmic TFLOP/s (F_proj + F_qr + F_small of the global
 problem) / max-over-ranks wall time; ms_per_step = rSVD wall-clock.
 
-Extra fields: "roofline" (the dominant projection kernel, HIP-event timed in a second pass over
-the same K steps), "cpu_baseline" (the fp64 C oracle -- a restatement of the reference, Eigen is
-absent -- on rank 0 at N = 1 on a bounded sample of the same workload).
+Extra fields: "roofline" (the dominant projection kernel, HIP-event timed on the engine's stream
+in a second pass over the same K steps; bound = min(MFMA peak, AI x 8 TB/s) with AI = 2 l /
+bytes per A element), "cpu_baseline" (the fp64 C oracle -- a restatement of the
+reference, Eigen is absent -- on rank 0 at N = 1 on a bounded sample of the same workload).
 """
 from __future__ import annotations
 
@@ -27,9 +33,19 @@ import time
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-# MI355X dense peaks (MI355X_MICROARCH.md): fp32 matrix 157.3 TF/s, fp64 matrix 78.6 TF/s, HBM 8 TB/s.
-PEAK_TFLOPS = {"f32": 157.3, "f64": 78.6}
+# MI355X dense peaks (MI355X_MICROARCH.md): matrix fp32 157.3, fp64 78.6, bf16 2516.6 TF/s (e4m3 A
+# is widened to bf16 in LDS, so its projections run at the bf16 rate); HBM 8 TB/s.
+PEAK_TFLOPS = {"f32": 157.3, "f64": 78.6, "bf16": 2516.6, "fp8": 2516.6}
+ELEM_BYTES = {"f32": 4, "f64": 8, "bf16": 2, "fp8": 1}
 PEAK_HBM_GBS = 8000.0
+
+CONFIGS = {
+    # name: (m, n, l, q, dtype, strong-scaled, cpu sample rows, label)
+    "c2": (4096, 4096, 64, 2, "f32", False, None, "C2: dense 4096x4096 fp32 rSVD, l=64, q=2"),
+    "c3": (1048576, 1024, 128, 1, "bf16", False, 16384, "C3: tall-skinny 1048576x1024 bf16 rSVD, l=128, q=1"),
+    "c4": (65536, 65536, 256, 2, "bf16", True, 2048, "C4: dense 65536x65536 bf16 rSVD, l=256, q=2"),
+    "c5": (131072, 8192, 512, 2, "fp8", True, 8192, "C5: 131072x8192 e4m3 rSVD, l=512, q=2"),
+}
 
 
 def algorithmic_flops(m, n, l, q):
@@ -40,18 +56,35 @@ def algorithmic_flops(m, n, l, q):
     return f_proj, f_qr, f_small
 
 
-def make_A(torch, m_local, n, rank, dtype, rank_cols=128, seed=0x5EED0002):
-    """Column-major rows [rank*m_local, ...) of the synthetic A, built on the GPU."""
+def make_A(torch, m_local, n, row0, dtype, rank_cols=128, seed=0x5EED0002):
+    """Column-major rows [row0, row0 + m_local) of the synthetic A, built on the GPU in row
+    chunks (A^T chunks, n x rows) so the fp32 temporaries stay small.  fp8: A / scale in e4m3 with
+    scale = max|A| / 448 (per tensor), returned with the scale."""
     dev = torch.device("cuda")
     gY = torch.Generator(device=dev).manual_seed(seed)
-    gX = torch.Generator(device=dev).manual_seed(seed + 1 + rank)
-    gN = torch.Generator(device=dev).manual_seed(seed + 7919 + rank)
     sig = 0.9 ** torch.arange(rank_cols, device=dev, dtype=torch.float32)
-    Y = torch.randn(n, rank_cols, generator=gY, device=dev)
-    X = torch.randn(m_local, rank_cols, generator=gX, device=dev)
-    At = (Y * sig) @ X.t() / (n ** 0.5)                       # n x m_local row-major == A^T
-    At += 1e-3 * torch.randn(n, m_local, generator=gN, device=dev)
-    return At.to(dtype).t()                                    # m_local x n, column-major view
+    Ys = torch.randn(n, rank_cols, generator=gY, device=dev) * sig / (n ** 0.5)
+    store = torch.float8_e4m3fn if dtype == "fp8" else {"f32": torch.float32, "f64": torch.float64,
+                                                        "bf16": torch.bfloat16}[dtype]
+    At = torch.empty(m_local, n, dtype=torch.float32 if dtype == "fp8" else store, device=dev)  # rows x n
+    chunk = max(1, min(m_local, (1 << 28) // n))
+    for c0 in range(0, m_local, chunk):
+        c1 = min(m_local, c0 + chunk)
+        g = torch.Generator(device=dev).manual_seed(seed + 1 + row0 + c0)
+        X = torch.randn(c1 - c0, rank_cols, generator=g, device=dev)
+        blk = X @ Ys.t() + 1e-3 * torch.randn(c1 - c0, n, generator=g, device=dev)
+        At[c0:c1] = blk.to(At.dtype)
+        del X, blk
+    # column-major m x n: store A^T row-major
+    if dtype == "fp8":
+        amax = float(At.abs().max())
+        scale = amax / 448.0
+        Acm = (At / scale).t().contiguous().to(store).t()
+        del At
+        return Acm, scale
+    Acm = At.t().contiguous().t()
+    del At
+    return Acm, 1.0
 
 
 def pmc_traffic(key, kernel_prefix):
@@ -74,9 +107,10 @@ def pmc_traffic(key, kernel_prefix):
     return best
 
 
-def cpu_baseline(A_host, l, q, flops_total, budget_s, threads):
+def cpu_baseline(A_host, l, q, budget_s, threads, note):
     import oracle
 
+    m, n = A_host.shape
     used = oracle.set_threads(threads)
     reps, t_all = 0, 0.0
     while reps < 10:
@@ -87,13 +121,14 @@ def cpu_baseline(A_host, l, q, flops_total, budget_s, threads):
         if t_all >= budget_s:
             break
     per = t_all / reps
+    fl = sum(algorithmic_flops(m, n, l, q))
     return {
-        "value": flops_total / per / 1e12,
+        "value": fl / per / 1e12,
         "unit": "TFLOP/s",
         "cores": used,
         "kind": "port",
-        "sample": f"{reps} full rSVD calls of the same {A_host.shape[0]}x{A_host.shape[1]} A (l={l}, q={q}) "
-                  f"in the fp64 C oracle (oracle/rsvd_oracle.c, -O3 -fopenmp); {per * 1e3:.1f} ms per rSVD",
+        "sample": f"{reps} full rSVD calls of a {m}x{n} A (l={l}, q={q}) {note} in the fp64 C oracle "
+                  f"(oracle/rsvd_oracle.c, -O3 -fopenmp); {per * 1e3:.1f} ms per rSVD",
         "ms_per_rsvd": per * 1e3,
     }
 
@@ -103,11 +138,12 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--m-per-gpu", type=int, default=4096)
-    ap.add_argument("--n", type=int, default=4096)
-    ap.add_argument("--l", type=int, default=64)
-    ap.add_argument("--q", type=int, default=2)
-    ap.add_argument("--dtype", default="f32", choices=["f32", "f64"])
+    ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
+    ap.add_argument("--m", type=int, default=None, help="override m (per GPU for weak-scaled configs)")
+    ap.add_argument("--n", type=int, default=None)
+    ap.add_argument("--l", type=int, default=None)
+    ap.add_argument("--q", type=int, default=None)
+    ap.add_argument("--dtype", default=None, choices=["f32", "f64", "bf16", "fp8"])
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU-oracle work (0 = skip)")
     args = ap.parse_args()
 
@@ -116,27 +152,36 @@ def main():
 
     import rsvd_kamaneh_raganato_terrana_amd as R
 
+    cm, cn, cl, cq, cdt, strong, cpu_rows, label = CONFIGS[args.config]
+    m_cfg = args.m or cm
+    n = args.n or cn
+    l = args.l or cl
+    q = cq if args.q is None else args.q
+    dt = args.dtype or cdt
+
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
+    if world == 1 and args.gpus > 1:
+        raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
     torch.cuda.set_device(local_rank)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
 
-    tdt = torch.float32 if args.dtype == "f32" else torch.float64
-    m_local, n, l, q = args.m_per_gpu, args.n, args.l, args.q
-    m_global = m_local * world
-    A = make_A(torch, m_local, n, rank, tdt)
+    if strong:  # global m x n, rows partitioned (src/rSVD.cpp:20-23)
+        m_global = m_cfg
+        m_local, row0 = R.row_partition(m_global, world, rank)
+    else:
+        m_local, row0 = m_cfg, m_cfg * rank
+        m_global = m_cfg * world
+    A, a_scale = make_A(torch, m_local, n, row0, dt)
     eng = R.Engine(local_rank)
     if world > 1:
         eng.set_comm(rank, world)
     torch.cuda.synchronize()
 
     def step():
-        return eng.rsvd(A, l, q=q, seed=0x5EED0002)
+        return eng.rsvd(A, l, q=q, seed=0x5EED0002, a_scale=a_scale)
 
     for _ in range(args.warmup):
         step()
@@ -152,12 +197,12 @@ def main():
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
-        dt = time.perf_counter() - t0
+        dt_s = time.perf_counter() - t0
         if world > 1:
-            t = torch.tensor([dt], device="cuda", dtype=torch.float64)
+            t = torch.tensor([dt_s], device="cuda", dtype=torch.float64)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            dt = float(t.item())
-        return dt
+            dt_s = float(t.item())
+        return dt_s
 
     elapsed = timed(args.steps)
     # pass 2: same K steps with hipEvent pairs around every projection kernel (roofline)
@@ -172,40 +217,52 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     value = f_total * args.steps / elapsed / 1e12
 
-    # dominant projection kernel (per launch: 2 m_local n l flops, m_local n A elements)
+    # dominant projection kernel (per launch: 2 m_local n l flops over m_local n A elements)
     kinds = [("proj_nn (Y = A X)", tm["nn_ms"], tm["nn_launches"]), ("proj_tn (Z = A^T Q)", tm["tn_ms"], tm["tn_launches"])]
     kname, kms, kn = max(kinds, key=lambda x: x[1])
     avg_ms = kms / max(kn, 1)
     flop_launch = 2.0 * m_local * n * l
-    a_bytes = m_local * n * (4 if args.dtype == "f32" else 8)
-    achieved = flop_launch / (avg_ms * 1e-3) / 1e12
-    key = f"c2_{args.dtype}_{m_local}x{n}_l{l}_q{q}"
-    tr = pmc_traffic(key, "proj_tn_kernel" if kname.startswith("proj_tn") else "proj_nn_kernel")
+    a_bytes = m_local * n * ELEM_BYTES[dt]
+    ai = flop_launch / a_bytes
+    t_s = avg_ms * 1e-3
+    if ai * PEAK_HBM_GBS / 1e3 < PEAK_TFLOPS[dt]:  # HBM-bound: AI x 8 TB/s below the MFMA peak
+        bound, achieved, peak, unit = "hbm", a_bytes / t_s / 1e9, PEAK_HBM_GBS, "GB/s"
+    else:
+        bound, achieved, peak, unit = "mfma", flop_launch / t_s / 1e12, PEAK_TFLOPS[dt], "TFLOP/s"
+    key = f"{args.config}_{dt}_{m_local}x{n}_l{l}_q{q}"
+    lowp = dt in ("bf16", "fp8")
+    kpref = "wproj_kernel" if lowp else ("proj_tn_kernel" if kname.startswith("proj_tn") else "proj_nn_kernel")
+    tr = pmc_traffic(key, kpref)
     roof = {
-        "bound": "mfma",
+        "bound": bound,
         "kernel": kname,
         "achieved": achieved,
-        "peak": PEAK_TFLOPS[args.dtype],
-        "unit": "TFLOP/s",
-        "frac": achieved / PEAK_TFLOPS[args.dtype],
+        "peak": peak,
+        "unit": unit,
+        "frac": achieved / peak,
         "traffic": tr[0] if tr else None,
         "traffic_unit": "bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)",
         "traffic_source": tr[1] if tr else None,
         "avg_launch_us": avg_ms * 1e3,
         "algorithmic_flop_per_launch": flop_launch,
         "algorithmic_bytes_per_launch": a_bytes,
-        "achieved_GBps": a_bytes / (avg_ms * 1e-3) / 1e9,
+        "achieved_TFLOPs": flop_launch / t_s / 1e12,
+        "achieved_GBps": a_bytes / t_s / 1e9,
         "launches_timed": kn,
         "proj_share_of_step": (tm["nn_ms"] + tm["tn_ms"]) / (elapsed * 1e3) if elapsed > 0 else None,
     }
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_budget > 0:
-        A_host = A.detach().double().cpu().numpy()
+        rows = m_local if cpu_rows is None else min(cpu_rows, m_local)
+        Ah = A[:rows]
+        Ah = (Ah.float() * a_scale if dt == "fp8" else Ah).double().cpu().numpy()
+        note = "(the full A)" if rows == m_local else f"(the first {rows} rows of the same A: bounded sample)"
         threads = int(os.environ.get("OMP_NUM_THREADS", str(min(16, os.cpu_count() or 1))))
-        cpu = cpu_baseline(A_host, l, q, f_total, args.cpu_budget, threads)
+        cpu = cpu_baseline(Ah, l, q, args.cpu_budget, threads, note)
 
     if rank == 0:
+        par = "single-gpu" if world == 1 else (f"row-partition x{world}" if strong else f"row-shard x{world}")
         line = {
             "metric": "rSVD wall-clock + achieved TFLOP/s, dense m x n rank-k",
             "value": value,
@@ -215,15 +272,14 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": ms_per_step,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if strong else "weak",
             "vs_baseline": None,
-            "dtype": args.dtype,
+            "dtype": dt,
             "data": "synthetic",
             "config": {
-                "workload": f"C2: dense {m_global}x{n} {args.dtype} rSVD, l={l}, q={q}, Jacobi small SVD"
-                            + (f", rows sharded {m_local}/GPU" if world > 1 else ""),
+                "workload": label + (f"; {m_global}x{n} global, {m_local} rows/GPU" if world > 1 else ""),
                 "m": m_global, "n": n, "l": l, "q": q, "m_per_gpu": m_local,
-                "parallelism": f"row-shard x{world}" if world > 1 else "single-gpu",
+                "parallelism": par,
                 "algorithmic_tflop_per_step": f_total / 1e12,
             },
             "roofline": roof,

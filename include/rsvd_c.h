@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define RSVD_ABI_VERSION 1
+#define RSVD_ABI_VERSION 2
 
 typedef enum {
     RSVD_OK = 0,
@@ -47,8 +47,12 @@ typedef enum {
 
 /* Storage / compute type of A.  F64: fp64 end to end (the reference's arithmetic class).
  * F32: fp32 MFMA projections and fp32 panels; Grams accumulated in fp64 (f64 MFMA), the panel
- * products by R^-1 in fp64, Cholesky factor and small Jacobi SVD in fp32. */
-typedef enum { RSVD_F64 = 0, RSVD_F32 = 1 } rsvd_dtype_t;
+ * products by R^-1 in fp64, Cholesky factor and small Jacobi SVD in fp32.
+ * BF16 / FP8_E4M3 (OCP e4m3fn): A stored in that type (A = a_scale * stored value), projections
+ * on the bf16 MFMA with a hi/lo-split fp32 skinny operand, fp32 panels, fp64 Grams / Cholesky /
+ * small SVD; Omega is the Philox Gaussian rounded to bf16 (resp. e4m3); U, S, V, Omega and Q are
+ * fp32 at the ABI. */
+typedef enum { RSVD_F64 = 0, RSVD_F32 = 1, RSVD_BF16 = 2, RSVD_FP8_E4M3 = 3 } rsvd_dtype_t;
 
 /* Mirrors enum class SVDMethod { Jacobi, Power, ParallelJacobi } (include/SVD_class.hpp:28-32). */
 typedef enum { RSVD_SVD_JACOBI = 0, RSVD_SVD_POWER = 1, RSVD_SVD_PARALLEL_JACOBI = 2 } rsvd_svd_method_t;
@@ -70,6 +74,7 @@ typedef struct {
     int32_t qr_mode;           /* rsvd_qr_mode_t                                               */
     int32_t reserved;
     uint64_t seed;             /* Philox key for Omega when no Omega is supplied               */
+    double a_scale;            /* A = a_scale * (stored A); 0 means 1 (used for FP8_E4M3)      */
 } rsvd_desc_t;
 
 /* Diagnostics of the last run on a handle. */
@@ -118,8 +123,10 @@ int rsvd_set_workspace(rsvd_handle_t h, void *ptr, size_t bytes);
 
 /* ---- device-pointer entry points (asynchronous on the handle stream) ---------------------- */
 
-/* rSVD: U (m x d, ldu), S (d), V (n x d, ldv), d = min(l, n); element type = desc->dtype.
- * omega: optional n x l column-major (ld = ldo) sketch; NULL => Philox(desc->seed). */
+/* rSVD: U (m x d, ldu), S (d), V (n x d, ldv), d = min(l, n); element type = desc->dtype (fp32
+ * for BF16 / FP8_E4M3).  omega: optional n x l column-major (ld = ldo) sketch in that element
+ * type (rounded to bf16 / e4m3 for the low-precision types); NULL => Philox(desc->seed).
+ * l <= 512. */
 int rsvd_run(rsvd_handle_t h, const rsvd_desc_t *desc, const void *A, const void *omega, int64_t ldo,
              void *U, int64_t ldu, void *S, void *V, int64_t ldv);
 
@@ -127,7 +134,9 @@ int rsvd_run(rsvd_handle_t h, const rsvd_desc_t *desc, const void *A, const void
 int rsvd_range_finder(rsvd_handle_t h, const rsvd_desc_t *desc, const void *A, const void *omega, int64_t ldo,
                       void *Q, int64_t ldq);
 
-/* generateOmega: n x l N(0,1), column-major (ld = n), element (i,j) = Philox stream element i+n*j. */
+/* generateOmega: n x l N(0,1), column-major (ld = n), element (i,j) = Philox stream element i+n*j.
+ * dtype BF16 / FP8_E4M3: the same values rounded to bf16 / e4m3 (round half to even; e4m3
+ * saturates at +-448), written as fp32 -- the Omega the low-precision rsvd_run draws. */
 int rsvd_generate_omega(rsvd_handle_t h, int64_t n, int32_t l, uint64_t seed, int32_t dtype, void *omega);
 
 /* ---- host-pointer fp64 entry points used by the C++ drop-in headers (synchronous) --------- */

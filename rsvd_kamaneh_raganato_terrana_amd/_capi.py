@@ -26,7 +26,7 @@ STATUS = {
     6: "communication failure",
 }
 
-F64, F32 = 0, 1
+F64, F32, BF16, FP8_E4M3 = 0, 1, 2, 3
 SVD_JACOBI, SVD_POWER, SVD_PARALLEL_JACOBI = 0, 1, 2
 QR_AUTO, QR_GS2, QR_CHOLQR2 = 0, 1, 2
 
@@ -45,7 +45,7 @@ class Desc(ctypes.Structure):
         ("m", ctypes.c_int64), ("n", ctypes.c_int64), ("lda", ctypes.c_int64),
         ("l", ctypes.c_int32), ("q", ctypes.c_int32), ("dtype", ctypes.c_int32),
         ("method", ctypes.c_int32), ("qr_mode", ctypes.c_int32), ("reserved", ctypes.c_int32),
-        ("seed", ctypes.c_uint64),
+        ("seed", ctypes.c_uint64), ("a_scale", ctypes.c_double),
     ]
 
 

@@ -10,8 +10,9 @@ Reference signatures mirrored (AMSC22-23/rSVD_Kamaneh_Raganato_Terrana):
 * ``SVDMethod`` (Jacobi, Power, ParallelJacobi)           include/SVD_class.hpp:28-32
 
 numpy float64 inputs take the synchronous fp64 host path (the drop-in the reference's Eigen
-callers see); torch CUDA tensors (float32 / float64) take the asynchronous device path on the
-current torch stream, with A resident in HBM.  There is no CPU fallback: without the HIP
+callers see); torch CUDA tensors (float64 / float32 / bfloat16 / float8_e4m3fn) take the
+asynchronous device path on the current torch stream, with A resident in HBM (bf16 / fp8 A return
+fp32 U, S, V; fp8 A carries a per-tensor scale, A = a_scale * stored).  There is no CPU fallback: without the HIP
 library or a GPU these functions raise.
 """
 from __future__ import annotations
@@ -158,37 +159,50 @@ class Engine:
         return {k: getattr(inf, k) for k, _ in Info._fields_}
 
     # -- device path -----------------------------------------------------------------------
-    def desc(self, A, l: int, q: int = 2, method: int = SVDMethod.Jacobi, seed: int = 0,
-             qr_mode: int = QRMode.Auto) -> Desc:
+    @staticmethod
+    def abi_dtype(t_dtype) -> int:
         torch = _torch()
-        dt = {torch.float64: _capi.F64, torch.float32: _capi.F32}.get(A.dtype)
+        dt = {torch.float64: _capi.F64, torch.float32: _capi.F32, torch.bfloat16: _capi.BF16,
+              torch.float8_e4m3fn: _capi.FP8_E4M3}.get(t_dtype)
         if dt is None:
-            raise TypeError(f"unsupported dtype {A.dtype}")
+            raise TypeError(f"unsupported dtype {t_dtype}")
+        return dt
+
+    @staticmethod
+    def out_dtype(t_dtype):
+        """Element type of U, S, V, Omega and Q for an A of this dtype (fp32 for bf16 / fp8)."""
+        torch = _torch()
+        return t_dtype if t_dtype in (torch.float64, torch.float32) else torch.float32
+
+    def desc(self, A, l: int, q: int = 2, method: int = SVDMethod.Jacobi, seed: int = 0,
+             qr_mode: int = QRMode.Auto, a_scale: float = 1.0) -> Desc:
+        dt = self.abi_dtype(A.dtype)
         lda = A.stride(1) if A.stride(0) == 1 else None
         if lda is None:
             raise ValueError("A must be column-major (use colmajor())")
         return Desc(m=A.shape[0], n=A.shape[1], lda=max(lda, A.shape[0]), l=l, q=q, dtype=dt,
-                    method=int(method), qr_mode=int(qr_mode), reserved=0, seed=seed)
+                    method=int(method), qr_mode=int(qr_mode), reserved=0, seed=seed, a_scale=a_scale)
 
     def rsvd(self, A, l: int, q: int = 2, method: int = SVDMethod.Jacobi, omega=None, seed: int = 0,
-             qr_mode: int = QRMode.Auto, out=None):
-        """Device rSVD: A (m x n, CUDA, column-major f32/f64) -> U (m x l), S (l), V (n x l)."""
+             qr_mode: int = QRMode.Auto, out=None, a_scale: float = 1.0):
+        """Device rSVD: A (m x n, CUDA, column-major f64/f32/bf16/e4m3) -> U (m x l), S (l), V (n x l)."""
         torch = _torch()
         A, _ = colmajor(A)
-        d = self.desc(A, l, q, method, seed, qr_mode)
+        d = self.desc(A, l, q, method, seed, qr_mode, a_scale)
         self.reserve(d)
         self._bind_stream()
         m, n = A.shape
         dd = min(l, n)
+        odt = self.out_dtype(A.dtype)
         if out is None:
-            U = empty_colmajor(m, dd, A.dtype, A.device)
-            S = torch.empty(dd, dtype=A.dtype, device=A.device)
-            V = empty_colmajor(n, dd, A.dtype, A.device)
+            U = empty_colmajor(m, dd, odt, A.device)
+            S = torch.empty(dd, dtype=odt, device=A.device)
+            V = empty_colmajor(n, dd, odt, A.device)
         else:
             U, S, V = out
         om, ldo = (None, 0)
         if omega is not None:
-            om, ldo = colmajor(omega.to(device=A.device, dtype=A.dtype))
+            om, ldo = colmajor(omega.to(device=A.device, dtype=odt))
         check(lib().rsvd_run(self.h, ctypes.byref(d), ctypes.c_void_p(A.data_ptr()),
                              ctypes.c_void_p(om.data_ptr() if om is not None else 0), ldo,
                              ctypes.c_void_p(U.data_ptr()), U.stride(1),
@@ -197,26 +211,31 @@ class Engine:
         return U, S, V
 
     def range_finder(self, A, omega, q: int = 2, qr_mode: int = QRMode.Auto):
-        torch = _torch()
         A, _ = colmajor(A)
-        om, ldo = colmajor(omega.to(device=A.device, dtype=A.dtype))
+        odt = self.out_dtype(A.dtype)
+        om, ldo = colmajor(omega.to(device=A.device, dtype=odt))
         l = om.shape[1]
         d = self.desc(A, l, q, SVDMethod.Jacobi, 0, qr_mode)
         self.reserve(d)
         self._bind_stream()
-        Q = empty_colmajor(A.shape[0], l, A.dtype, A.device)
+        Q = empty_colmajor(A.shape[0], l, odt, A.device)
         check(lib().rsvd_range_finder(self.h, ctypes.byref(d), ctypes.c_void_p(A.data_ptr()),
                                       ctypes.c_void_p(om.data_ptr()), ldo, ctypes.c_void_p(Q.data_ptr()),
                                       Q.stride(1)), self.h)
         return Q
 
     def generate_omega(self, n: int, l: int, seed: int = 0, dtype=None):
+        """Omega on the device.  dtype bfloat16 / float8_e4m3fn: the Omega those A types draw
+        (Philox values rounded to bf16 / e4m3), returned as float32."""
         torch = _torch()
         dtype = dtype or torch.float64
-        self._reserve_bytes(n * ((l + 15) // 16 * 16) * 8)
+        lp = 16
+        while lp < l:
+            lp *= 2
+        self._reserve_bytes(n * lp * 8)
         self._bind_stream()
-        Om = empty_colmajor(n, l, dtype, f"cuda:{self.device}")
-        check(lib().rsvd_generate_omega(self.h, n, l, seed, _capi.F64 if dtype == torch.float64 else _capi.F32,
+        Om = empty_colmajor(n, l, self.out_dtype(dtype), f"cuda:{self.device}")
+        check(lib().rsvd_generate_omega(self.h, n, l, seed, self.abi_dtype(dtype),
                                         ctypes.c_void_p(Om.data_ptr())), self.h)
         return Om
 

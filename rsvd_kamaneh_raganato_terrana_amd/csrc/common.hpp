@@ -76,4 +76,32 @@ __device__ __forceinline__ double warp_sum(double v) {
     return v;
 }
 
+// Counter-based Philox4x32-10 Gaussian stream shared by every GPU and the CPU oracle
+// (oracle/rsvd_oracle.c orc_philox_gaussian): element e of the stream keyed by `seed`.
+__device__ __forceinline__ void philox4x32_10(uint64_t ctr, uint64_t seed, uint32_t out[4]) {
+    uint32_t c0 = (uint32_t)ctr, c1 = (uint32_t)(ctr >> 32), c2 = 0x52535644u, c3 = 0u;
+    uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint32_t hi0 = __umulhi(0xD2511F53u, c0), lo0 = 0xD2511F53u * c0;
+        const uint32_t hi1 = __umulhi(0xCD9E8D57u, c2), lo1 = 0xCD9E8D57u * c2;
+        const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+        c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    out[0] = c0; out[1] = c1; out[2] = c2; out[3] = c3;
+}
+
+__device__ __forceinline__ double gauss_elem(uint64_t e, uint64_t seed) {
+    uint32_t x[4];
+    philox4x32_10(e >> 1, seed, x);
+    const double two_m53 = 1.1102230246251565404e-16;
+    const double u1 = ((double)(((uint64_t)(x[0] >> 5) << 26) | (x[1] >> 6)) + 0.5) * two_m53;
+    const double u2 = ((double)(((uint64_t)(x[2] >> 5) << 26) | (x[3] >> 6)) + 0.5) * two_m53;
+    const double rr = sqrt(-2.0 * log(u1));
+    const double th = 6.283185307179586476925286766559 * u2;
+    return (e & 1) ? rr * sin(th) : rr * cos(th);
+}
+
 }  // namespace rsvd

@@ -25,51 +25,13 @@
 #include <vector>
 
 #include "../../include/rsvd_c.h"
+#include "handle.hpp"
 #include "kernels.hpp"
+#include "wide.hpp"
 
 using namespace rsvd;
 
-struct rsvd_handle_s {
-    int device = 0;
-    hipStream_t stream = nullptr;
-    bool own_stream = false;
-    std::string err;
-    char* ws = nullptr;
-    size_t ws_bytes = 0;
-    bool ws_external = false;  // workspace supplied by the caller (rsvd_set_workspace)
-    int* dflags = nullptr;  // [0] cholqr breakdown count, [1] jacobi sweeps
-    rsvd_info_t info{};
-    int rank = 0, world = 1;
-    rsvd_allreduce_fn allreduce = nullptr;
-    void* ar_user = nullptr;
-    // timing mode: hipEvent pairs around every projection kernel (kind 0 = A*X, 1 = A^T*Q)
-    bool timing = false;
-    std::vector<hipEvent_t> ev_pool;
-    std::vector<std::pair<int, int>> ev_used;  // (kind, first event index)
-    size_t ev_next = 0;
-    double acc_ms[2] = {0.0, 0.0};
-    int acc_n[2] = {0, 0};
-};
-
 namespace {
-
-#define RSVD_CK(expr)                                                                         \
-    do {                                                                                      \
-        hipError_t _e = (expr);                                                               \
-        if (_e != hipSuccess) {                                                               \
-            h->err = std::string(#expr) + ": " + hipGetErrorString(_e);                       \
-            return RSVD_ERR_HIP;                                                              \
-        }                                                                                     \
-    } while (0)
-
-#define RSVD_TRY(expr)                   \
-    do {                                 \
-        int _s = (expr);                 \
-        if (_s != RSVD_OK) return _s;    \
-    } while (0)
-
-inline int lp_of(int l) { return (l + 15) / 16 * 16; }
-inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
 template <typename T>
 struct Layout {
@@ -101,36 +63,19 @@ struct Layout {
     }
 };
 
-int ensure_ws(rsvd_handle_t h, size_t bytes) {
-    if (bytes <= h->ws_bytes) return RSVD_OK;
-    if (h->ws_external) {
-        h->err = "caller workspace too small: need " + std::to_string(bytes) + " bytes";
-        return RSVD_ERR_INVALID_ARG;
-    }
-    if (h->ws) {
-        RSVD_CK(hipStreamSynchronize(h->stream));
-        RSVD_CK(hipFree(h->ws));
-        h->ws = nullptr;
-        h->ws_bytes = 0;
-    }
-    RSVD_CK(hipMalloc(&h->ws, bytes));
-    h->ws_bytes = bytes;
-    return RSVD_OK;
-}
-
 int check_desc_msg(const rsvd_desc_t* d, const char** err) {
     if (!d) { *err = "null descriptor"; return RSVD_ERR_INVALID_ARG; }
     if (d->m <= 0 || d->n <= 0 || d->l <= 0 || d->q < 0 || d->lda < d->m) {
         *err = "invalid sizes (need m, n, l > 0, q >= 0, lda >= m)";
         return RSVD_ERR_INVALID_ARG;
     }
-    if (d->dtype != RSVD_F64 && d->dtype != RSVD_F32) { *err = "unsupported dtype"; return RSVD_ERR_UNSUPPORTED; }
+    if (d->dtype < RSVD_F64 || d->dtype > RSVD_FP8_E4M3) { *err = "unsupported dtype"; return RSVD_ERR_UNSUPPORTED; }
     if (d->qr_mode < RSVD_QR_AUTO || d->qr_mode > RSVD_QR_CHOLQR2) { *err = "bad qr_mode"; return RSVD_ERR_INVALID_ARG; }
     if (d->method != RSVD_SVD_JACOBI && d->method != RSVD_SVD_PARALLEL_JACOBI) {
         *err = "Unsupported SVD method";  // src/rSVD.cpp:123 wording
         return RSVD_ERR_UNSUPPORTED;
     }
-    if (d->l > 64) { *err = "l > 64 not supported yet"; return RSVD_ERR_UNSUPPORTED; }
+    if (d->l > 512) { *err = "l > 512 not supported"; return RSVD_ERR_UNSUPPORTED; }
     if (d->l > d->n || d->l > d->m) { *err = "l > min(m, n) not supported"; return RSVD_ERR_UNSUPPORTED; }
     return RSVD_OK;
 }
@@ -421,6 +366,10 @@ int rsvd_get_info(rsvd_handle_t h, rsvd_info_t* info) {
         h->err = "a Gram reduction timed out waiting for its producers";
         return RSVD_ERR_HIP;
     }
+    if (flags[3]) {
+        h->err = "the block Jacobi grid barrier timed out";
+        return RSVD_ERR_HIP;
+    }
     int fallbacks = 0;
     for (int k = 4; k < 16; ++k) fallbacks += flags[k] != 0;
     h->info.cholqr_fallbacks = fallbacks;
@@ -485,6 +434,7 @@ int rsvd_workspace_bytes(const rsvd_desc_t* d, size_t* bytes) {
     if (!d || !bytes) return RSVD_ERR_INVALID_ARG;
     const char* err = "";
     RSVD_TRY(check_desc_msg(d, &err));
+    if (wide_path(d)) return wide_workspace_bytes(d, bytes);
     if (d->dtype == RSVD_F64)
         *bytes = Layout<double>(d->m, d->n, d->l).total;
     else
@@ -501,6 +451,7 @@ int rsvd_run(rsvd_handle_t h, const rsvd_desc_t* d, const void* A, const void* o
         return RSVD_ERR_INVALID_ARG;
     }
     RSVD_TRY(set_device(h));
+    if (wide_path(d)) return wide_run(h, d, A, omega, ldo, U, ldu, S, V, ldv, nullptr, 0);
     if (d->dtype == RSVD_F64) return run_typed<double>(h, d, A, omega, ldo, U, ldu, S, V, ldv, nullptr, 0);
     return run_typed<float>(h, d, A, omega, ldo, U, ldu, S, V, ldv, nullptr, 0);
 }
@@ -514,6 +465,7 @@ int rsvd_range_finder(rsvd_handle_t h, const rsvd_desc_t* d, const void* A, cons
         return RSVD_ERR_INVALID_ARG;
     }
     RSVD_TRY(set_device(h));
+    if (wide_path(d)) return wide_run(h, d, A, omega, ldo, nullptr, 0, nullptr, nullptr, 0, Q, ldq);
     if (d->dtype == RSVD_F64) return run_typed<double>(h, d, A, omega, ldo, nullptr, 0, nullptr, nullptr, 0, Q, ldq);
     return run_typed<float>(h, d, A, omega, ldo, nullptr, 0, nullptr, nullptr, 0, Q, ldq);
 }
@@ -534,6 +486,11 @@ int rsvd_generate_omega(rsvd_handle_t h, int64_t n, int32_t l, uint64_t seed, in
         RSVD_CK(launch_philox_omega<float>(reinterpret_cast<float*>(h->ws), n, l, LP, seed, h->stream));
         RSVD_CK(launch_panel_to_colmajor<float>(reinterpret_cast<float*>(h->ws), n, l, LP,
                                                 reinterpret_cast<float*>(omega), n, h->stream));
+    } else if (dtype == RSVD_BF16 || dtype == RSVD_FP8_E4M3) {
+        // the Omega of the low-precision paths: Philox values rounded to bf16 / e4m3, as fp32
+        RSVD_TRY(ensure_ws(h, (size_t)n * LP * 2));
+        RSVD_CK(launch_omega_lowp(reinterpret_cast<bf16_t*>(h->ws), n, l, LP, seed, dtype == RSVD_FP8_E4M3,
+                                  reinterpret_cast<float*>(omega), h->stream));
     } else {
         return RSVD_ERR_UNSUPPORTED;
     }

@@ -1,0 +1,69 @@
+// handle.hpp -- the rsvd handle (one GPU + stream + workspace) shared by the narrow engine
+// (driver.cpp) and the wide engine (wide.cpp).  Private to librsvd_hip.so.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "../../include/rsvd_c.h"
+
+struct rsvd_handle_s {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    std::string err;
+    char* ws = nullptr;
+    size_t ws_bytes = 0;
+    bool ws_external = false;  // workspace supplied by the caller (rsvd_set_workspace)
+    int* dflags = nullptr;  // [0] cholqr breakdown count, [1] jacobi sweeps
+    rsvd_info_t info{};
+    int rank = 0, world = 1;
+    rsvd_allreduce_fn allreduce = nullptr;
+    void* ar_user = nullptr;
+    // timing mode: hipEvent pairs around every projection kernel (kind 0 = A*X, 1 = A^T*Q)
+    bool timing = false;
+    std::vector<hipEvent_t> ev_pool;
+    std::vector<std::pair<int, int>> ev_used;  // (kind, first event index)
+    size_t ev_next = 0;
+    double acc_ms[2] = {0.0, 0.0};
+    int acc_n[2] = {0, 0};
+};
+
+#define RSVD_CK(expr)                                                                         \
+    do {                                                                                      \
+        hipError_t _e = (expr);                                                               \
+        if (_e != hipSuccess) {                                                               \
+            h->err = std::string(#expr) + ": " + hipGetErrorString(_e);                       \
+            return RSVD_ERR_HIP;                                                              \
+        }                                                                                     \
+    } while (0)
+
+#define RSVD_TRY(expr)                   \
+    do {                                 \
+        int _s = (expr);                 \
+        if (_s != RSVD_OK) return _s;    \
+    } while (0)
+
+inline int lp_of(int l) { return (l + 15) / 16 * 16; }
+inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
+
+inline int ensure_ws(rsvd_handle_t h, size_t bytes) {
+    if (bytes <= h->ws_bytes) return RSVD_OK;
+    if (h->ws_external) {
+        h->err = "caller workspace too small: need " + std::to_string(bytes) + " bytes";
+        return RSVD_ERR_INVALID_ARG;
+    }
+    if (h->ws) {
+        RSVD_CK(hipStreamSynchronize(h->stream));
+        RSVD_CK(hipFree(h->ws));
+        h->ws = nullptr;
+        h->ws_bytes = 0;
+    }
+    RSVD_CK(hipMalloc(&h->ws, bytes));
+    h->ws_bytes = bytes;
+    return RSVD_OK;
+}
+

@@ -47,7 +47,7 @@ __device__ __forceinline__ typename Vec16<T>::type load_vec_guarded(const T* __r
 template <typename T, int LP>
 __global__ __launch_bounds__(kWave* kWaves) void proj_nn_kernel(
     const T* __restrict__ A, int64_t lda, int64_t m, int64_t n, const T* __restrict__ X,
-    T* __restrict__ out, int64_t slab_stride, int64_t kchunk, int nrowblk, int vec_ok) {
+    T* __restrict__ out, int64_t slab_stride, int64_t kchunk, int nrowblk, int vec_ok, int ldp) {
     typedef Mfma<T> M;
     typedef typename M::acc_t acc_t;
     typedef typename Vec16<T>::type V;
@@ -78,7 +78,7 @@ __global__ __launch_bounds__(kWave* kWaves) void proj_nn_kernel(
         T b[G];
         if (k < kend) {
             a = load_vec_guarded<T>(A + k * lda, row, m, vec_ok);
-            const T* xr = X + k * LP + r;
+            const T* xr = X + k * ldp + r;
 #pragma unroll
             for (int g = 0; g < G; ++g) b[g] = xr[16 * g];
         } else {
@@ -120,7 +120,7 @@ __global__ __launch_bounds__(kWave* kWaves) void proj_nn_kernel(
             for (int t = 0; t < VW; ++t) sp[t] += op[t];
         }
         const int lr = e / LP;
-        if (i0 + lr < m) *reinterpret_cast<V*>(dst + (i0 + lr) * LP + (e % LP)) = sum;
+        if (i0 + lr < m) *reinterpret_cast<V*>(dst + (i0 + lr) * ldp + (e % LP)) = sum;
     }
 }
 
@@ -128,7 +128,7 @@ __global__ __launch_bounds__(kWave* kWaves) void proj_nn_kernel(
 template <typename T, int LP, int JT>
 __global__ __launch_bounds__(kWave* kWaves) void proj_tn_kernel(
     const T* __restrict__ A, int64_t lda, int64_t m, int64_t n, const T* __restrict__ Q,
-    T* __restrict__ out, int64_t slab_stride, int64_t ichunk, int ncolblk, int vec_ok) {
+    T* __restrict__ out, int64_t slab_stride, int64_t ichunk, int ncolblk, int vec_ok, int ldp) {
     typedef Mfma<T> M;
     typedef typename M::acc_t acc_t;
     typedef typename Vec16<T>::type V;
@@ -172,7 +172,7 @@ __global__ __launch_bounds__(kWave* kWaves) void proj_tn_kernel(
             const int64_t i = ib + t;
             T b[G];
             if (i < iend) {
-                const T* qr = Q + i * LP + r;
+                const T* qr = Q + i * ldp + r;
 #pragma unroll
                 for (int g = 0; g < G; ++g) b[g] = qr[16 * g];
             } else {
@@ -208,7 +208,7 @@ __global__ __launch_bounds__(kWave* kWaves) void proj_tn_kernel(
             for (int t = 0; t < VW; ++t) sp[t] += op[t];
         }
         const int lr = e / LP;
-        if (j0 + lr < n) *reinterpret_cast<V*>(dst + (j0 + lr) * LP + (e % LP)) = sum;
+        if (j0 + lr < n) *reinterpret_cast<V*>(dst + (j0 + lr) * ldp + (e % LP)) = sum;
     }
 }
 
@@ -229,39 +229,49 @@ ProjPlan make_plan(int64_t K, int blocks, int64_t kstep_wg) {
     return p;
 }
 
+// ldp = panel row stride; ldp > LP runs the kernel once per LP-wide column group (wide sketches
+// on fp32 / fp64 A: A is re-read ldp / LP times) and reduces all groups' slabs in one pass.
 template <typename T, int LP>
 hipError_t nn_dispatch(const T* A, int64_t lda, int64_t m, int64_t n, const T* X, const ProjPlan& p,
-                       T* slabs, T* Y, hipStream_t s, hipEvent_t done) {
+                       T* slabs, T* Y, hipStream_t s, hipEvent_t done, int ldp) {
     constexpr int VW = Vec16<T>::N;
     constexpr int WR = 16 * VW;
     const size_t lds = (size_t)kWaves * WR * LP * sizeof(T);
     T* out = (p.splits == 1) ? Y : slabs;
-    const int64_t stride = m * LP;
+    const int64_t stride = m * ldp;
     const int vec_ok = (lda % VW == 0) && ((reinterpret_cast<uintptr_t>(A) & 15) == 0);
-    hipLaunchKernelGGL((proj_nn_kernel<T, LP>), dim3(p.blocks * p.splits), dim3(kWave * kWaves), lds, s, A,
-                       lda, m, n, X, out, stride, p.chunk, p.blocks, vec_ok);
-    hipError_t e = hipGetLastError();
-    if (e == hipSuccess && done) e = hipEventRecord(done, s);
+    for (int c0 = 0; c0 < ldp; c0 += LP) {
+        hipLaunchKernelGGL((proj_nn_kernel<T, LP>), dim3(p.blocks * p.splits), dim3(kWave * kWaves), lds, s, A,
+                           lda, m, n, X + c0, out + c0, stride, p.chunk, p.blocks, vec_ok, ldp);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    hipError_t e = hipSuccess;
+    if (done) e = hipEventRecord(done, s);
     if (e != hipSuccess || p.splits == 1) return e;
-    return launch_sum_slabs<T>(slabs, stride, p.splits, m * LP, Y, s);
+    return launch_sum_slabs<T>(slabs, stride, p.splits, m * ldp, Y, s);
 }
 
 template <typename T, int LP>
 hipError_t tn_dispatch(const T* A, int64_t lda, int64_t m, int64_t n, const T* Q, const ProjPlan& p,
-                       T* slabs, T* Z, hipStream_t s, hipEvent_t done) {
+                       T* slabs, T* Z, hipStream_t s, hipEvent_t done, int ldp) {
     constexpr int VW = Vec16<T>::N;
     constexpr int JT = 2;
     constexpr int WJ = 16 * JT;
     const size_t lds = (size_t)kWaves * WJ * LP * sizeof(T);
     T* out = (p.splits == 1) ? Z : slabs;
-    const int64_t stride = n * LP;
+    const int64_t stride = n * ldp;
     const int vec_ok = (lda % VW == 0) && ((reinterpret_cast<uintptr_t>(A) & 15) == 0);
-    hipLaunchKernelGGL((proj_tn_kernel<T, LP, JT>), dim3(p.blocks * p.splits), dim3(kWave * kWaves), lds, s,
-                       A, lda, m, n, Q, out, stride, p.chunk, p.blocks, vec_ok);
-    hipError_t e = hipGetLastError();
-    if (e == hipSuccess && done) e = hipEventRecord(done, s);
+    for (int c0 = 0; c0 < ldp; c0 += LP) {
+        hipLaunchKernelGGL((proj_tn_kernel<T, LP, JT>), dim3(p.blocks * p.splits), dim3(kWave * kWaves), lds, s,
+                           A, lda, m, n, Q + c0, out + c0, stride, p.chunk, p.blocks, vec_ok, ldp);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    hipError_t e = hipSuccess;
+    if (done) e = hipEventRecord(done, s);
     if (e != hipSuccess || p.splits == 1) return e;
-    return launch_sum_slabs<T>(slabs, stride, p.splits, n * LP, Z, s);
+    return launch_sum_slabs<T>(slabs, stride, p.splits, n * ldp, Z, s);
 }
 
 }  // namespace
@@ -283,11 +293,13 @@ template <typename T>
 hipError_t launch_proj_nn(const T* A, int64_t lda, int64_t m, int64_t n, const T* X, int LP,
                           const ProjPlan& p, T* slabs, T* Y, hipStream_t s, hipEvent_t done) {
     switch (LP) {
-        case 16: return nn_dispatch<T, 16>(A, lda, m, n, X, p, slabs, Y, s, done);
-        case 32: return nn_dispatch<T, 32>(A, lda, m, n, X, p, slabs, Y, s, done);
-        case 48: return nn_dispatch<T, 48>(A, lda, m, n, X, p, slabs, Y, s, done);
-        case 64: return nn_dispatch<T, 64>(A, lda, m, n, X, p, slabs, Y, s, done);
-        default: return hipErrorInvalidValue;
+        case 16: return nn_dispatch<T, 16>(A, lda, m, n, X, p, slabs, Y, s, done, 16);
+        case 32: return nn_dispatch<T, 32>(A, lda, m, n, X, p, slabs, Y, s, done, 32);
+        case 48: return nn_dispatch<T, 48>(A, lda, m, n, X, p, slabs, Y, s, done, 48);
+        case 64: return nn_dispatch<T, 64>(A, lda, m, n, X, p, slabs, Y, s, done, 64);
+        default:
+            if (LP % 64 || LP > 512) return hipErrorInvalidValue;
+            return nn_dispatch<T, 64>(A, lda, m, n, X, p, slabs, Y, s, done, LP);
     }
 }
 
@@ -295,11 +307,13 @@ template <typename T>
 hipError_t launch_proj_tn(const T* A, int64_t lda, int64_t m, int64_t n, const T* Q, int LP,
                           const ProjPlan& p, T* slabs, T* Z, hipStream_t s, hipEvent_t done) {
     switch (LP) {
-        case 16: return tn_dispatch<T, 16>(A, lda, m, n, Q, p, slabs, Z, s, done);
-        case 32: return tn_dispatch<T, 32>(A, lda, m, n, Q, p, slabs, Z, s, done);
-        case 48: return tn_dispatch<T, 48>(A, lda, m, n, Q, p, slabs, Z, s, done);
-        case 64: return tn_dispatch<T, 64>(A, lda, m, n, Q, p, slabs, Z, s, done);
-        default: return hipErrorInvalidValue;
+        case 16: return tn_dispatch<T, 16>(A, lda, m, n, Q, p, slabs, Z, s, done, 16);
+        case 32: return tn_dispatch<T, 32>(A, lda, m, n, Q, p, slabs, Z, s, done, 32);
+        case 48: return tn_dispatch<T, 48>(A, lda, m, n, Q, p, slabs, Z, s, done, 48);
+        case 64: return tn_dispatch<T, 64>(A, lda, m, n, Q, p, slabs, Z, s, done, 64);
+        default:
+            if (LP % 64 || LP > 512) return hipErrorInvalidValue;
+            return tn_dispatch<T, 64>(A, lda, m, n, Q, p, slabs, Z, s, done, LP);
     }
 }
 

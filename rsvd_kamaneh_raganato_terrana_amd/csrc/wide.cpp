@@ -1,0 +1,328 @@
+// wide.cpp -- host orchestration of the wide rSVD engine (l up to 512; bf16 / fp8 / fp32 / fp64 A).
+//
+// Same algorithm and op order as the narrow engine (driver.cpp) and the reference
+// (src/rSVD.cpp:57-133):
+//   Omega                                              generateOmega        src/rSVD.cpp:81
+//   Y = A Omega ; Q = orth(Y)                          intermediate_step    src/rSVD.cpp:59-61
+//   q x { Z = A^T Q ; X = orth(Z) ; Y = A X ; Q = orth(Y) }                 src/rSVD.cpp:62-69
+//   B^T = A^T Q ; Q_B = orth(B^T) ; R = Q_B^T B^T      B = Q^T A + QR       src/rSVD.cpp:89, SVD_class.hpp:116-123
+//   W = R^T = U_w S V_w^T                              SVD<Jacobi>          SVD_class.hpp:126-178
+//   U = Q U_w ; V = Q_B V_w                            U = Q * Utilde       src/rSVD.cpp:128
+// with the wide kernels (wide.hpp): bf16-MFMA projections for bf16 / fp8 A (fp32 / fp64 A use the
+// narrow MFMA kernels per 64-column group), CholeskyQR(2) with fp64 Grams for any LP <= 512, and
+// the block Jacobi small SVD for LP >= 128 (jacobi.hip's one-workgroup kernel below).
+// Row sharding (world > 1) follows driver.cpp: m-side Grams and the n-side products are summed
+// through the all-reduce hook; every rank holds Q_B, S, V and its rows of U.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <string>
+
+#include "handle.hpp"
+#include "kernels.hpp"
+#include "wide.hpp"
+
+namespace rsvd {
+
+namespace {
+
+inline int64_t rup(int64_t x, int64_t q) { return (x + q - 1) / q * q; }
+
+bool lowp_dtype(int dt) { return dt == RSVD_BF16 || dt == RSVD_FP8_E4M3; }
+
+int wide_lp(int l, int dtype) {
+    if (lowp_dtype(dtype)) {
+        int lp = 16;
+        while (lp < l) lp *= 2;
+        return lp;  // the bf16 projection kernels are built for 16 .. 512
+    }
+    return (int)rup(l, 64);  // 64-column groups of the fp32 / fp64 projection kernels
+}
+
+template <typename T>
+struct WideLayout {
+    int64_t m, n;
+    int l, LP;
+    bool lowp;
+    WProjPlan wnn, wtn;
+    ProjPlan pnn, ptn;
+    GramPlan gm, gn, gx;
+    size_t off_Xn, off_Zn, off_Ym, off_Qm, off_T1, off_Xh, off_Xl, off_Qh, off_Ql, off_pslab, off_gslab;
+    size_t off_G, off_R, off_Rinv, off_W, off_R1, off_Uw, off_Vw, off_JX, off_JJ, off_colflag, off_sync, total;
+
+    WideLayout(const rsvd_desc_t* d) : m(d->m), n(d->n), l(d->l), LP(wide_lp(d->l, d->dtype)) {
+        lowp = lowp_dtype(d->dtype);
+        int64_t pslab = 1;
+        if (lowp) {
+            wnn = plan_wproj(m, n, LP);
+            wtn = plan_wproj(n, m, LP);
+            pslab = std::max<int64_t>(wnn.splits > 1 ? wnn.splits * m : 0, wtn.splits > 1 ? wtn.splits * n : 0);
+        } else {
+            pnn = plan_proj_nn<T>(m, n, 64);
+            ptn = plan_proj_tn<T>(m, n, 64);
+            pslab = std::max<int64_t>(pnn.splits > 1 ? pnn.splits * m : 0, ptn.splits > 1 ? ptn.splits * n : 0);
+        }
+        gm = plan_gram_wide(m, LP, 0);
+        gn = plan_gram_wide(n, LP, 0);
+        gx = plan_gram_wide(n, LP, 1);
+        const size_t gslab = (size_t)std::max({(int64_t)gm.blocks * gm.chunks, (int64_t)gn.blocks * gn.chunks,
+                                               (int64_t)gx.blocks * gx.chunks}) * 1024;
+        const int64_t mx = std::max(m, n);
+        const size_t L2 = (size_t)LP * LP;
+        size_t o = 0;
+        auto take = [&](size_t bytes) {
+            const size_t at = o;
+            o = align256(o + bytes);
+            return at;
+        };
+        off_Xn = take(sizeof(T) * n * LP);
+        off_Zn = take(sizeof(T) * n * LP);
+        off_Ym = take(sizeof(T) * m * LP);
+        off_Qm = take(sizeof(T) * m * LP);
+        off_T1 = take(sizeof(T) * mx * LP);
+        const size_t bn = lowp ? 2 * n * LP : 0, bm = lowp ? 2 * m * LP : 0;
+        off_Xh = take(bn);
+        off_Xl = take(bn);
+        off_Qh = take(bm);
+        off_Ql = take(bm);
+        off_pslab = take(sizeof(T) * std::max<int64_t>(pslab, 1) * LP);
+        off_gslab = take(sizeof(double) * gslab);
+        off_G = take(sizeof(double) * L2);
+        off_R = take(sizeof(double) * L2);
+        off_Rinv = take(sizeof(double) * L2);
+        off_W = take(sizeof(double) * L2);
+        off_R1 = take(sizeof(double) * L2);
+        off_Uw = take(sizeof(double) * L2);
+        off_Vw = take(sizeof(double) * L2);
+        off_JX = take(sizeof(double) * 2 * L2);
+        off_JJ = take(sizeof(double) * 2 * L2);
+        off_colflag = take(sizeof(int) * LP);
+        off_sync = take(sizeof(unsigned) * 128);
+        total = o;
+    }
+};
+
+template <typename T>
+struct WideEngine {
+    rsvd_handle_t h;
+    const WideLayout<T>& L;
+    hipStream_t s;
+    int dtype;
+    T *Xn, *Zn, *Ym, *Qm, *T1, *pslab;
+    bf16_t *Xh, *Xl, *Qh, *Ql;
+    double *gslab, *G, *R, *Rinv, *W, *R1, *Uw, *Vw, *JX, *JJ;
+    int* colflag;
+    unsigned* sync;
+    int inter_passes = 1;  // power-iteration intermediates only carry a subspace (driver.cpp)
+    int qr_mode = RSVD_QR_AUTO;
+    int orth_index = 0;
+    int64_t row_off = 0, m_total = 0;  // this rank's rows of the m side
+    uint64_t seed = 0;
+
+    WideEngine(rsvd_handle_t h_, const WideLayout<T>& L_, int dtype_) : h(h_), L(L_), s(h_->stream), dtype(dtype_) {
+        char* b = h->ws;
+        Xn = reinterpret_cast<T*>(b + L.off_Xn);
+        Zn = reinterpret_cast<T*>(b + L.off_Zn);
+        Ym = reinterpret_cast<T*>(b + L.off_Ym);
+        Qm = reinterpret_cast<T*>(b + L.off_Qm);
+        T1 = reinterpret_cast<T*>(b + L.off_T1);
+        pslab = reinterpret_cast<T*>(b + L.off_pslab);
+        Xh = L.lowp ? reinterpret_cast<bf16_t*>(b + L.off_Xh) : nullptr;
+        Xl = L.lowp ? reinterpret_cast<bf16_t*>(b + L.off_Xl) : nullptr;
+        Qh = L.lowp ? reinterpret_cast<bf16_t*>(b + L.off_Qh) : nullptr;
+        Ql = L.lowp ? reinterpret_cast<bf16_t*>(b + L.off_Ql) : nullptr;
+        gslab = reinterpret_cast<double*>(b + L.off_gslab);
+        G = reinterpret_cast<double*>(b + L.off_G);
+        R = reinterpret_cast<double*>(b + L.off_R);
+        Rinv = reinterpret_cast<double*>(b + L.off_Rinv);
+        W = reinterpret_cast<double*>(b + L.off_W);
+        R1 = reinterpret_cast<double*>(b + L.off_R1);
+        Uw = reinterpret_cast<double*>(b + L.off_Uw);
+        Vw = reinterpret_cast<double*>(b + L.off_Vw);
+        JX = reinterpret_cast<double*>(b + L.off_JX);
+        JJ = reinterpret_cast<double*>(b + L.off_JJ);
+        colflag = reinterpret_cast<int*>(b + L.off_colflag);
+        sync = reinterpret_cast<unsigned*>(b + L.off_sync);
+    }
+
+    int allreduce(void* buf, int64_t count, int32_t dt) {
+        if (h->world <= 1 || !h->allreduce) return RSVD_OK;
+        if (h->allreduce(buf, count, dt, (void*)s, h->ar_user) != 0) {
+            h->err = "all-reduce hook failed";
+            return RSVD_ERR_COMM;
+        }
+        return RSVD_OK;
+    }
+
+    int ev_begin(int kind, int& idx) {
+        idx = -1;
+        if (!h->timing) return RSVD_OK;
+        while (h->ev_pool.size() < h->ev_next + 2) {
+            hipEvent_t e;
+            RSVD_CK(hipEventCreate(&e));
+            h->ev_pool.push_back(e);
+        }
+        idx = (int)h->ev_next;
+        h->ev_next += 2;
+        h->ev_used.push_back({kind, idx});
+        RSVD_CK(hipEventRecord(h->ev_pool[idx], s));
+        return RSVD_OK;
+    }
+
+    // Y = A X (X: bf16 panels for low precision, T panel otherwise)
+    int proj_nn(const void* A, int64_t lda, const T* X, const bf16_t* xh, const bf16_t* xl, T* Y) {
+        int ev;
+        RSVD_TRY(ev_begin(0, ev));
+        hipEvent_t done = ev >= 0 ? h->ev_pool[ev + 1] : nullptr;
+        if (L.lowp) {
+            RSVD_CK(launch_wproj(1, dtype == RSVD_FP8_E4M3, A, lda, L.m, L.n, xh, xl, L.LP, L.wnn,
+                                 reinterpret_cast<float*>(pslab), reinterpret_cast<float*>(Y), s, done));
+        } else {
+            RSVD_CK(launch_proj_nn<T>(reinterpret_cast<const T*>(A), lda, L.m, L.n, X, L.LP, L.pnn, pslab, Y, s, done));
+        }
+        return RSVD_OK;
+    }
+    // Z = A^T Q, summed over the row shards
+    int proj_tn(const void* A, int64_t lda, const T* Q, const bf16_t* qh, const bf16_t* ql, T* Z) {
+        int ev;
+        RSVD_TRY(ev_begin(1, ev));
+        hipEvent_t done = ev >= 0 ? h->ev_pool[ev + 1] : nullptr;
+        if (L.lowp) {
+            RSVD_CK(launch_wproj(0, dtype == RSVD_FP8_E4M3, A, lda, L.m, L.n, qh, ql, L.LP, L.wtn,
+                                 reinterpret_cast<float*>(pslab), reinterpret_cast<float*>(Z), s, done));
+        } else {
+            RSVD_CK(launch_proj_tn<T>(reinterpret_cast<const T*>(A), lda, L.m, L.n, Q, L.LP, L.ptn, pslab, Z, s, done));
+        }
+        return allreduce(Z, L.n * L.LP, sizeof(T) == 8 ? RSVD_F64 : RSVD_F32);
+    }
+
+    double tol() const { return sizeof(T) == 4 ? 1e-13 : 1e-28; }
+
+    // One CholeskyQR pass Out = P chol(P^T P)^-1 (+ bf16 hi/lo of Out).  `pred`: predicated pass.
+    int cholqr_pass(const T* P, int64_t rows, const GramPlan& gp, T* Out, bool sharded, bf16_t* hi, bf16_t* lo,
+                    int* flag, const int* pred) {
+        RSVD_CK(launch_gram_wide<T>(P, nullptr, rows, L.LP, gp, gslab, G, pred, s));
+        if (sharded) RSVD_TRY(allreduce(G, (int64_t)L.LP * L.LP, RSVD_F64));
+        RSVD_CK(launch_chol_wide(G, L.l, L.LP, tol(), R, Rinv, nullptr, colflag, flag, W, pred, s));
+        RSVD_CK(launch_panel_gemm<T>(P, rows, L.LP, Rinv, 1, Out, 0, 0, hi, lo, pred, s));
+        return RSVD_OK;
+    }
+
+    // Q = orth(P): CholeskyQR (passes = 1) or CholeskyQR2; output panels (repair = true) get the
+    // rank-deficiency completion (predicated on the breakdown flag of this orth).
+    int orth(const T* P, bool mside, T* Q, int passes, bf16_t* hi, bf16_t* lo, bool repair) {
+        const int64_t rows = mside ? L.m : L.n;
+        const GramPlan& gp = mside ? L.gm : L.gn;
+        const bool sharded = mside && h->world > 1;
+        int* flag = h->dflags + 4 + (orth_index < 12 ? orth_index : 11);
+        ++orth_index;
+        if (qr_mode == RSVD_QR_CHOLQR2 || qr_mode == RSVD_QR_GS2) passes = 2;
+        if (passes <= 1) {
+            RSVD_TRY(cholqr_pass(P, rows, gp, Q, sharded, hi, lo, flag, nullptr));
+        } else {
+            RSVD_TRY(cholqr_pass(P, rows, gp, T1, sharded, nullptr, nullptr, flag, nullptr));
+            RSVD_TRY(cholqr_pass(T1, rows, gp, Q, sharded, hi, lo, flag, nullptr));
+        }
+        if (repair) {
+            const int64_t off = mside ? row_off : 0, tot = mside ? m_total : L.n;
+            RSVD_CK(launch_repair_panel<T>(Q, rows, L.l, L.LP, colflag, flag, seed ^ (0x5EEDull + orth_index), off,
+                                           tot, T1, s));
+            RSVD_TRY(cholqr_pass(T1, rows, gp, Q, sharded, hi, lo, flag, flag));
+        }
+        return RSVD_OK;
+    }
+
+    int load_omega(const void* omega, int64_t ldo, uint64_t sd) {
+        if (L.lowp) {
+            const int f8 = dtype == RSVD_FP8_E4M3;
+            if (omega) {
+                RSVD_CK(launch_omega_lowp_from(reinterpret_cast<const float*>(omega), ldo, L.n, L.l, L.LP, f8, Xh, s));
+            } else {
+                RSVD_CK(launch_omega_lowp(Xh, L.n, L.l, L.LP, sd, f8, nullptr, s));
+            }
+        } else if (omega) {
+            RSVD_CK(launch_colmajor_to_panel<T>(reinterpret_cast<const T*>(omega), ldo, L.n, L.l, L.LP, Xn, s));
+        } else {
+            RSVD_CK(launch_philox_omega<T>(Xn, L.n, L.l, L.LP, sd, s));
+        }
+        return RSVD_OK;
+    }
+
+    int range_finder(const void* A, int64_t lda, int q) {
+        RSVD_TRY(proj_nn(A, lda, Xn, Xh, nullptr, Ym));  // the sketch: Omega is exactly bf16 (lowp)
+        RSVD_TRY(orth(Ym, true, Qm, q == 0 ? 2 : inter_passes, Qh, Ql, q == 0));
+        for (int i = 0; i < q; ++i) {
+            const bool last = i == q - 1;
+            RSVD_TRY(proj_tn(A, lda, Qm, Qh, Ql, Zn));
+            RSVD_TRY(orth(Zn, false, Xn, inter_passes, Xh, Xl, false));
+            RSVD_TRY(proj_nn(A, lda, Xn, Xh, Xl, Ym));
+            RSVD_TRY(orth(Ym, true, Qm, last ? 2 : inter_passes, Qh, Ql, last));
+        }
+        return RSVD_OK;
+    }
+
+    int run(const rsvd_desc_t* d, const void* A, void* U, int64_t ldu, T* S, void* V, int64_t ldv) {
+        RSVD_TRY(range_finder(A, d->lda, d->q));
+        RSVD_TRY(proj_tn(A, d->lda, Qm, Qh, Ql, Zn));               // B^T = A^T Q
+        RSVD_TRY(orth(Zn, false, Xn, 2, nullptr, nullptr, true));  // Q_B
+        RSVD_CK(launch_gram_wide<T>(Xn, Zn, L.n, L.LP, L.gx, gslab, R1, nullptr, s));  // R = Q_B^T B^T
+        // the small SVD always runs in fp64 (U_w, V_w feed the fp32 panel products of U and V)
+        double* Sd = G;  // free scratch by now
+        if (L.LP <= 64) {
+            RSVD_CK(launch_small_svd<double>(R1, L.l, L.LP, Uw, Vw, Sd, h->dflags + 1, s));
+        } else {
+            RSVD_CK(launch_block_jacobi<double>(R1, L.l, L.LP, JX, JJ, Uw, Vw, Sd, sync, h->dflags + 1, s));
+        }
+        const double sc = (d->a_scale != 0.0) ? d->a_scale : 1.0;
+        RSVD_CK(launch_convert_scale<T>(Sd, S, L.l, sc, s));
+        RSVD_CK(launch_panel_gemm<T>(Qm, L.m, L.LP, Uw, 0, reinterpret_cast<T*>(U), ldu, L.l, nullptr, nullptr,
+                                     nullptr, s));
+        RSVD_CK(launch_panel_gemm<T>(Xn, L.n, L.LP, Vw, 0, reinterpret_cast<T*>(V), ldv, L.l, nullptr, nullptr,
+                                     nullptr, s));
+        return RSVD_OK;
+    }
+};
+
+template <typename T>
+int wide_typed(rsvd_handle_t h, const rsvd_desc_t* d, const void* A, const void* omega, int64_t ldo, void* U,
+               int64_t ldu, void* S, void* V, int64_t ldv, void* Qout, int64_t ldq) {
+    WideLayout<T> L(d);
+    RSVD_TRY(ensure_ws(h, L.total));
+    RSVD_CK(hipMemsetAsync(h->dflags, 0, 16 * sizeof(int), h->stream));
+    h->info.splits_nn = L.lowp ? L.wnn.splits : L.pnn.splits;
+    h->info.splits_tn = L.lowp ? L.wtn.splits : L.ptn.splits;
+    WideEngine<T> E(h, L, d->dtype);
+    E.qr_mode = d->qr_mode;
+    E.seed = d->seed;
+    // Repair stream layout of the m side: rank g's rows are stream rows [g m, g m + m) of a
+    // world * m panel (any disjoint layout keeps the repaired global columns Gaussian).
+    E.row_off = (int64_t)h->rank * d->m;
+    E.m_total = (int64_t)h->world * d->m;
+    RSVD_TRY(E.load_omega(omega, ldo, d->seed));
+    if (Qout) {
+        RSVD_TRY(E.range_finder(A, d->lda, d->q));
+        RSVD_CK(launch_panel_to_colmajor<T>(E.Qm, L.m, L.l, L.LP, reinterpret_cast<T*>(Qout), ldq, h->stream));
+        return RSVD_OK;
+    }
+    return E.run(d, A, U, ldu, reinterpret_cast<T*>(S), V, ldv);
+}
+
+}  // namespace
+
+bool wide_path(const rsvd_desc_t* d) { return lowp_dtype(d->dtype) || d->l > 64; }
+
+int wide_workspace_bytes(const rsvd_desc_t* d, size_t* bytes) {
+    if (d->dtype == RSVD_F64)
+        *bytes = WideLayout<double>(d).total;
+    else
+        *bytes = WideLayout<float>(d).total;
+    return RSVD_OK;
+}
+
+int wide_run(rsvd_handle_t h, const rsvd_desc_t* d, const void* A, const void* omega, int64_t ldo, void* U,
+             int64_t ldu, void* S, void* V, int64_t ldv, void* Qout, int64_t ldq) {
+    if (d->dtype == RSVD_F64) return wide_typed<double>(h, d, A, omega, ldo, U, ldu, S, V, ldv, Qout, ldq);
+    return wide_typed<float>(h, d, A, omega, ldo, U, ldu, S, V, ldv, Qout, ldq);
+}
+
+}  // namespace rsvd

@@ -1,0 +1,105 @@
+// wide.hpp -- launch wrappers of the "wide" rSVD path: sketch widths up to 512 and bf16 / fp8 A.
+//
+// Panels (Y, Q, Z, Omega, B^T, Q_B) are row-major `rows x LP` in fp32 (fp64 when A is fp64), as
+// in the narrow path (common.hpp).  For bf16 / fp8 A the projections run on the bf16 MFMA
+// (v_mfma_f32_16x16x32_bf16) and read the skinny operand as a bf16 "hi" panel plus, for the
+// power-iteration and B projections, a bf16 "lo" panel (P ~= hi + lo, 16 significant bits; the
+// Gaussian sketch Omega is itself rounded to bf16 / e4m3, so the first projection is exact in
+// one pass).  The QR is CholeskyQR(2) with fp64 Grams on the fp64 MFMA, a one-workgroup blocked
+// Cholesky + triangular inverse, and an MFMA panel product that also emits the next hi/lo
+// panels.  The small SVD is a block one-sided Jacobi on a persistent grid (wide_svd.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "../../include/rsvd_c.h"
+
+namespace rsvd {
+
+typedef uint16_t bf16_t;  // storage of one bf16
+typedef uint8_t fp8_t;    // storage of one OCP e4m3fn
+
+// ---- wide_proj.hip -----------------------------------------------------------------------------
+// Sketch widths the bf16 projection kernels are built for (LP = padded l).
+bool wproj_supported_lp(int LP);
+int wproj_rows_per_block(int LP);  // output rows per workgroup (256 / 128 / 64)
+struct WProjPlan {
+    int splits;      // K splits (1 = straight into the output panel)
+    int64_t chunk;   // K range per workgroup (multiple of 32)
+    int blocks;      // output row blocks
+};
+WProjPlan plan_wproj(int64_t rows_out, int64_t K, int LP);
+// NN: Y (m x LP, fp32) = A (m x n) * S       S = n x LP bf16 panel(s)      src/rSVD.cpp:59,66
+// TN: Z (n x LP, fp32) = A^T * S             S = m x LP bf16 panel(s)      src/rSVD.cpp:63,89
+// A is column-major (lda) bf16 (a_fp8 = 0) or e4m3 (a_fp8 = 1).  Slo == nullptr: single pass.
+// `done` (optional) is recorded after the MFMA kernel, before the slab reduction.
+hipError_t launch_wproj(int nn, int a_fp8, const void* A, int64_t lda, int64_t m, int64_t n, const bf16_t* Shi,
+                        const bf16_t* Slo, int LP, const WProjPlan& p, float* slabs, float* Out, hipStream_t s,
+                        hipEvent_t done = nullptr);
+
+// ---- wide_qr.hip -------------------------------------------------------------------------------
+struct GramPlan {
+    int blocks;   // 32 x 32 blocks of the Gram (upper triangle, or all for a cross Gram)
+    int chunks;   // row chunks
+    int64_t rows_per_chunk;
+};
+GramPlan plan_gram_wide(int64_t rows, int LP, int cross);
+// Partial Grams of P^T P (cross: P^T P2) per (chunk, 32x32 block) into `slabs` (fp64), then
+// G = sum over chunks (LP x LP fp64 row-major, mirrored when symmetric).  `pred` (nullable): skip
+// both launches unless *pred != 0.
+template <typename T>
+hipError_t launch_gram_wide(const T* P, const T* P2, int64_t rows, int LP, const GramPlan& gp, double* slabs,
+                            double* G, const int* pred, hipStream_t s);
+// R = chol(G[:l,:l]) (upper) and Rinv = R^-1, LP x LP fp64 zero-padded, one workgroup.  A pivot
+// d_k <= tol * G_kk (or not finite) is a breakdown: R row k := e_k, colflag[k] = 1, *flag += 1.
+// Also writes Rinv as fp32 when Rinv32 != nullptr.  `work`: LP x LP fp64.  `pred`: as above.
+hipError_t launch_chol_wide(const double* G, int l, int LP, double tol, double* R, double* Rinv, float* Rinv32,
+                            int* colflag, int* flag, double* work, const int* pred, hipStream_t s);
+// Out (rows x LP) = In (rows x LP) * M (LP x LP fp64, applied in T; `upper`: only k <= c of M
+// is read).  Out layouts: row-major panel (ldo = 0) or the caller's column-major matrix (first
+// `cols` columns, leading dimension ldo).  Optionally also writes the bf16 hi / lo panels of Out
+// (row-major, LP wide).  `pred`: as above.
+template <typename T>
+hipError_t launch_panel_gemm(const T* In, int64_t rows, int LP, const double* M, int upper, T* Out, int64_t ldo,
+                             int cols, bf16_t* hi, bf16_t* lo, const int* pred, hipStream_t s);
+// y[0..n) = (T)(x * sc)
+template <typename T>
+hipError_t launch_convert_scale(const double* x, T* y, int n, double sc, hipStream_t s);
+// Rank-deficiency repair of an orthonormalised panel: copies Q into Out, replacing every column
+// k with colflag[k] != 0 by Philox Gaussian values / sqrt(rows_total) (stream element
+// row_off + i + rows_total * k: row shards of one global panel draw one global column).
+// No-op unless *flag != 0.
+template <typename T>
+hipError_t launch_repair_panel(const T* Q, int64_t rows, int l, int LP, const int* colflag, const int* flag,
+                               uint64_t seed, int64_t row_off, int64_t rows_total, T* Out, hipStream_t s);
+// fp32 / fp64 panel -> bf16 hi (+ lo) panels (rows x LP).
+template <typename T>
+hipError_t launch_split_bf16(const T* P, int64_t rows, int LP, bf16_t* hi, bf16_t* lo, hipStream_t s);
+// Omega for bf16 / fp8 A: Philox N(0,1) rounded to bf16 (round_fp8 = 0) or e4m3 (= 1), written
+// as the bf16 panel (n x LP) and, when `f` != nullptr, as fp32 column-major (ld n) for callers.
+hipError_t launch_omega_lowp(bf16_t* panel, int64_t n, int l, int LP, uint64_t seed, int round_fp8, float* f,
+                             hipStream_t s);
+// Caller-supplied Omega (fp32 column-major, ld) -> bf16 panel, rounding to bf16 / e4m3.
+hipError_t launch_omega_lowp_from(const float* om, int64_t ld, int64_t n, int l, int LP, int round_fp8,
+                                  bf16_t* panel, hipStream_t s);
+
+// ---- wide_svd.hip ------------------------------------------------------------------------------
+// Block one-sided Jacobi of W (W[i][c] = R[c][i], l x l): X = W, J = I; rotate column blocks
+// pairwise until orthogonal; then S (descending), Uw = X / S (completed to orthonormal when
+// S = 0), Vw = J (both LP x LP fp64 row-major, [row][col]).  Work: X, J (2 LP^2 fp64 each:
+// double buffers), sync (72 words, zeroed here).  LP in {64, 96, ..., 512}.  info[0] = sweeps;
+// info[2] = 1 on a barrier timeout.
+template <typename T>
+hipError_t launch_block_jacobi(const double* R, int l, int LP, double* X, double* J, double* Uw, double* Vw, T* S,
+                               unsigned* sync, int* info, hipStream_t s);
+
+// ---- wide.cpp: the host pipeline ------------------------------------------------------------------
+// True when `d` runs on the wide engine (bf16 / fp8 A, or l > 64).
+bool wide_path(const rsvd_desc_t* d);
+int wide_workspace_bytes(const rsvd_desc_t* d, size_t* bytes);
+// rSVD (Qout == nullptr) or intermediate_step (Q into Qout) on the handle's stream.
+int wide_run(rsvd_handle_t h, const rsvd_desc_t* d, const void* A, const void* omega, int64_t ldo, void* U,
+             int64_t ldu, void* S, void* V, int64_t ldv, void* Qout, int64_t ldq);
+
+}  // namespace rsvd

@@ -1,0 +1,334 @@
+// wide_proj.hip -- bf16 / fp8 A projections on the bf16 MFMA (gfx950), sketch width LP <= 512.
+//
+//   NN:  Y = A * S     (A m x n column-major, S n x LP panel)    src/rSVD.cpp:59,66
+//   TN:  Z = A^T * S   (S m x LP panel, Z n x LP)                 src/rSVD.cpp:63,89 (B^T = A^T Q)
+//
+// The skinny operand S arrives as bf16 panels: "hi" (and "lo" with S ~= hi + lo) -- two MFMAs
+// per product keep 16 significant bits of S, which is what the 1e-4 parity bar needs (SURVEY.md
+// §7 "Hard parts"); the Gaussian sketch is itself bf16 (or e4m3) so A*Omega is one pass.  A is
+// read from HBM exactly once per launch; fp8 A is widened to bf16 on the way (exact).
+//
+// v_mfma_f32_16x16x32_bf16 operand maps (cdna_hip_programming.md §3): lane l holds
+// A[row l&15][k = 8(l>>4) + j] and B[k = 8(l>>4) + j][col l&15], j = 0..7; D: col = l&15,
+// row = 4(l>>4) + reg.  The contraction index k is the A column index for NN (strided in HBM)
+// and the A row index for TN (contiguous):
+//  * S (both) and A (NN) are staged per 32-deep k-step into LDS as row-major [k][...] tiles
+//    (16-B padded rows, 2-way bank conflicts at most) and read with ds_read_b64_tr_b16, which
+//    hands each lane 4 consecutive k of one column -- the fragment shape, no shuffles.
+//  * A (TN) goes straight from HBM to the fragment: 8 consecutive rows of one A column.
+// Staging is register-prefetched one k-step ahead (loads for step s+1 in flight while step s
+// computes).  Workgroup = 4 waves as WR (rows) x WC (columns); a wave owns 64 output rows x
+// 16 G columns (acc = 4 x G MFMA tiles).  K is split over workgroups into fp32 slabs
+// (launch_sum_slabs) when the row blocks alone cannot fill the chip; the XCD-aware remap puts
+// the row blocks of one K chunk on one XCD so their shared S chunk is an L2 hit.
+#include <type_traits>
+
+#include "common.hpp"
+#include "kernels.hpp"
+#include "wide.hpp"
+
+namespace rsvd {
+
+namespace {
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8_t;
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
+typedef __attribute__((ext_vector_type(4))) short s16x4;
+typedef __attribute__((ext_vector_type(8))) short s16x8;
+
+template <int LP> struct WCfg;
+template <> struct WCfg<16> { static constexpr int WR = 4, WC = 1, G = 1; };
+template <> struct WCfg<32> { static constexpr int WR = 4, WC = 1, G = 2; };
+template <> struct WCfg<64> { static constexpr int WR = 4, WC = 1, G = 4; };
+template <> struct WCfg<128> { static constexpr int WR = 4, WC = 1, G = 8; };
+template <> struct WCfg<256> { static constexpr int WR = 2, WC = 2, G = 8; };
+template <> struct WCfg<512> { static constexpr int WR = 1, WC = 4, G = 8; };
+
+constexpr int RT = 4;   // 16-row MFMA tiles per wave
+constexpr int KS = 32;  // k per step (one MFMA deep)
+
+__device__ __forceinline__ s16x4 tr_read(const bf16_t* p) {
+    typedef s16x4 __attribute__((address_space(3))) * lds_ptr;
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_ptr)(const_cast<bf16_t*>(p)));
+}
+__device__ __forceinline__ bf16x8_t join(s16x4 a, s16x4 b) {
+    return __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
+}
+// 4 e4m3 bytes -> 4 bf16 (exact: e4m3 has 4 significant bits)
+__device__ __forceinline__ uint2 fp8x4_to_bf16x4(uint32_t v) {
+    const bf16x2_t a = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(v, 1.0f, false);
+    const bf16x2_t b = __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(v, 1.0f, true);
+    return make_uint2(__builtin_bit_cast(uint32_t, a), __builtin_bit_cast(uint32_t, b));
+}
+
+template <bool FP8, bool NN, int LP, bool SPLIT>
+constexpr size_t wproj_lds() {
+    constexpr int WI = WCfg<LP>::WR * 64;
+    return (size_t)(SPLIT ? 2 : 1) * KS * (LP + 8) * 2 + (NN ? (size_t)KS * (WI + 8) * 2 : 0);
+}
+
+template <bool FP8, bool NN, int LP, bool SPLIT>
+__global__ __launch_bounds__(256) void wproj_kernel(const void* __restrict__ Av, int64_t lda, int64_t rows_out,
+                                                    int64_t K, const bf16_t* __restrict__ Shi,
+                                                    const bf16_t* __restrict__ Slo, float* __restrict__ out,
+                                                    int64_t slab_stride, int64_t kchunk, int nrowblk, int vec_ok) {
+    typedef WCfg<LP> C;
+    constexpr int WR = C::WR, G = C::G;
+    constexpr int WI = WR * 64;
+    constexpr int PS = LP + 8;  // S tile row pitch (bf16 elements)
+    constexpr int PA = WI + 8;  // A tile row pitch (NN)
+    constexpr int NS = SPLIT ? 2 : 1;
+    constexpr int SCH = KS * LP / 8;  // 16-B chunks of one S tile
+    constexpr int SPT = (SCH + 255) / 256;
+    constexpr int AEL = FP8 ? 16 : 8;  // A elements per 16-B chunk
+    constexpr int ACH = KS * WI / AEL;
+    constexpr int APT = NN ? (ACH + 255) / 256 : 1;
+    typedef typename std::conditional<FP8, uint2, uint4>::type AF;  // 8 A elements along k
+    typedef typename std::conditional<FP8, fp8_t, bf16_t>::type TA;
+    const TA* __restrict__ A = reinterpret_cast<const TA*>(Av);
+
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    bf16_t* Ss = reinterpret_cast<bf16_t*>(smem_raw);  // [NS][KS][PS]
+    bf16_t* As = Ss + NS * KS * PS;                    // [KS][PA]   (NN)
+
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int r = lane & 15, h = lane >> 4, q = r >> 2, p = r & 3;
+    const int wr = w % WR, wc = w / WR;
+    const int bid = xcd_remap(blockIdx.x, gridDim.x);
+    const int rb = bid % nrowblk, sp = bid / nrowblk;
+    const int64_t row0 = (int64_t)rb * WI;
+    const int64_t kbeg = (int64_t)sp * kchunk;
+    const int64_t kend = (kbeg + kchunk < K) ? kbeg + kchunk : K;
+    const bf16_t* Sarr[2] = {Shi, Slo};
+
+    uint4 sreg[NS][SPT];
+    uint4 areg[APT];
+    AF afr[NN ? 1 : RT];
+
+    auto load_S = [&](int64_t kk) {
+#pragma unroll
+        for (int a = 0; a < NS; ++a)
+#pragma unroll
+            for (int t = 0; t < SPT; ++t) {
+                const int u = tid + 256 * t;
+                const int krow = u / (LP / 8), c8 = u % (LP / 8);
+                const int64_t k = kk + krow;
+                uint4 v = make_uint4(0, 0, 0, 0);
+                if (u < SCH && k < kend) v = *reinterpret_cast<const uint4*>(Sarr[a] + k * LP + c8 * 8);
+                sreg[a][t] = v;
+            }
+    };
+    auto store_S = [&]() {
+#pragma unroll
+        for (int a = 0; a < NS; ++a)
+#pragma unroll
+            for (int t = 0; t < SPT; ++t) {
+                const int u = tid + 256 * t;
+                if (u < SCH) {
+                    const int krow = u / (LP / 8), c8 = u % (LP / 8);
+                    *reinterpret_cast<uint4*>(Ss + (a * KS + krow) * PS + c8 * 8) = sreg[a][t];
+                }
+            }
+    };
+    auto load_A_nn = [&](int64_t kk) {
+#pragma unroll
+        for (int t = 0; t < APT; ++t) {
+            const int u = tid + 256 * t;
+            const int j = u / (WI / AEL), ic = u % (WI / AEL);
+            const int64_t jj = kk + j, i = row0 + (int64_t)ic * AEL;
+            uint4 v = make_uint4(0, 0, 0, 0);
+            if (u < ACH && jj < kend) {
+                const TA* src = A + jj * lda + i;
+                if (vec_ok && i + AEL <= rows_out) {
+                    v = *reinterpret_cast<const uint4*>(src);
+                } else {
+                    TA* e = reinterpret_cast<TA*>(&v);
+#pragma unroll
+                    for (int x = 0; x < AEL; ++x) e[x] = (i + x < rows_out) ? src[x] : TA(0);
+                }
+            }
+            areg[t] = v;
+        }
+    };
+    auto store_A_nn = [&]() {
+#pragma unroll
+        for (int t = 0; t < APT; ++t) {
+            const int u = tid + 256 * t;
+            if (u < ACH) {
+                const int j = u / (WI / AEL), ic = u % (WI / AEL);
+                if (FP8) {
+                    const uint2 b0 = fp8x4_to_bf16x4(areg[t].x), b1 = fp8x4_to_bf16x4(areg[t].y);
+                    const uint2 b2 = fp8x4_to_bf16x4(areg[t].z), b3 = fp8x4_to_bf16x4(areg[t].w);
+                    uint4* d = reinterpret_cast<uint4*>(As + j * PA + ic * AEL);
+                    d[0] = make_uint4(b0.x, b0.y, b1.x, b1.y);
+                    d[1] = make_uint4(b2.x, b2.y, b3.x, b3.y);
+                } else {
+                    *reinterpret_cast<uint4*>(As + j * PA + ic * AEL) = areg[t];
+                }
+            }
+        }
+    };
+    auto load_A_tn = [&](int64_t kk) {
+#pragma unroll
+        for (int t = 0; t < (NN ? 1 : RT); ++t) {
+            const int64_t jc = row0 + wr * 64 + 16 * t + r;  // output row = column of A
+            const int64_t i = kk + 8 * h;
+            AF v;
+            TA* e = reinterpret_cast<TA*>(&v);
+#pragma unroll
+            for (int x = 0; x < 8; ++x) e[x] = TA(0);
+            if (jc < rows_out) {
+                const TA* src = A + jc * lda + i;
+                if (vec_ok && i + 8 <= kend) {
+                    v = *reinterpret_cast<const AF*>(src);
+                } else {
+#pragma unroll
+                    for (int x = 0; x < 8; ++x) e[x] = (i + x < kend) ? src[x] : TA(0);
+                }
+            }
+            afr[t] = v;
+        }
+    };
+
+    f32x4 acc[RT][G];
+#pragma unroll
+    for (int t = 0; t < RT; ++t)
+#pragma unroll
+        for (int g = 0; g < G; ++g) acc[t][g] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    if (kbeg < kend) {
+        load_S(kbeg);
+        if (NN) load_A_nn(kbeg); else load_A_tn(kbeg);
+    }
+    for (int64_t kk = kbeg; kk < kend; kk += KS) {
+        __syncthreads();  // previous step's LDS reads are done
+        store_S();
+        if (NN) store_A_nn();
+        AF acur[NN ? 1 : RT];
+        if (!NN) {
+#pragma unroll
+            for (int t = 0; t < (NN ? 1 : RT); ++t) acur[t] = afr[t];
+        }
+        __syncthreads();
+        if (kk + KS < kend) {  // prefetch the next step while this one computes
+            load_S(kk + KS);
+            if (NN) load_A_nn(kk + KS); else load_A_tn(kk + KS);
+        }
+        bf16x8_t af[RT];
+#pragma unroll
+        for (int t = 0; t < RT; ++t) {
+            if (NN) {
+                const bf16_t* b = As + (8 * h + q) * PA + wr * 64 + 16 * t + 4 * p;
+                af[t] = join(tr_read(b), tr_read(b + 4 * PA));
+            } else if (FP8) {
+                const uint2 x = *reinterpret_cast<const uint2*>(&acur[t]);
+                const uint2 lo = fp8x4_to_bf16x4(x.x), hi = fp8x4_to_bf16x4(x.y);
+                af[t] = __builtin_bit_cast(bf16x8_t, make_uint4(lo.x, lo.y, hi.x, hi.y));
+            } else {
+                af[t] = __builtin_bit_cast(bf16x8_t, *reinterpret_cast<const uint4*>(&acur[t]));
+            }
+        }
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const int col = wc * G * 16 + 16 * g + 4 * p;
+            const bf16_t* b = Ss + (8 * h + q) * PS + col;
+            const bf16x8_t bh = join(tr_read(b), tr_read(b + 4 * PS));
+            bf16x8_t bl;
+            if (SPLIT) {
+                const bf16_t* c = b + KS * PS;
+                bl = join(tr_read(c), tr_read(c + 4 * PS));
+            }
+#pragma unroll
+            for (int t = 0; t < RT; ++t) {
+                acc[t][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[t], bh, acc[t][g], 0, 0, 0);
+                if (SPLIT) acc[t][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[t], bl, acc[t][g], 0, 0, 0);
+            }
+        }
+    }
+
+    float* dst = out + (int64_t)sp * slab_stride;
+#pragma unroll
+    for (int t = 0; t < RT; ++t)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int64_t row = row0 + wr * 64 + 16 * t + 4 * h + j;
+            if (row < rows_out) {
+#pragma unroll
+                for (int g = 0; g < G; ++g) dst[row * LP + wc * G * 16 + 16 * g + r] = acc[t][g][j];
+            }
+        }
+}
+
+template <bool FP8, bool NN, int LP, bool SPLIT>
+hipError_t wproj_go(const void* A, int64_t lda, int64_t m, int64_t n, const bf16_t* Shi, const bf16_t* Slo,
+                    const WProjPlan& p, float* slabs, float* Out, hipStream_t s, hipEvent_t done) {
+    const int64_t rows_out = NN ? m : n, K = NN ? n : m;
+    float* o = p.splits == 1 ? Out : slabs;
+    const int64_t stride = rows_out * LP;
+    const int esz = FP8 ? 1 : 2;
+    const int vec_ok = ((lda * esz) % 16 == 0) && ((reinterpret_cast<uintptr_t>(A) & 15) == 0);
+    hipLaunchKernelGGL((wproj_kernel<FP8, NN, LP, SPLIT>), dim3(p.blocks * p.splits), dim3(256),
+                       (wproj_lds<FP8, NN, LP, SPLIT>()), s, A, lda, rows_out, K, Shi, Slo, o, stride, p.chunk,
+                       p.blocks, vec_ok);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess && done) e = hipEventRecord(done, s);
+    if (e != hipSuccess || p.splits == 1) return e;
+    return launch_sum_slabs<float>(slabs, stride, p.splits, stride, Out, s);
+}
+
+template <int LP>
+hipError_t wproj_lp(int nn, int fp8, const void* A, int64_t lda, int64_t m, int64_t n, const bf16_t* Shi,
+                    const bf16_t* Slo, const WProjPlan& p, float* slabs, float* Out, hipStream_t s, hipEvent_t d) {
+    const bool split = Slo != nullptr;
+#define GO(F, N, SP) return wproj_go<F, N, LP, SP>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d)
+    if (fp8) {
+        if (nn) { if (split) GO(true, true, true); GO(true, true, false); }
+        if (split) GO(true, false, true);
+        GO(true, false, false);
+    }
+    if (nn) { if (split) GO(false, true, true); GO(false, true, false); }
+    if (split) GO(false, false, true);
+    GO(false, false, false);
+#undef GO
+}
+
+}  // namespace
+
+bool wproj_supported_lp(int LP) {
+    return LP == 16 || LP == 32 || LP == 64 || LP == 128 || LP == 256 || LP == 512;
+}
+
+int wproj_rows_per_block(int LP) { return LP <= 128 ? 256 : (LP == 256 ? 128 : 64); }
+
+WProjPlan plan_wproj(int64_t rows_out, int64_t K, int LP) {
+    WProjPlan p;
+    const int WI = wproj_rows_per_block(LP);
+    p.blocks = (int)((rows_out + WI - 1) / WI);
+    const int target = LP >= 512 ? 256 : 512;  // LP = 512 runs one workgroup per CU (registers)
+    int64_t splits = (target + p.blocks - 1) / p.blocks;
+    const int64_t max_by_work = K / (KS * 8);
+    if (splits > max_by_work) splits = max_by_work;
+    if (splits > 128) splits = 128;
+    if (splits < 1) splits = 1;
+    int64_t chunk = (K + splits - 1) / splits;
+    chunk = (chunk + KS - 1) / KS * KS;
+    p.chunk = chunk;
+    p.splits = (int)((K + chunk - 1) / chunk);
+    return p;
+}
+
+hipError_t launch_wproj(int nn, int a_fp8, const void* A, int64_t lda, int64_t m, int64_t n, const bf16_t* Shi,
+                        const bf16_t* Slo, int LP, const WProjPlan& p, float* slabs, float* Out, hipStream_t s,
+                        hipEvent_t done) {
+    switch (LP) {
+        case 16: return wproj_lp<16>(nn, a_fp8, A, lda, m, n, Shi, Slo, p, slabs, Out, s, done);
+        case 32: return wproj_lp<32>(nn, a_fp8, A, lda, m, n, Shi, Slo, p, slabs, Out, s, done);
+        case 64: return wproj_lp<64>(nn, a_fp8, A, lda, m, n, Shi, Slo, p, slabs, Out, s, done);
+        case 128: return wproj_lp<128>(nn, a_fp8, A, lda, m, n, Shi, Slo, p, slabs, Out, s, done);
+        case 256: return wproj_lp<256>(nn, a_fp8, A, lda, m, n, Shi, Slo, p, slabs, Out, s, done);
+        case 512: return wproj_lp<512>(nn, a_fp8, A, lda, m, n, Shi, Slo, p, slabs, Out, s, done);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+}  // namespace rsvd

@@ -89,9 +89,13 @@ def test_workspace_bytes_and_argument_checks(lib):
     assert lib.rsvd_workspace_bytes(ctypes.byref(_desc(dtype=_capi.F64)), ctypes.byref(nb64)) == 0
     assert nb64.value > nb.value
     # 1 = RSVD_ERR_INVALID_ARG, 2 = RSVD_ERR_UNSUPPORTED
-    for bad, code in ((dict(l=0), 1), (dict(q=-1), 1), (dict(lda=100), 1), (dict(l=65), 2), (dict(m=10, l=16), 2),
+    for bad, code in ((dict(l=0), 1), (dict(q=-1), 1), (dict(lda=100), 1), (dict(l=513), 2), (dict(m=10, l=16), 2),
                       (dict(dtype=7), 2), (dict(method=1), 2)):
         assert lib.rsvd_workspace_bytes(ctypes.byref(_desc(**bad)), ctypes.byref(nb)) == code, bad
+    # the wide engine (l > 64, bf16 / e4m3 A): l-wide panels, bf16 hi/lo copies, slabs -- O((m + n) l)
+    for dt, l in ((_capi.F32, 128), (_capi.BF16, 256), (_capi.FP8_E4M3, 512), (_capi.F64, 100)):
+        assert lib.rsvd_workspace_bytes(ctypes.byref(_desc(dtype=dt, l=l)), ctypes.byref(nb)) == 0, (dt, l)
+        assert 0 < nb.value < 80 * 4096 * 512 * 8, (dt, l, nb.value)
 
 
 def test_status_mapping():
