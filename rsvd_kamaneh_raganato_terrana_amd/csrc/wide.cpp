@@ -48,14 +48,21 @@ struct WideLayout {
     ProjPlan pnn, ptn;
     GramPlan gm, gn, gx;
     size_t off_Xn, off_Zn, off_Ym, off_Qm, off_T1, off_Xh, off_Xl, off_Qh, off_Ql, off_pslab, off_gslab;
-    size_t off_G, off_R, off_Rinv, off_W, off_R1, off_Uw, off_Vw, off_JX, off_JJ, off_colflag, off_sync, total;
+    size_t off_G, off_R, off_Rinv, off_W, off_R1, off_Uw, off_Vw, off_JX, off_JJ, off_M32, off_colflag, off_sync, total;
 
-    WideLayout(const rsvd_desc_t* d) : m(d->m), n(d->n), l(d->l), LP(wide_lp(d->l, d->dtype)) {
+    int64_t mpad, npad;  // bf16 panel rows, zero-padded to a multiple of 32 (wproj2 reads whole k-steps)
+
+    // a_aligned: A's base is 16-B aligned (the LDS-DMA projection kernel needs 16-B source chunks)
+    WideLayout(const rsvd_desc_t* d, bool a_aligned = true)
+        : m(d->m), n(d->n), l(d->l), LP(wide_lp(d->l, d->dtype)) {
         lowp = lowp_dtype(d->dtype);
+        mpad = rup(m, 32);
+        npad = rup(n, 32);
         int64_t pslab = 1;
         if (lowp) {
-            wnn = plan_wproj(m, n, LP);
-            wtn = plan_wproj(n, m, LP);
+            const bool v2 = d->dtype == RSVD_BF16 && a_aligned && d->lda % 8 == 0 && m >= 8;
+            wnn = plan_wproj(m, n, LP, v2);
+            wtn = plan_wproj(n, m, LP, v2);
             pslab = std::max<int64_t>(wnn.splits > 1 ? wnn.splits * m : 0, wtn.splits > 1 ? wtn.splits * n : 0);
         } else {
             pnn = plan_proj_nn<T>(m, n, 64);
@@ -80,7 +87,7 @@ struct WideLayout {
         off_Ym = take(sizeof(T) * m * LP);
         off_Qm = take(sizeof(T) * m * LP);
         off_T1 = take(sizeof(T) * mx * LP);
-        const size_t bn = lowp ? 2 * n * LP : 0, bm = lowp ? 2 * m * LP : 0;
+        const size_t bn = lowp ? 2 * npad * LP : 0, bm = lowp ? 2 * mpad * LP : 0;
         off_Xh = take(bn);
         off_Xl = take(bn);
         off_Qh = take(bm);
@@ -96,6 +103,7 @@ struct WideLayout {
         off_Vw = take(sizeof(double) * L2);
         off_JX = take(sizeof(double) * 2 * L2);
         off_JJ = take(sizeof(double) * 2 * L2);
+        off_M32 = take(sizeof(float) * 3 * L2);  // Rinv, Uw, Vw in fp32 (panel_gemm operand for fp32 panels)
         off_colflag = take(sizeof(int) * LP);
         off_sync = take(sizeof(unsigned) * 128);
         total = o;
@@ -111,6 +119,7 @@ struct WideEngine {
     T *Xn, *Zn, *Ym, *Qm, *T1, *pslab;
     bf16_t *Xh, *Xl, *Qh, *Ql;
     double *gslab, *G, *R, *Rinv, *W, *R1, *Uw, *Vw, *JX, *JJ;
+    float *Rinv32, *Uw32, *Vw32;
     int* colflag;
     unsigned* sync;
     int inter_passes = 1;  // power-iteration intermediates only carry a subspace (driver.cpp)
@@ -141,6 +150,9 @@ struct WideEngine {
         Vw = reinterpret_cast<double*>(b + L.off_Vw);
         JX = reinterpret_cast<double*>(b + L.off_JX);
         JJ = reinterpret_cast<double*>(b + L.off_JJ);
+        Rinv32 = reinterpret_cast<float*>(b + L.off_M32);
+        Uw32 = Rinv32 + (size_t)L.LP * L.LP;
+        Vw32 = Uw32 + (size_t)L.LP * L.LP;
         colflag = reinterpret_cast<int*>(b + L.off_colflag);
         sync = reinterpret_cast<unsigned*>(b + L.off_sync);
     }
@@ -197,14 +209,19 @@ struct WideEngine {
     }
 
     double tol() const { return sizeof(T) == 4 ? 1e-13 : 1e-28; }
+    // panel_gemm's operand in the panel precision: fp64 matrices as-is, fp32 copies for fp32 panels
+    const T* mat(const double* m64, const float* m32) const {
+        if constexpr (sizeof(T) == 8) return m64; else return m32;
+    }
 
     // One CholeskyQR pass Out = P chol(P^T P)^-1 (+ bf16 hi/lo of Out).  `pred`: predicated pass.
     int cholqr_pass(const T* P, int64_t rows, const GramPlan& gp, T* Out, bool sharded, bf16_t* hi, bf16_t* lo,
                     int* flag, const int* pred) {
         RSVD_CK(launch_gram_wide<T>(P, nullptr, rows, L.LP, gp, gslab, G, pred, s));
         if (sharded) RSVD_TRY(allreduce(G, (int64_t)L.LP * L.LP, RSVD_F64));
-        RSVD_CK(launch_chol_wide(G, L.l, L.LP, tol(), R, Rinv, nullptr, colflag, flag, W, pred, s));
-        RSVD_CK(launch_panel_gemm<T>(P, rows, L.LP, Rinv, 1, Out, 0, 0, hi, lo, pred, s));
+        RSVD_CK(launch_chol_wide(G, L.l, L.LP, tol(), R, Rinv, sizeof(T) == 4 ? Rinv32 : nullptr, colflag, flag, W,
+                                 pred, s));
+        RSVD_CK(launch_panel_gemm<T>(P, rows, L.LP, mat(Rinv, Rinv32), 1, Out, 0, 0, hi, lo, pred, s));
         return RSVD_OK;
     }
 
@@ -275,10 +292,15 @@ struct WideEngine {
         }
         const double sc = (d->a_scale != 0.0) ? d->a_scale : 1.0;
         RSVD_CK(launch_convert_scale<T>(Sd, S, L.l, sc, s));
-        RSVD_CK(launch_panel_gemm<T>(Qm, L.m, L.LP, Uw, 0, reinterpret_cast<T*>(U), ldu, L.l, nullptr, nullptr,
-                                     nullptr, s));
-        RSVD_CK(launch_panel_gemm<T>(Xn, L.n, L.LP, Vw, 0, reinterpret_cast<T*>(V), ldv, L.l, nullptr, nullptr,
-                                     nullptr, s));
+        if (sizeof(T) == 4) {
+            const int L2 = L.LP * L.LP;
+            RSVD_CK(launch_convert_scale<float>(Uw, Uw32, L2, 1.0, s));
+            RSVD_CK(launch_convert_scale<float>(Vw, Vw32, L2, 1.0, s));
+        }
+        RSVD_CK(launch_panel_gemm<T>(Qm, L.m, L.LP, mat(Uw, Uw32), 0, reinterpret_cast<T*>(U), ldu, L.l, nullptr,
+                                     nullptr, nullptr, s));
+        RSVD_CK(launch_panel_gemm<T>(Xn, L.n, L.LP, mat(Vw, Vw32), 0, reinterpret_cast<T*>(V), ldv, L.l, nullptr,
+                                     nullptr, nullptr, s));
         return RSVD_OK;
     }
 };
@@ -286,9 +308,16 @@ struct WideEngine {
 template <typename T>
 int wide_typed(rsvd_handle_t h, const rsvd_desc_t* d, const void* A, const void* omega, int64_t ldo, void* U,
                int64_t ldu, void* S, void* V, int64_t ldv, void* Qout, int64_t ldq) {
-    WideLayout<T> L(d);
+    WideLayout<T> L(d, (reinterpret_cast<uintptr_t>(A) & 15) == 0);
     RSVD_TRY(ensure_ws(h, L.total));
     RSVD_CK(hipMemsetAsync(h->dflags, 0, 16 * sizeof(int), h->stream));
+    if (L.lowp) {  // the zero padding rows of the bf16 panels (never written by the kernels)
+        const size_t bpr = (size_t)2 * L.LP;
+        for (size_t off : {L.off_Xh, L.off_Xl})
+            if (L.npad > L.n) RSVD_CK(hipMemsetAsync(h->ws + off + L.n * bpr, 0, (L.npad - L.n) * bpr, h->stream));
+        for (size_t off : {L.off_Qh, L.off_Ql})
+            if (L.mpad > L.m) RSVD_CK(hipMemsetAsync(h->ws + off + L.m * bpr, 0, (L.mpad - L.m) * bpr, h->stream));
+    }
     h->info.splits_nn = L.lowp ? L.wnn.splits : L.pnn.splits;
     h->info.splits_tn = L.lowp ? L.wtn.splits : L.ptn.splits;
     WideEngine<T> E(h, L, d->dtype);
@@ -312,10 +341,11 @@ int wide_typed(rsvd_handle_t h, const rsvd_desc_t* d, const void* A, const void*
 bool wide_path(const rsvd_desc_t* d) { return lowp_dtype(d->dtype) || d->l > 64; }
 
 int wide_workspace_bytes(const rsvd_desc_t* d, size_t* bytes) {
+    // the larger of the two projection plans (LDS-DMA kernel or not: decided per run by alignment)
     if (d->dtype == RSVD_F64)
         *bytes = WideLayout<double>(d).total;
     else
-        *bytes = WideLayout<float>(d).total;
+        *bytes = std::max(WideLayout<float>(d, true).total, WideLayout<float>(d, false).total);
     return RSVD_OK;
 }
 

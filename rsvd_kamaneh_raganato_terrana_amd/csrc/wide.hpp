@@ -28,8 +28,11 @@ struct WProjPlan {
     int splits;      // K splits (1 = straight into the output panel)
     int64_t chunk;   // K range per workgroup (multiple of 32)
     int blocks;      // output row blocks
+    bool v2;         // LDS-DMA pipelined kernel (bf16 A, LP >= 128, 16-B aligned columns, m >= 8)
 };
-WProjPlan plan_wproj(int64_t rows_out, int64_t K, int LP);
+// v2 requires: bf16 A with lda % 8 == 0 and a 16-B aligned base, m >= 8, and S panels zero-padded
+// to a multiple of 32 rows (the engine allocates them so).
+WProjPlan plan_wproj(int64_t rows_out, int64_t K, int LP, bool v2 = false);
 // NN: Y (m x LP, fp32) = A (m x n) * S       S = n x LP bf16 panel(s)      src/rSVD.cpp:59,66
 // TN: Z (n x LP, fp32) = A^T * S             S = m x LP bf16 panel(s)      src/rSVD.cpp:63,89
 // A is column-major (lda) bf16 (a_fp8 = 0) or e4m3 (a_fp8 = 1).  Slo == nullptr: single pass.
@@ -56,12 +59,12 @@ hipError_t launch_gram_wide(const T* P, const T* P2, int64_t rows, int LP, const
 // Also writes Rinv as fp32 when Rinv32 != nullptr.  `work`: LP x LP fp64.  `pred`: as above.
 hipError_t launch_chol_wide(const double* G, int l, int LP, double tol, double* R, double* Rinv, float* Rinv32,
                             int* colflag, int* flag, double* work, const int* pred, hipStream_t s);
-// Out (rows x LP) = In (rows x LP) * M (LP x LP fp64, applied in T; `upper`: only k <= c of M
-// is read).  Out layouts: row-major panel (ldo = 0) or the caller's column-major matrix (first
+// Out (rows x LP) = In (rows x LP) * M (LP x LP, row-major, in the panel precision T; `upper`:
+// only k <= c of M is read).  Out layouts: row-major panel (ldo = 0) or the caller's column-major matrix (first
 // `cols` columns, leading dimension ldo).  Optionally also writes the bf16 hi / lo panels of Out
 // (row-major, LP wide).  `pred`: as above.
 template <typename T>
-hipError_t launch_panel_gemm(const T* In, int64_t rows, int LP, const double* M, int upper, T* Out, int64_t ldo,
+hipError_t launch_panel_gemm(const T* In, int64_t rows, int LP, const T* M, int upper, T* Out, int64_t ldo,
                              int cols, bf16_t* hi, bf16_t* lo, const int* pred, hipStream_t s);
 // y[0..n) = (T)(x * sc)
 template <typename T>

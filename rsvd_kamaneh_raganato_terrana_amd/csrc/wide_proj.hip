@@ -259,6 +259,244 @@ __global__ __launch_bounds__(256) void wproj_kernel(const void* __restrict__ Av,
         }
 }
 
+// ------------------------------------------------------------------------------------------------
+// v2 (bf16 A, LP in {128, 256, 512}): the same products on a 512-thread workgroup fed by an
+// LDS-DMA pipeline.  Every operand tile of a 32-deep k-step -- the S hi / lo tiles [32][LP] and the
+// A tile ([32 j][WI i] for NN, [WI j][32 i] for TN) -- is copied HBM -> LDS with
+// global_load_lds_dwordx4 into a ring of NST stages (2-4 by LDS size), NST - 1 steps ahead, with
+// one raw s_barrier per k-step and a counted vmcnt wait (cdna_hip_programming.md §5 "Pipelining
+// across barriers").  glds writes lane-linear LDS, so the images are swizzled through the per-lane
+// SOURCE address: 16-B chunk c of row k lands at chunk c ^ f(k), f(k) = 2((k & 3) | ((k >> 3) & 1) << 2)
+// for the [32][...] images (ds_read_b64_tr_b16 conflict-free) and c ^ ((j >> 1) & 3) for the TN A
+// image (ds_read_b128 conflict-free; tools/ check in DESIGN.md §3.6).  The S panels must be
+// zero-padded to a multiple of 32 rows; A indices are clamped in bounds (the zero S rows cancel
+// whatever the clamped A values are).
+template <int LP> struct W2Cfg;
+template <> struct W2Cfg<128> { static constexpr int WR = 8, WC = 1, G = 8; };
+template <> struct W2Cfg<256> { static constexpr int WR = 4, WC = 2, G = 8; };
+template <> struct W2Cfg<512> { static constexpr int WR = 2, WC = 4, G = 8; };
+
+template <int LP, bool SPLIT>
+struct W2Shape {
+    static constexpr int WR = W2Cfg<LP>::WR, WC = W2Cfg<LP>::WC, G = W2Cfg<LP>::G;
+    static constexpr int WI = WR * 64;            // output rows per workgroup
+    static constexpr int NS = SPLIT ? 2 : 1;
+    static constexpr int SBYTES = KS * LP * 2;    // one S panel tile
+    static constexpr int ABYTES = KS * WI * 2;    // the A tile
+    static constexpr int STAGE = NS * SBYTES + ABYTES;
+    static constexpr int NST0 = 147456 / STAGE;
+    static constexpr int NST = NST0 > 4 ? 4 : (NST0 < 2 ? 2 : NST0);
+    static constexpr int SGL = SBYTES / 8192;     // glds per thread per S tile (512 threads x 16 B)
+    static constexpr int AGL = ABYTES / 8192;
+    static constexpr int GL = NS * SGL + AGL;     // glds per thread per stage
+    static constexpr size_t LDS = (size_t)NST * STAGE;
+};
+
+__device__ __forceinline__ int swz(int row) { return 2 * ((row & 3) | (((row >> 3) & 1) << 2)); }
+
+typedef __attribute__((address_space(3))) void* lds_void_ptr;
+
+__device__ __forceinline__ void glds16(const void* g, char* lds_wave_base) {
+    __builtin_amdgcn_global_load_lds(g, (lds_void_ptr)lds_wave_base, 16, 0, 0);
+}
+
+// LDS reads of the v2 kernel are inline asm: hipcc's waitcnt pass treats a compiler-visible LDS
+// read as possibly aliasing the in-flight LDS-DMA and drains vmcnt(0) before it, which would
+// serialise the ring (cdna_hip_programming.md §5, "Three .s-level traps").  The asm reads are
+// ordered among themselves (volatile) and retired by explicit lgkmcnt waits.
+__device__ __forceinline__ uint32_t lds_addr(const void* p) { return (uint32_t)(uintptr_t)(lds_void_ptr)p; }
+typedef __attribute__((ext_vector_type(2))) int i32x2;  // asm operands: int vectors stay in registers
+typedef __attribute__((ext_vector_type(4))) int i32x4;
+__device__ __forceinline__ i32x2 tr_read_a(uint32_t a) {
+    i32x2 v;
+    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(v) : "v"(a));
+    return v;
+}
+__device__ __forceinline__ i32x4 read128_a(uint32_t a) {
+    i32x4 v;
+    asm volatile("ds_read_b128 %0, %1" : "=v"(v) : "v"(a));
+    return v;
+}
+__device__ __forceinline__ bf16x8_t join2(i32x2 a, i32x2 b) {
+    return __builtin_bit_cast(bf16x8_t, __builtin_shufflevector(a, b, 0, 1, 2, 3));
+}
+// The wait names the registers it retires as in/out operands, so hipcc cannot read (copy, pack)
+// an asm-loaded register before the data has landed.
+__device__ __forceinline__ void wait_lgkm0(i32x2& a, i32x2& b, i32x2& c, i32x2& d) {
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d)::"memory");
+}
+__device__ __forceinline__ void wait_lgkm0(i32x2& a, i32x2& b) {
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a), "+v"(b)::"memory");
+}
+__device__ __forceinline__ void wait_lgkm0(i32x4& a) { asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a)::"memory"); }
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {  // s_waitcnt vmcnt(N), expcnt / lgkmcnt untouched
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+    __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+}
+
+template <bool NN, int LP, bool SPLIT>
+__global__ __launch_bounds__(512) void wproj2_kernel(const bf16_t* __restrict__ A, int64_t lda, int64_t rows_out,
+                                                     int64_t K, int64_t arows, const bf16_t* __restrict__ Shi,
+                                                     const bf16_t* __restrict__ Slo, float* __restrict__ out,
+                                                     int64_t slab_stride, int64_t kchunk, int nrowblk) {
+    typedef W2Shape<LP, SPLIT> SH;
+    constexpr int WR = SH::WR, G = SH::G, WI = SH::WI, NS = SH::NS, NST = SH::NST;
+    extern __shared__ __attribute__((aligned(1024))) char smem_raw[];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int r = lane & 15, h = lane >> 4, q = r >> 2, p = r & 3;
+    const int wr = w % WR, wc = w / WR;
+    const int bid = xcd_remap(blockIdx.x, gridDim.x);
+    const int rb = bid % nrowblk, sp = bid / nrowblk;
+    const int64_t row0 = (int64_t)rb * WI;
+    const int64_t kbeg = (int64_t)sp * kchunk;
+    const int64_t kend = (kbeg + kchunk < K) ? kbeg + kchunk : K;
+    const int nsteps = (int)((kend - kbeg + KS - 1) / KS);
+
+    // issue the glds of step `st` into ring slot st % NST
+    auto issue = [&](int st) {
+        char* slot = smem_raw + (size_t)(st % NST) * SH::STAGE;
+        const int64_t k0 = kbeg + (int64_t)st * KS;
+#pragma unroll
+        for (int a = 0; a < NS; ++a) {
+            const bf16_t* S = a ? Slo : Shi;
+#pragma unroll
+            for (int t = 0; t < SH::SGL; ++t) {
+                const int gi = t * 8 + w;             // wave instruction index within the tile
+                const int u = gi * 64 + lane;         // 16-B chunk of the LDS image
+                const int row = u / (LP / 8), cc = u % (LP / 8);
+                glds16(S + (k0 + row) * LP + 8 * (cc ^ swz(row)), slot + a * SH::SBYTES + gi * 1024);
+            }
+        }
+        char* at = slot + NS * SH::SBYTES;
+#pragma unroll
+        for (int t = 0; t < SH::AGL; ++t) {
+            const int gi = t * 8 + w;
+            const int u = gi * 64 + lane;
+            const bf16_t* src;
+            if (NN) {  // [32 j][WI i]: row = A column k0 + j, 8 rows i per chunk
+                const int j = u / (WI / 8), cc = u % (WI / 8);
+                int64_t jj = k0 + j;
+                jj = jj < K ? jj : K - 1;
+                int64_t i = row0 + 8 * (cc ^ swz(j));
+                i = (i + 8 <= arows) ? i : arows - 8;
+                src = A + jj * lda + i;
+            } else {  // [WI j][32 i]: row = A column row0 + j, 4 chunks of 8 rows i
+                const int j = u >> 2, cc = u & 3;
+                int64_t jc = row0 + j;
+                jc = jc < rows_out ? jc : rows_out - 1;
+                int64_t i = k0 + 8 * (cc ^ ((j >> 1) & 3));
+                i = (i + 8 <= arows) ? i : arows - 8;
+                src = A + jc * lda + i;
+            }
+            glds16(src, at + gi * 1024);
+        }
+    };
+
+    f32x4 acc[RT][G];
+#pragma unroll
+    for (int t = 0; t < RT; ++t)
+#pragma unroll
+        for (int g = 0; g < G; ++g) acc[t][g] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+    for (int st = 0; st < NST - 1; ++st)
+        if (st < nsteps) issue(st);
+
+    for (int st = 0; st < nsteps; ++st) {
+        // stage st has landed once at most the younger stages' glds are outstanding
+        if (st + NST - 2 < nsteps) wait_vm<(NST - 2) * SH::GL>(); else wait_vm<0>();
+        __builtin_amdgcn_s_barrier();
+        if (st + NST - 1 < nsteps) issue(st + NST - 1);
+        const uint32_t slot = lds_addr(smem_raw) + (uint32_t)((st % NST) * SH::STAGE);
+        const uint32_t At = slot + NS * SH::SBYTES;
+        bf16x8_t af[RT];
+        i32x2 a1[RT], a2[RT];
+        i32x4 a4[RT];
+#pragma unroll
+        for (int t = 0; t < RT; ++t) {
+            if (NN) {
+                const int col = wr * 64 + 16 * t + 4 * p;  // i within the tile
+                const int k1 = 8 * h + q, k2 = k1 + 4;
+                a1[t] = tr_read_a(At + k1 * (WI * 2) + 16 * ((col >> 3) ^ swz(k1)) + 2 * (col & 7));
+                a2[t] = tr_read_a(At + k2 * (WI * 2) + 16 * ((col >> 3) ^ swz(k2)) + 2 * (col & 7));
+            } else {
+                const int j = wr * 64 + 16 * t + r;
+                a4[t] = read128_a(At + j * 64 + 16 * (h ^ ((j >> 1) & 3)));
+            }
+        }
+        // B fragments of column tile g: hi (and lo) halves of the transposed S rows 8h+q, 8h+q+4
+        auto bread = [&](int g, i32x2* b) {
+            const int col = wc * G * 16 + 16 * g + 4 * p;
+            const int k1 = 8 * h + q, k2 = k1 + 4;
+            const uint32_t o1 = 2 * (k1 * LP + 8 * ((col >> 3) ^ swz(k1)) + (col & 7));
+            const uint32_t o2 = 2 * (k2 * LP + 8 * ((col >> 3) ^ swz(k2)) + (col & 7));
+            b[0] = tr_read_a(slot + o1);
+            b[1] = tr_read_a(slot + o2);
+            if (SPLIT) {
+                b[2] = tr_read_a(slot + SH::SBYTES + o1);
+                b[3] = tr_read_a(slot + SH::SBYTES + o2);
+            }
+        };
+        i32x2 bb[2][4];
+        bread(0, bb[0]);
+        auto wait_b = [&](i32x2* b) {
+            if (SPLIT) wait_lgkm0(b[0], b[1], b[2], b[3]);
+            else wait_lgkm0(b[0], b[1]);
+        };
+        wait_b(bb[0]);
+#pragma unroll
+        for (int t = 0; t < RT; ++t) {  // (retired by the wait above; these waits are no-ops that pin the order)
+            if (NN) wait_lgkm0(a1[t], a2[t]);
+            else wait_lgkm0(a4[t]);
+            af[t] = NN ? join2(a1[t], a2[t]) : __builtin_bit_cast(bf16x8_t, a4[t]);
+        }
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            if (g + 1 < G) bread(g + 1, bb[(g + 1) & 1]);  // next tile's fragments in flight
+            const i32x2* b = bb[g & 1];
+            const bf16x8_t bh = join2(b[0], b[1]);
+#pragma unroll
+            for (int t = 0; t < RT; ++t) acc[t][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[t], bh, acc[t][g], 0, 0, 0);
+            if (SPLIT) {
+                const bf16x8_t bl = join2(b[2], b[3]);
+#pragma unroll
+                for (int t = 0; t < RT; ++t)
+                    acc[t][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[t], bl, acc[t][g], 0, 0, 0);
+            }
+            if (g + 1 < G) wait_b(bb[(g + 1) & 1]);
+        }
+    }
+
+    float* dst = out + (int64_t)sp * slab_stride;
+#pragma unroll
+    for (int t = 0; t < RT; ++t)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int64_t row = row0 + wr * 64 + 16 * t + 4 * h + j;
+            if (row < rows_out) {
+#pragma unroll
+                for (int g = 0; g < G; ++g) dst[row * LP + wc * G * 16 + 16 * g + r] = acc[t][g][j];
+            }
+        }
+}
+
+template <bool NN, int LP, bool SPLIT>
+hipError_t wproj2_go(const void* A, int64_t lda, int64_t m, int64_t n, const bf16_t* Shi, const bf16_t* Slo,
+                     const WProjPlan& p, float* slabs, float* Out, hipStream_t s, hipEvent_t done) {
+    typedef W2Shape<LP, SPLIT> SH;
+    const int64_t rows_out = NN ? m : n, K = NN ? n : m;
+    float* o = p.splits == 1 ? Out : slabs;
+    const int64_t stride = rows_out * LP;
+    hipLaunchKernelGGL((wproj2_kernel<NN, LP, SPLIT>), dim3(p.blocks * p.splits), dim3(512), SH::LDS, s,
+                       reinterpret_cast<const bf16_t*>(A), lda, rows_out, K, m, Shi, Slo, o, stride, p.chunk, p.blocks);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess && done) e = hipEventRecord(done, s);
+    if (e != hipSuccess || p.splits == 1) return e;
+    return launch_sum_slabs<float>(slabs, stride, p.splits, stride, Out, s);
+}
+
 template <bool FP8, bool NN, int LP, bool SPLIT>
 hipError_t wproj_go(const void* A, int64_t lda, int64_t m, int64_t n, const bf16_t* Shi, const bf16_t* Slo,
                     const WProjPlan& p, float* slabs, float* Out, hipStream_t s, hipEvent_t done) {
@@ -280,6 +518,14 @@ template <int LP>
 hipError_t wproj_lp(int nn, int fp8, const void* A, int64_t lda, int64_t m, int64_t n, const bf16_t* Shi,
                     const bf16_t* Slo, const WProjPlan& p, float* slabs, float* Out, hipStream_t s, hipEvent_t d) {
     const bool split = Slo != nullptr;
+    if constexpr (LP >= 128) {
+        if (p.v2) {
+            if (nn) return split ? wproj2_go<true, LP, true>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d)
+                                 : wproj2_go<true, LP, false>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d);
+            return split ? wproj2_go<false, LP, true>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d)
+                         : wproj2_go<false, LP, false>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d);
+        }
+    }
 #define GO(F, N, SP) return wproj_go<F, N, LP, SP>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d)
     if (fp8) {
         if (nn) { if (split) GO(true, true, true); GO(true, true, false); }
@@ -300,11 +546,12 @@ bool wproj_supported_lp(int LP) {
 
 int wproj_rows_per_block(int LP) { return LP <= 128 ? 256 : (LP == 256 ? 128 : 64); }
 
-WProjPlan plan_wproj(int64_t rows_out, int64_t K, int LP) {
+WProjPlan plan_wproj(int64_t rows_out, int64_t K, int LP, bool v2) {
     WProjPlan p;
-    const int WI = wproj_rows_per_block(LP);
+    p.v2 = v2 && LP >= 128;
+    const int WI = p.v2 ? (LP == 128 ? 512 : (LP == 256 ? 256 : 128)) : wproj_rows_per_block(LP);
     p.blocks = (int)((rows_out + WI - 1) / WI);
-    const int target = LP >= 512 ? 256 : 512;  // LP = 512 runs one workgroup per CU (registers)
+    const int target = (p.v2 || LP >= 512) ? 256 : 512;  // one workgroup per CU (LDS ring / registers)
     int64_t splits = (target + p.blocks - 1) / p.blocks;
     const int64_t max_by_work = K / (KS * 8);
     if (splits > max_by_work) splits = max_by_work;

@@ -130,9 +130,13 @@ __global__ void gram_reduce_kernel(const double* __restrict__ slabs, int nblk, i
 }
 
 // ------------------------------------------------------------------------------------------------
-// Cholesky + inverse, one workgroup of 1024 threads (16 waves).  W (work) holds the Gram being
-// reduced; R and Rinv are the outputs; the 16x16 inverse diagonal blocks stay in LDS.
-constexpr int kCholThreads = 1024;
+// Cholesky + inverse, one workgroup of kCholThreads threads.  W (work) holds the Gram being
+// reduced; R and Rinv are the outputs; the 16x16 inverse diagonal blocks stay in LDS.  Per 16-
+// column block p: wave 0 factors the diagonal block in registers (lane j owns column j, pivots and
+// rows broadcast with v_readlane: no workgroup barriers inside), all waves then form the strip
+// R[p][p+1..] = D^-T W[p][p+1..] and the trailing update W -= R[p]^T R[p] on the fp64 MFMA
+// (3 barriers per block).  R^-1 is assembled bottom-up by block rows (1 barrier per block).
+constexpr int kCholThreads = 512;
 
 // acc += X^T Y for 16x16 fp64 blocks X (ldx), Y (ldy) given row-major: acc[i][j] += sum_k X[k][i] Y[k][j]
 __device__ __forceinline__ f64x4 mma_tn16(const double* X, int64_t ldx, const double* Y, int64_t ldy, f64x4 acc,
@@ -149,6 +153,13 @@ __device__ __forceinline__ f64x4 mma_nn16(const double* X, int64_t ldx, const do
     return acc;
 }
 
+__device__ __forceinline__ double readlane_d(double v, int lane) {
+    const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
+    const unsigned lo = __builtin_amdgcn_readlane((unsigned)u, lane);
+    const unsigned hi = __builtin_amdgcn_readlane((unsigned)(u >> 32), lane);
+    return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
+}
+
 __global__ __launch_bounds__(kCholThreads) void chol_wide_kernel(const double* __restrict__ G, int l, int LP,
                                                                  double tol, double* __restrict__ W,
                                                                  double* __restrict__ R, double* __restrict__ Rinv,
@@ -158,9 +169,9 @@ __global__ __launch_bounds__(kCholThreads) void chol_wide_kernel(const double* _
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
     const int np = LP / 16;
     double* Dinv = reinterpret_cast<double*>(smem_raw);  // [np][16][16]
-    double* D = Dinv + np * 256;                         // [16][17] current diagonal block
-    double* d0 = D + 16 * 17;                            // [LP] original diagonal of G
-    int* bad = reinterpret_cast<int*>(d0 + LP);          // [16]
+    double* d0 = Dinv + np * 256;                        // [LP] original diagonal of G
+    double* Tsc = d0 + LP;                               // [waves][16][16] per-wave scratch
+    int* bad = reinterpret_cast<int*>(Tsc + (kCholThreads / 64) * 256);  // [16]
     const int tid = threadIdx.x, nt = blockDim.x;
     const int lane = tid & 63, wv = tid >> 6, nw = nt >> 6;
     const int r = lane & 15, h = lane >> 4;
@@ -180,58 +191,62 @@ __global__ __launch_bounds__(kCholThreads) void chol_wide_kernel(const double* _
 
     for (int p = 0; p < np; ++p) {
         const int p16 = 16 * p;
-        // (1) factor the diagonal block (upper Cholesky, in LDS), breakdowns -> identity rows
-        for (int e = tid; e < 256; e += nt) D[(e / 16) * 17 + e % 16] = W[(int64_t)(p16 + e / 16) * LP + p16 + e % 16];
-        if (tid < 16) bad[tid] = 0;
-        __syncthreads();
-        for (int k = 0; k < 16; ++k) {
-            const int gk = p16 + k;
-            if (tid == 0) {
-                double d = D[k * 17 + k];
-                if (gk >= l) {
-                    D[k * 17 + k] = 1.0;
-                    for (int j = k + 1; j < 16; ++j) D[k * 17 + j] = 0.0;
-                } else if (!(d > tol * d0[gk]) || !(d0[gk] > 0.0) || !isfinite(d)) {
-                    bad[k] = 1;
-                    D[k * 17 + k] = 1.0;
-                    for (int j = k + 1; j < 16; ++j) D[k * 17 + j] = 0.0;
-                } else {
-                    const double rk = sqrt(d), inv = 1.0 / rk;
-                    D[k * 17 + k] = rk;
-                    for (int j = k + 1; j < 16; ++j) D[k * 17 + j] *= inv;
+        double* Di = Dinv + p * 256;
+        // (1) wave 0: upper Cholesky of the 16x16 diagonal block and its inverse, in registers
+        if (wv == 0) {
+            const int j = lane & 15;
+            double col[16];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) col[i] = W[(int64_t)(p16 + i) * LP + p16 + j];  // D[i][j]
+            int badmask = 0;
+#pragma unroll
+            for (int k = 0; k < 16; ++k) {
+                const int gk = p16 + k;
+                const double dkk = readlane_d(col[k], k);
+                const bool pad = gk >= l;
+                const bool isbad = !pad && (!(dkk > tol * d0[gk]) || !(d0[gk] > 0.0) || !isfinite(dkk));
+                if (isbad) badmask |= 1 << k;
+                const bool unit = pad || isbad;
+                const double rk = unit ? 1.0 : sqrt(dkk);
+                const double inv = 1.0 / rk;
+                if (j > k) col[k] = unit ? 0.0 : col[k] * inv;
+                if (j == k) col[k] = rk;
+#pragma unroll
+                for (int i = k + 1; i < 16; ++i) {
+                    const double dki = readlane_d(col[k], i);  // D[k][i]
+                    if (j >= i) col[i] -= dki * col[k];
                 }
             }
-            __syncthreads();
-            if (tid < 256) {
-                const int i = tid / 16, j = tid % 16;
-                if (i > k && j >= i) D[i * 17 + j] -= D[k * 17 + i] * D[k * 17 + j];
-            }
-            __syncthreads();
-        }
-        if (tid < 16) {
-            if (bad[tid]) {
-                colflag[p16 + tid] = 1;
-                atomicAdd(flag, 1);
-            }
-        }
-        // (2) Dinv = D^-1 (upper): one thread per column j, back substitution
-        double* Di = Dinv + p * 256;
-        if (tid < 16) {
-            const int j = tid;
-            for (int i = 0; i < 16; ++i) Di[i * 16 + j] = 0.0;
-            Di[j * 16 + j] = 1.0 / D[j * 17 + j];
-            for (int i = j - 1; i >= 0; --i) {
+            // zero the strictly lower part of this column (it held the symmetric copy)
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+                if (i > j) col[i] = 0.0;
+            // Dinv column j by back substitution: x[i] = -(sum_{k>i} D[i][k] x[k]) / D[i][i]
+            double x[16];
+#pragma unroll
+            for (int i = 15; i >= 0; --i) {
                 double s = 0.0;
-                for (int k = i + 1; k <= j; ++k) s += D[i * 17 + k] * Di[k * 16 + j];
-                Di[i * 16 + j] = -s / D[i * 17 + i];
+#pragma unroll
+                for (int k = i + 1; k < 16; ++k) s += readlane_d(col[i], k) * x[k];  // D[i][k] from lane k
+                const double dii = readlane_d(col[i], i);
+                x[i] = (i == j) ? 1.0 / dii : ((i < j) ? -s / dii : 0.0);
             }
-        }
-        for (int e = tid; e < 256; e += nt) {
-            const int i = e / 16, j = e % 16;
-            R[(int64_t)(p16 + i) * LP + p16 + j] = (j >= i) ? D[i * 17 + j] : 0.0;
+            if (lane < 16) {
+#pragma unroll
+                for (int i = 0; i < 16; ++i) {
+                    Di[i * 16 + j] = x[i];
+                    R[(int64_t)(p16 + i) * LP + p16 + j] = col[i];
+                }
+            }
+            if (lane < 16) bad[lane] = (badmask >> lane) & 1;
+            if (lane == 0 && badmask) {
+                atomicAdd(flag, __popc(badmask));
+                for (int k = 0; k < 16; ++k)
+                    if (badmask & (1 << k)) colflag[p16 + k] = 1;
+            }
         }
         __syncthreads();
-        // (3) strip: R[p][jb] = Dinv^T W[p][jb], or 0 for rows that broke down (one wave per block)
+        // (2) strip: R[p][jb] = Dinv^T W[p][jb], or 0 for rows that broke down (one wave per block)
         for (int jb = p + 1 + wv; jb < np; jb += nw) {
             f64x4 acc = MD::zero();
             acc = mma_tn16(Di, 16, W + (int64_t)p16 * LP + 16 * jb, LP, acc, r, h);
@@ -242,7 +257,7 @@ __global__ __launch_bounds__(kCholThreads) void chol_wide_kernel(const double* _
             }
         }
         __syncthreads();
-        // (4) trailing update W[ib][jb] -= R[p][ib]^T R[p][jb], p < ib <= jb
+        // (3) trailing update W[ib][jb] -= R[p][ib]^T R[p][jb], p < ib <= jb
         const int nt2 = np - p - 1;
         const int ntri = nt2 * (nt2 + 1) / 2;
         for (int t = wv; t < ntri; t += nw) {
@@ -264,6 +279,7 @@ __global__ __launch_bounds__(kCholThreads) void chol_wide_kernel(const double* _
         __syncthreads();
     }
     // Rinv, bottom block row first: Rinv[p][p] = Dinv_p, Rinv[p][jb] = -Dinv_p sum_{p<k<=jb} R[p][k] Rinv[k][jb]
+    double* Tw = Tsc + wv * 256;
     for (int p = np - 1; p >= 0; --p) {
         const double* Di = Dinv + p * 256;
         const int p16 = 16 * p;
@@ -273,9 +289,6 @@ __global__ __launch_bounds__(kCholThreads) void chol_wide_kernel(const double* _
             for (int kb = p + 1; kb <= jb; ++kb)
                 acc = mma_nn16(R + (int64_t)p16 * LP + 16 * kb, LP, Rinv + (int64_t)(16 * kb) * LP + 16 * jb, LP, acc,
                                r, h);
-            // T (16x16, D layout) -> LDS scratch of this wave, then Rinv[p][jb] = -Di T
-            double* Tw = D;  // D is free now; waves use disjoint 16x16 regions beyond it
-            Tw = reinterpret_cast<double*>(bad + 16) + wv * 256;
 #pragma unroll
             for (int j = 0; j < 4; ++j) Tw[MD::row(h, j) * 16 + r] = acc[j];
             __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's LDS stores landed
@@ -283,8 +296,7 @@ __global__ __launch_bounds__(kCholThreads) void chol_wide_kernel(const double* _
             f64x4 o = MD::zero();
             o = mma_nn16(Di, 16, Tw, 16, o, r, h);
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
-                Rinv[(int64_t)(p16 + MD::row(h, j)) * LP + 16 * jb + r] = -o[j];
+            for (int j = 0; j < 4; ++j) Rinv[(int64_t)(p16 + MD::row(h, j)) * LP + 16 * jb + r] = -o[j];
             __builtin_amdgcn_wave_barrier();
         }
         __syncthreads();
@@ -295,22 +307,26 @@ __global__ __launch_bounds__(kCholThreads) void chol_wide_kernel(const double* _
 
 size_t chol_lds_bytes(int LP) {
     const int np = LP / 16;
-    return (size_t)np * 256 * 8 + 16 * 17 * 8 + (size_t)LP * 8 + 16 * 4 + (size_t)(kCholThreads / 64) * 256 * 8 + 64;
+    return (size_t)np * 256 * 8 + (size_t)LP * 8 + (size_t)(kCholThreads / 64) * 256 * 8 + 16 * 4 + 64;
 }
 
 // ------------------------------------------------------------------------------------------------
-// Out = In * M.  Workgroup = 64 rows x CT columns (4 waves x 16 rows), K in chunks of 64 staged
-// through LDS.  fp32 panels: v_mfma_f32_16x16x4_f32 with a lane's float4 of In feeding 4 MFMAs
-// (k = k0 + 4h + t); fp64 panels: f64 MFMA with double2 (k = k0 + 2h + t, 8-deep steps).
+// Out = In * M.  Workgroup = 64 rows x CT columns (4 waves x 16 rows; LP > CT -> column blocks,
+// adjacent on one XCD so In rows are re-read from L2).  K runs in chunks staged through LDS with
+// 16-B loads of M (given in T precision); a lane's In vector (float4 / double2) feeds VW MFMAs
+// (k-slot h of MFMA t <-> k = k0 + VW h + t), the chunk's In vectors are loaded before the M
+// staging so their latency overlaps it.  fp32: v_mfma_f32_16x16x4_f32; fp64: the f64 form.
+// Upper-triangular M (R^-1): K stops at the block's last column (no per-tile skipping inside the
+// unrolled MFMA loop: a data-dependent skip there makes hipcc shuffle the accumulators).
 template <typename T> struct PG;
 template <> struct PG<float> {
     typedef float4 V;
-    static constexpr int VW = 4;
+    static constexpr int VW = 4, PAD = 4;  // pitch CT+4: the two k-rows of a half-wave hit disjoint banks
     typedef Mfma<float> M;
 };
 template <> struct PG<double> {
     typedef double2 V;
-    static constexpr int VW = 2;
+    static constexpr int VW = 2, PAD = 8;
     typedef Mfma<double> M;
 };
 
@@ -323,7 +339,7 @@ __device__ __forceinline__ float bf2f(bf16_t b) { return __uint_as_float((uint32
 
 template <typename T, int CT>
 __global__ __launch_bounds__(256) void panel_gemm_kernel(const T* __restrict__ In, int64_t rows, int LP,
-                                                         const double* __restrict__ Mm, int upper, T* __restrict__ Out,
+                                                         const T* __restrict__ Mm, int upper, T* __restrict__ Out,
                                                          int64_t ldo, int cols, bf16_t* __restrict__ hi,
                                                          bf16_t* __restrict__ lo, int ncb,
                                                          const int* __restrict__ pred) {
@@ -333,12 +349,14 @@ __global__ __launch_bounds__(256) void panel_gemm_kernel(const T* __restrict__ I
     typedef typename C::V V;
     constexpr int VW = C::VW;
     constexpr int G = CT / 16;
-    constexpr int KC = 64;
+    constexpr int NJ = 4;             // k-steps of 4 VW per chunk
+    constexpr int KC = NJ * 4 * VW;   // 64 (fp32) / 32 (fp64)
+    constexpr int MP = CT + C::PAD;   // LDS pitch of the M chunk
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-    T* Ms = reinterpret_cast<T*>(smem_raw);  // [KC][CT]
+    T* Ms = reinterpret_cast<T*>(smem_raw);  // [KC][MP]
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int r = lane & 15, h = lane >> 4;
-    const int bid = blockIdx.x;
+    const int bid = xcd_remap(blockIdx.x, gridDim.x);
     const int cb = bid % ncb;
     const int64_t row0 = (int64_t)(bid / ncb) * 64;
     const int c0 = cb * CT;
@@ -349,28 +367,42 @@ __global__ __launch_bounds__(256) void panel_gemm_kernel(const T* __restrict__ I
 #pragma unroll
     for (int g = 0; g < G; ++g) acc[g] = M::zero();
     for (int kc = 0; kc < kmax; kc += KC) {
-        __syncthreads();
-        for (int e = tid; e < KC * CT; e += 256) {
-            const int k = kc + e / CT, c = c0 + e % CT;
-            Ms[e] = (k < LP && c < LP) ? (T)Mm[(int64_t)k * LP + c] : T(0);
+        V a[NJ];
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+            const int k = kc + 4 * VW * j + VW * h;
+            if (rok && k < LP) {
+                a[j] = *reinterpret_cast<const V*>(In + row * LP + k);
+            } else {
+                T* e = reinterpret_cast<T*>(&a[j]);
+#pragma unroll
+                for (int t = 0; t < VW; ++t) e[t] = T(0);
+            }
+        }
+        __syncthreads();  // the previous chunk's LDS reads are done
+        for (int e = tid; e < KC * CT / VW; e += 256) {
+            const int kr = e / (CT / VW), cv = (e % (CT / VW)) * VW;
+            V v;
+            if (kc + kr < LP && c0 + cv < LP) {
+                v = *reinterpret_cast<const V*>(Mm + (int64_t)(kc + kr) * LP + c0 + cv);
+            } else {
+                T* x = reinterpret_cast<T*>(&v);
+#pragma unroll
+                for (int t = 0; t < VW; ++t) x[t] = T(0);
+            }
+            *reinterpret_cast<V*>(Ms + kr * MP + cv) = v;
         }
         __syncthreads();
-        const int kend = (kc + KC < kmax) ? kc + KC : kmax;
-        for (int k0 = kc; k0 < kend; k0 += 4 * VW) {
-            V a;
-            T* ae = reinterpret_cast<T*>(&a);
-            if (rok) a = *reinterpret_cast<const V*>(In + row * LP + k0 + VW * h);
-            else
 #pragma unroll
-                for (int t = 0; t < VW; ++t) ae[t] = T(0);
+        for (int j = 0; j < NJ; ++j) {
+            const int k0 = kc + 4 * VW * j;
+            if (k0 >= kmax) break;
+            const T* ae = reinterpret_cast<const T*>(&a[j]);
 #pragma unroll
             for (int t = 0; t < VW; ++t) {
-                const int kl = k0 - kc + VW * h + t;
+                const T* mrow = Ms + (4 * VW * j + VW * h + t) * MP + r;
 #pragma unroll
-                for (int g = 0; g < G; ++g) {
-                    if (upper && c0 + 16 * g + 15 < k0) continue;  // wave-uniform: M[k][c] = 0 for k > c
-                    acc[g] = M::mma(ae[t], Ms[kl * CT + 16 * g + r], acc[g]);
-                }
+                for (int g = 0; g < G; ++g) acc[g] = M::mma(ae[t], mrow[16 * g], acc[g]);
             }
         }
     }
@@ -396,7 +428,7 @@ __global__ __launch_bounds__(256) void panel_gemm_kernel(const T* __restrict__ I
     }
     // column-major caller output: transpose through LDS, store column segments contiguously
     __syncthreads();
-    T* Ts = Ms;  // [CT][64 + 1]
+    T* Ts = Ms;  // [CT][64 + 1]  (fits: KC * MP >= CT * 65 is checked at launch)
 #pragma unroll
     for (int g = 0; g < G; ++g)
 #pragma unroll
@@ -535,14 +567,15 @@ hipError_t launch_chol_wide(const double* G, int l, int LP, double tol, double* 
 }
 
 template <typename T>
-hipError_t launch_panel_gemm(const T* In, int64_t rows, int LP, const double* Mm, int upper, T* Out, int64_t ldo,
+hipError_t launch_panel_gemm(const T* In, int64_t rows, int LP, const T* Mm, int upper, T* Out, int64_t ldo,
                              int cols, bf16_t* hi, bf16_t* lo, const int* pred, hipStream_t s) {
     if (!Mm || LP % 16) return hipErrorInvalidValue;
     const int64_t rb = (rows + 63) / 64;
 #define GO(CT)                                                                                                  \
     {                                                                                                           \
         const int ncb = (LP + CT - 1) / CT;                                                                     \
-        const size_t lds = std::max<size_t>((size_t)64 * CT, (size_t)CT * 65) * sizeof(T);                      \
+        constexpr int KC = 16 * PG<T>::VW;                                                                      \
+        const size_t lds = std::max<size_t>((size_t)KC * (CT + PG<T>::PAD), (size_t)CT * 65) * sizeof(T);       \
         hipLaunchKernelGGL((panel_gemm_kernel<T, CT>), dim3((unsigned)(rb * ncb)), dim3(256), lds, s, In, rows, \
                            LP, Mm, upper, Out, ldo, cols, hi, lo, ncb, pred);                                   \
         return hipGetLastError();                                                                               \
@@ -592,7 +625,7 @@ hipError_t launch_convert_scale(const double* x, T* y, int n, double sc, hipStre
     template hipError_t launch_convert_scale<T>(const double*, T*, int, double, hipStream_t);                                             \
     template hipError_t launch_gram_wide<T>(const T*, const T*, int64_t, int, const GramPlan&, double*, double*,    \
                                             const int*, hipStream_t);                                               \
-    template hipError_t launch_panel_gemm<T>(const T*, int64_t, int, const double*, int, T*, int64_t, int, bf16_t*, \
+    template hipError_t launch_panel_gemm<T>(const T*, int64_t, int, const T*, int, T*, int64_t, int, bf16_t*,      \
                                              bf16_t*, const int*, hipStream_t);                                     \
     template hipError_t launch_repair_panel<T>(const T*, int64_t, int, int, const int*, const int*, uint64_t,       \
                                                int64_t, int64_t, T*, hipStream_t);                                  \

@@ -85,14 +85,85 @@ __device__ __forceinline__ void jacobi_angle(double a, double b, double g, doubl
     s = c * t;
 }
 
-constexpr int GS = 33;  // LDS pitch of the 32 x 32 blocks
+constexpr int GS = 33;       // LDS pitch of the 32 x 32 blocks
+constexpr int kInnerSweeps = 1;
+
+// Full-precision fp64 reciprocal square root / reciprocal from the hardware estimates (two
+// Newton steps each): the inner rotations need c^2 + s^2 = 1 to rounding, not IEEE division.
+__device__ __forceinline__ double rsqrt_nr(double d) {
+    double y = __builtin_amdgcn_rsq(d);
+    y = y * (1.5 - 0.5 * d * y * y);
+    return y * (1.5 - 0.5 * d * y * y);
+}
+__device__ __forceinline__ double rcp_nr(double d) {
+    double y = __builtin_amdgcn_rcp(d);
+    y = y * (2.0 - d * y);
+    return y * (2.0 - d * y);
+}
+
+// jacobi_angle on the scaled operands (no overflow / underflow for any finite a, b, g)
+__device__ __forceinline__ void pair_angle(const double* G, int p, int q, double tol2, double negl, double& c,
+                                           double& s, bool& rot) {
+    const double a = G[p * GS + p], b = G[q * GS + q], g = G[p * GS + q];
+    rot = g != 0.0 && g * g > tol2 * a * b && a > negl && b > negl;
+    const double d = b - a, g2 = 2.0 * g;
+    const double inv = rcp_nr(fmax(fmax(fabs(d), fabs(g2)), 1e-300));
+    const double ds = fabs(d) * inv, gs = fabs(g2) * inv;
+    const double hyp2 = ds * ds + gs * gs;  // in [1, 2]
+    const double tmag = gs * rcp_nr(ds + hyp2 * rsqrt_nr(hyp2));
+    const double t = ((d >= 0.0) == (g >= 0.0)) ? tmag : -tmag;
+    const double cc = rsqrt_nr(1.0 + t * t);
+    c = rot ? cc : 1.0;
+    s = rot ? cc * t : 0.0;
+}
+
+size_t block_jacobi_lds(int LP) { return ((size_t)32 * (LP + 1) + 3 * 32 * GS) * sizeof(double); }
+
+// Stage the 32 columns col(0..31) of a column-major LP x LP matrix into LDS rows of pitch LP + 1.
+template <typename F>
+__device__ __forceinline__ void stage_pair(double* Xs, const double* __restrict__ S, int LP, F col) {
+    const int XP = LP + 1;
+    const int per = LP / 2;  // double2 per column
+    for (int e = threadIdx.x; e < 32 * per; e += 256) {
+        const int k = e / per, i = 2 * (e % per);
+        const double2 v = *reinterpret_cast<const double2*>(S + (int64_t)col(k) * LP + i);
+        Xs[k * XP + i] = v.x;
+        Xs[k * XP + i + 1] = v.y;
+    }
+}
+
+// D[:, col(j)] = sum_k Xs[k][:] Jp[k][j] for the 32 pair columns (fp64 MFMA), wave w -> row tiles w, w+4, ...
+template <typename F>
+__device__ __forceinline__ void apply_pair(const double* Xs, const double* Jp, double* __restrict__ D, int LP, F col,
+                                           int w, int r, int h) {
+    const int XP = LP + 1;
+    for (int it = w; it < LP / 16; it += 4) {
+        const int i0 = 16 * it;
+        f64x4 acc0 = MD::zero(), acc1 = MD::zero();
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) {
+            const double a = Xs[(4 * kk + h) * XP + i0 + r];
+            acc0 = MD::mma(a, Jp[(4 * kk + h) * GS + r], acc0);
+            acc1 = MD::mma(a, Jp[(4 * kk + h) * GS + 16 + r], acc1);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            D[(int64_t)col(r) * LP + i0 + MD::row(h, j)] = acc0[j];
+            D[(int64_t)col(16 + r) * LP + i0 + MD::row(h, j)] = acc1[j];
+        }
+    }
+}
 
 __global__ __launch_bounds__(256) void block_jacobi_kernel(const double* __restrict__ R, int l, int LP,
                                                            double* __restrict__ Xb, double* __restrict__ Jb,
                                                            unsigned* __restrict__ sync, int* __restrict__ info) {
-    __shared__ double Gs[32 * GS], Jp[32 * GS];
-    __shared__ double cs_[16], sn_[16];
-    __shared__ int flags[4];
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    const int XP = LP + 1;
+    double* Xs = reinterpret_cast<double*>(smem_raw);  // [32][LP + 1]: the pair's columns
+    double* Ga = Xs + 32 * XP;                         // [32][GS] x 2: the pair Gram, double-buffered
+    double* Gb = Ga + 32 * GS;
+    double* Jp = Gb + 32 * GS;                         // [32][GS] accumulated inner rotation
+    __shared__ int flags[8];
     __shared__ double fro;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int r = lane & 15, h = lane >> 4;
@@ -133,29 +204,36 @@ __global__ __launch_bounds__(256) void block_jacobi_kernel(const double* __restr
         for (int round = 0; round < NB - 1; ++round) {
             int P, Q;
             rr_pair(round, wg, NB, P, Q);
-            const double* Xs = Xb + (size_t)par * L2;
-            const double* Js = Jb + (size_t)par * L2;
+            const double* Xsrc = Xb + (size_t)par * L2;
+            const double* Jsrc = Jb + (size_t)par * L2;
             double* Xd = Xb + (size_t)(1 - par) * L2;
             double* Jd = Jb + (size_t)(1 - par) * L2;
             auto col = [&](int k) { return k < 16 ? 16 * P + k : 16 * Q + k - 16; };
-            // 1. Gp = X_pair^T X_pair: wave w -> 16 x 16 tile (w >> 1, w & 1)
-            {
-                const int ta = w >> 1, tb = w & 1;
-                const double* xa = Xs + (int64_t)col(16 * ta + r) * LP;
-                const double* xb = Xs + (int64_t)col(16 * tb + r) * LP;
-                f64x4 acc = MD::zero();
-                for (int i0 = 0; i0 < LP; i0 += 4) acc = MD::mma(xa[i0 + h], xb[i0 + h], acc);
-#pragma unroll
-                for (int j = 0; j < 4; ++j) Gs[(16 * ta + MD::row(h, j)) * GS + 16 * tb + r] = acc[j];
-            }
-            if (tid < 4) flags[tid] = 0;
+            // 1. the pair's columns of X into LDS
+            stage_pair(Xs, Xsrc, LP, col);
+            if (tid < 8) flags[tid] = 0;
             for (int e = tid; e < 32 * 32; e += 256) Jp[(e / 32) * GS + e % 32] = (e / 32 == e % 32) ? 1.0 : 0.0;
             __syncthreads();
-            // 2. convergence test on the fresh Gram: any pair above threshold?
+            // 2. Gp = X_pair^T X_pair: wave w -> tile (w >> 1, w & 1), four independent MFMA chains
+            {
+                const int ta = w >> 1, tb = w & 1;
+                const double* xa = Xs + (16 * ta + r) * XP + h;
+                const double* xb = Xs + (16 * tb + r) * XP + h;
+                f64x4 acc[4] = {MD::zero(), MD::zero(), MD::zero(), MD::zero()};
+                for (int i0 = 0; i0 < LP; i0 += 16) {
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) acc[u] = MD::mma(xa[i0 + 4 * u], xb[i0 + 4 * u], acc[u]);
+                }
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    Ga[(16 * ta + MD::row(h, j)) * GS + 16 * tb + r] = (acc[0][j] + acc[1][j]) + (acc[2][j] + acc[3][j]);
+            }
+            __syncthreads();
+            // 3. convergence test on the fresh Gram
             for (int e = tid; e < 32 * 32; e += 256) {
                 const int i = e / 32, j = e % 32;
                 if (i < j) {
-                    const double a = Gs[i * GS + i], b = Gs[j * GS + j], g = Gs[i * GS + j];
+                    const double a = Ga[i * GS + i], b = Ga[j * GS + j], g = Ga[i * GS + j];
                     if (g != 0.0 && g * g > tol2 * a * b && a > negl && b > negl) {
                         flags[0] = 1;
                         if (g * g > quad2 * a * b) flags[1] = 1;
@@ -163,84 +241,75 @@ __global__ __launch_bounds__(256) void block_jacobi_kernel(const double* __restr
                 }
             }
             __syncthreads();
-            const bool work = flags[0] != 0;
-            if (work) {
+            if (flags[0]) {
                 if (tid == 0) {
                     __hip_atomic_store(sync + 4 + sweep, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     if (flags[1]) __hip_atomic_store(sync + 36 + sweep, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
-                // 3. cyclic Jacobi on Gp (two-sided updates), accumulated into Jp
-                for (int isw = 0; isw < 4; ++isw) {
-                    if (tid == 0) flags[2] = 0;
-                    __syncthreads();
+                // 4. inner cyclic Jacobi on Gp: thread (k, k2) rotates the 2x2 block (pair k rows, pair k2
+                //    columns) from both sides into the other G buffer -- one barrier per inner round
+                const int k = tid >> 4, k2 = tid & 15;
+                double* cur = Ga;
+                double* nxt = Gb;
+                for (int isw = 0; isw < kInnerSweeps; ++isw) {
+                    bool any = false;
                     for (int ir = 0; ir < 31; ++ir) {
-                        if (tid < 16) {
-                            int p, q;
-                            rr_pair(ir, tid, 32, p, q);
-                            const double a = Gs[p * GS + p], b = Gs[q * GS + q], g = Gs[p * GS + q];
-                            double c = 1.0, s = 0.0;
-                            if (g != 0.0 && g * g > tol2 * a * b && a > negl && b > negl) {
-                                jacobi_angle(a, b, g, c, s);
-                                flags[2] = 1;
+                        int p, q, p2, q2;
+                        rr_pair(ir, k, 32, p, q);
+                        rr_pair(ir, k2, 32, p2, q2);
+                        // every lane computes the angle of its column pair k2; the row pair k's angle
+                        // comes from the lane of this wave with k2 == k (lane 16 (k & 3) + k)
+                        double c2, s2;
+                        bool r2;
+                        pair_angle(cur, p2, q2, tol2, negl, c2, s2, r2);
+                        const int src = 16 * (k & 3) + k;
+                        const double c1 = __shfl(c2, src, 64), s1 = __shfl(s2, src, 64);
+                        const bool r1 = __shfl((int)r2, src, 64) != 0;
+                        const double b00 = cur[p * GS + p2], b01 = cur[p * GS + q2];
+                        const double b10 = cur[q * GS + p2], b11 = cur[q * GS + q2];
+                        // left: rows (p, q) <- (c1 row_p - s1 row_q, s1 row_p + c1 row_q)
+                        const double l00 = c1 * b00 - s1 * b10, l01 = c1 * b01 - s1 * b11;
+                        const double l10 = s1 * b00 + c1 * b10, l11 = s1 * b01 + c1 * b11;
+                        // right: cols (p2, q2) <- (c2 col_p2 - s2 col_q2, s2 col_p2 + c2 col_q2)
+                        nxt[p * GS + p2] = c2 * l00 - s2 * l01;
+                        nxt[p * GS + q2] = s2 * l00 + c2 * l01;
+                        nxt[q * GS + p2] = c2 * l10 - s2 * l11;
+                        nxt[q * GS + q2] = s2 * l10 + c2 * l11;
+                        if (k == k2 && r1) any = true;
+                        // Jp <- Jp J: columns (p2, q2) of pair k2, rows k and k + 16 (disjoint per thread)
+                        if (r2) {
+#pragma unroll
+                            for (int rr = 0; rr < 2; ++rr) {
+                                const int row = k + 16 * rr;
+                                const double jp = Jp[row * GS + p2], jq = Jp[row * GS + q2];
+                                Jp[row * GS + p2] = c2 * jp - s2 * jq;
+                                Jp[row * GS + q2] = s2 * jp + c2 * jq;
                             }
-                            cs_[tid] = c;
-                            sn_[tid] = s;
                         }
                         __syncthreads();
-                        // columns p, q of Gs and Jp
-                        for (int e = tid; e < 16 * 32; e += 256) {
-                            const int k = e / 32, i = e % 32;
-                            const double c = cs_[k], s = sn_[k];
-                            if (s == 0.0) continue;
-                            int p, q;
-                            rr_pair(ir, k, 32, p, q);
-                            const double gp = Gs[i * GS + p], gq = Gs[i * GS + q];
-                            Gs[i * GS + p] = c * gp - s * gq;
-                            Gs[i * GS + q] = s * gp + c * gq;
-                            const double jp = Jp[i * GS + p], jq = Jp[i * GS + q];
-                            Jp[i * GS + p] = c * jp - s * jq;
-                            Jp[i * GS + q] = s * jp + c * jq;
-                        }
-                        __syncthreads();
-                        // rows p, q of Gs
-                        for (int e = tid; e < 16 * 32; e += 256) {
-                            const int k = e / 32, i = e % 32;
-                            const double c = cs_[k], s = sn_[k];
-                            if (s == 0.0) continue;
-                            int p, q;
-                            rr_pair(ir, k, 32, p, q);
-                            const double gp = Gs[p * GS + i], gq = Gs[q * GS + i];
-                            Gs[p * GS + i] = c * gp - s * gq;
-                            Gs[q * GS + i] = s * gp + c * gq;
-                        }
-                        __syncthreads();
+                        double* t = cur;
+                        cur = nxt;
+                        nxt = t;
                     }
-                    if (flags[2] == 0) break;
+                    if (any) flags[2 + (isw & 1)] = 1;
+                    __syncthreads();
+                    const bool more = flags[2 + (isw & 1)] != 0;
+                    if (tid == 0) flags[2 + ((isw + 1) & 1)] = 0;
+                    __syncthreads();
+                    if (!more) break;
                 }
-                // 4. X_pair Jp, J_pair Jp -> destination buffer (wave w: row tiles w, w+4, ...)
-                for (int mtx = 0; mtx < 2; ++mtx) {
-                    const double* S = mtx ? Js : Xs;
-                    double* D = mtx ? Jd : Xd;
-                    for (int it = w; it < LP / 16; it += 4) {
-                        const int i0 = 16 * it;
-                        f64x4 acc[2] = {MD::zero(), MD::zero()};
-#pragma unroll
-                        for (int kk = 0; kk < 8; ++kk) {
-                            const double a = S[(int64_t)col(4 * kk + h) * LP + i0 + r];
-                            acc[0] = MD::mma(a, Jp[(4 * kk + h) * GS + r], acc[0]);
-                            acc[1] = MD::mma(a, Jp[(4 * kk + h) * GS + 16 + r], acc[1]);
-                        }
-#pragma unroll
-                        for (int ct = 0; ct < 2; ++ct)
-#pragma unroll
-                            for (int j = 0; j < 4; ++j) D[(int64_t)col(16 * ct + r) * LP + i0 + MD::row(h, j)] = acc[ct][j];
-                    }
-                }
+                // 5. X_pair Jp and J_pair Jp -> destination buffer
+                apply_pair(Xs, Jp, Xd, LP, col, w, r, h);
+                __syncthreads();
+                stage_pair(Xs, Jsrc, LP, col);
+                __syncthreads();
+                apply_pair(Xs, Jp, Jd, LP, col, w, r, h);
             } else {
-                for (int e = tid; e < 32 * LP; e += 256) {
-                    const int64_t o = (int64_t)col(e / LP) * LP + e % LP;
-                    Xd[o] = Xs[o];
-                    Jd[o] = Js[o];
+                for (int e = tid; e < 32 * (LP / 2); e += 256) {
+                    const int kk = e / (LP / 2), i = 2 * (e % (LP / 2));
+                    const int64_t o = (int64_t)col(kk) * LP + i;
+                    *reinterpret_cast<double2*>(Xd + o) = *reinterpret_cast<const double2*>(Xsrc + o);
+                    *reinterpret_cast<double2*>(Jd + o) = *reinterpret_cast<const double2*>(Jsrc + o);
                 }
             }
             par = 1 - par;
@@ -377,7 +446,8 @@ hipError_t launch_block_jacobi(const double* R, int l, int LP, double* X, double
     if (LP % 32 || LP < 64 || LP > 512) return hipErrorInvalidValue;
     hipError_t e = hipMemsetAsync(sync, 0, kSyncWords * sizeof(unsigned), s);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(block_jacobi_kernel, dim3(LP / 32), dim3(256), 0, s, R, l, LP, X, J, sync, info);
+    hipLaunchKernelGGL(block_jacobi_kernel, dim3(LP / 32), dim3(256), block_jacobi_lds(LP), s, R, l, LP, X, J, sync,
+                       info);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     const size_t lds = (size_t)LP * 8 * 2 + (size_t)LP * 4 + 64;

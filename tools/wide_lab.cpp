@@ -1,0 +1,331 @@
+// wide_lab.cpp -- hipEvent timings of the wide-engine kernels on synthetic inputs (tuning aid).
+// Build: make -C rsvd_kamaneh_raganato_terrana_amd/csrc widelab ; run on the GPU box:
+//   tools/wide_lab [what]   what in {all, pg, gram, chol, jac, proj}
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "../rsvd_kamaneh_raganato_terrana_amd/csrc/kernels.hpp"
+#include "../rsvd_kamaneh_raganato_terrana_amd/csrc/wide.hpp"
+
+using namespace rsvd;
+
+#define CK(x)                                                                                    \
+    do {                                                                                         \
+        hipError_t e = (x);                                                                      \
+        if (e != hipSuccess) {                                                                   \
+            fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e));     \
+            exit(1);                                                                             \
+        }                                                                                        \
+    } while (0)
+
+static hipStream_t S;
+
+static double time_us(const std::function<void()>& f, int reps = 5) {
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    f();
+    CK(hipStreamSynchronize(S));
+    std::vector<float> t;
+    for (int i = 0; i < reps; ++i) {
+        CK(hipEventRecord(a, S));
+        f();
+        CK(hipEventRecord(b, S));
+        CK(hipEventSynchronize(b));
+        float ms;
+        CK(hipEventElapsedTime(&ms, a, b));
+        t.push_back(ms * 1e3f);
+    }
+    std::sort(t.begin(), t.end());
+    CK(hipEventDestroy(a));
+    CK(hipEventDestroy(b));
+    return t[t.size() / 2];
+}
+
+template <typename T>
+static T* dev_random(size_t n, float scale = 1.0f, unsigned seed = 1) {
+    std::vector<T> h(n);
+    std::mt19937 g(seed);
+    std::normal_distribution<float> d(0.f, scale);
+    for (auto& x : h) x = (T)d(g);
+    T* p;
+    CK(hipMalloc(&p, n * sizeof(T)));
+    CK(hipMemcpy(p, h.data(), n * sizeof(T), hipMemcpyHostToDevice));
+    return p;
+}
+
+static void bench_pg() {
+    for (int LP : {128, 256, 512}) {
+        const int64_t rows = LP == 128 ? (1 << 20) : (LP == 256 ? 65536 : 131072);
+        float* In = dev_random<float>((size_t)rows * LP);
+        float* Out;
+        bf16_t *hi, *lo;
+        CK(hipMalloc(&Out, (size_t)rows * LP * 4));
+        CK(hipMalloc(&hi, (size_t)rows * LP * 2));
+        CK(hipMalloc(&lo, (size_t)rows * LP * 2));
+        float* M = dev_random<float>((size_t)LP * LP, 0.1f);
+        const double gb = (double)rows * LP * 4 * 2 / 1e9;
+        double t0 = time_us([&] { CK(launch_panel_gemm<float>(In, rows, LP, M, 1, Out, 0, 0, nullptr, nullptr, nullptr, S)); });
+        double t1 = time_us([&] { CK(launch_panel_gemm<float>(In, rows, LP, M, 1, Out, 0, 0, hi, lo, nullptr, S)); });
+        double t2 = time_us([&] { CK(launch_panel_gemm<float>(In, rows, LP, M, 0, Out, rows, LP, nullptr, nullptr, nullptr, S)); });
+        double t3 = time_us([&] { CK(launch_split_bf16<float>(In, rows, LP, hi, lo, S)); });
+        printf("panel_gemm rows=%ld LP=%d: upper %.1f us (%.0f GB/s)  +hi/lo %.1f us  general->colmajor %.1f us  split_bf16 %.1f us\n",
+               (long)rows, LP, t0, gb / t0 * 1e6 / 1e3, t1, t2, t3);
+        CK(hipFree(In)); CK(hipFree(Out)); CK(hipFree(hi)); CK(hipFree(lo)); CK(hipFree(M));
+    }
+}
+
+static void bench_gram() {
+    for (int LP : {128, 256, 512}) {
+        const int64_t rows = LP == 128 ? (1 << 20) : (LP == 256 ? 65536 : 131072);
+        float* P = dev_random<float>((size_t)rows * LP);
+        GramPlan gp = plan_gram_wide(rows, LP, 0);
+        double* slabs;
+        double* G;
+        CK(hipMalloc(&slabs, (size_t)gp.blocks * gp.chunks * 1024 * 8));
+        CK(hipMalloc(&G, (size_t)LP * LP * 8));
+        double t = time_us([&] { CK(launch_gram_wide<float>(P, nullptr, rows, LP, gp, slabs, G, nullptr, S)); });
+        const double fl = 2.0 * rows * LP * LP * gp.blocks / ((LP / 32.0) * (LP / 32.0));
+        printf("gram rows=%ld LP=%d blocks=%d chunks=%d: %.1f us  (%.1f TF/s fp64, %.0f GB/s)\n", (long)rows, LP, gp.blocks,
+               gp.chunks, t, fl / t / 1e6, rows * LP * 4.0 / t / 1e3);
+        CK(hipFree(P)); CK(hipFree(slabs)); CK(hipFree(G));
+    }
+}
+
+static double* spd(int LP, int l) {  // G = X^T X + I with X random l x l
+    std::vector<double> X((size_t)l * l), G((size_t)LP * LP, 0.0);
+    std::mt19937 g(3);
+    std::normal_distribution<double> d;
+    for (auto& x : X) x = d(g);
+    for (int i = 0; i < l; ++i)
+        for (int j = 0; j < l; ++j) {
+            double s = (i == j) ? 1.0 : 0.0;
+            for (int k = 0; k < l; ++k) s += X[(size_t)k * l + i] * X[(size_t)k * l + j];
+            G[(size_t)i * LP + j] = s;
+        }
+    double* p;
+    CK(hipMalloc(&p, G.size() * 8));
+    CK(hipMemcpy(p, G.data(), G.size() * 8, hipMemcpyHostToDevice));
+    return p;
+}
+
+static void bench_chol() {
+    for (int LP : {64, 128, 256, 512}) {
+        double* G = spd(LP, LP);
+        double *R, *Ri, *W;
+        float* R32;
+        int *cf, *fl;
+        CK(hipMalloc(&R, (size_t)LP * LP * 8));
+        CK(hipMalloc(&Ri, (size_t)LP * LP * 8));
+        CK(hipMalloc(&W, (size_t)LP * LP * 8));
+        CK(hipMalloc(&R32, (size_t)LP * LP * 4));
+        CK(hipMalloc(&cf, LP * 4));
+        CK(hipMalloc(&fl, 4));
+        CK(hipMemset(fl, 0, 4));
+        double t = time_us([&] { CK(launch_chol_wide(G, LP, LP, 1e-13, R, Ri, R32, cf, fl, W, nullptr, S)); });
+        // check R^T R = G and R Ri = I on the host
+        std::vector<double> hR((size_t)LP * LP), hRi((size_t)LP * LP), hG((size_t)LP * LP);
+        CK(hipMemcpy(hR.data(), R, hR.size() * 8, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(hRi.data(), Ri, hRi.size() * 8, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(hG.data(), G, hG.size() * 8, hipMemcpyDeviceToHost));
+        double e1 = 0, e2 = 0, ng = 0;
+        for (int i = 0; i < LP; ++i)
+            for (int j = 0; j < LP; ++j) {
+                double s = 0, s2 = 0;
+                for (int k = 0; k < LP; ++k) {
+                    s += hR[(size_t)k * LP + i] * hR[(size_t)k * LP + j];
+                    s2 += hR[(size_t)i * LP + k] * hRi[(size_t)k * LP + j];
+                }
+                e1 += (s - hG[(size_t)i * LP + j]) * (s - hG[(size_t)i * LP + j]);
+                ng += hG[(size_t)i * LP + j] * hG[(size_t)i * LP + j];
+                e2 += (s2 - (i == j)) * (s2 - (i == j));
+            }
+        printf("chol LP=%d: %.1f us   |R^T R - G|/|G| = %.2e  |R Rinv - I| = %.2e\n", LP, t, sqrt(e1 / ng), sqrt(e2));
+        CK(hipFree(G)); CK(hipFree(R)); CK(hipFree(Ri)); CK(hipFree(W)); CK(hipFree(R32)); CK(hipFree(cf)); CK(hipFree(fl));
+    }
+}
+
+static void bench_jac() {
+    for (int LP : {128, 256, 512}) {
+        // R: upper triangular with a 0.97^i graded diagonal + noise (like a QR-preconditioned B^T)
+        std::vector<double> hR((size_t)LP * LP, 0.0);
+        std::mt19937 g(5);
+        std::normal_distribution<double> d;
+        for (int i = 0; i < LP; ++i)
+            for (int j = i; j < LP; ++j) hR[(size_t)i * LP + j] = (i == j ? 1.0 : 0.05 * d(g)) * pow(0.97, i);
+        double* R;
+        CK(hipMalloc(&R, hR.size() * 8));
+        CK(hipMemcpy(R, hR.data(), hR.size() * 8, hipMemcpyHostToDevice));
+        double *X, *J, *Uw, *Vw, *Sd;
+        unsigned* sync;
+        int* info;
+        CK(hipMalloc(&X, (size_t)2 * LP * LP * 8));
+        CK(hipMalloc(&J, (size_t)2 * LP * LP * 8));
+        CK(hipMalloc(&Uw, (size_t)LP * LP * 8));
+        CK(hipMalloc(&Vw, (size_t)LP * LP * 8));
+        CK(hipMalloc(&Sd, LP * 8));
+        CK(hipMalloc(&sync, 128 * 4));
+        CK(hipMalloc(&info, 16 * 4));
+        CK(hipMemset(info, 0, 64));
+        double t = time_us([&] { CK(launch_block_jacobi<double>(R, LP, LP, X, J, Uw, Vw, Sd, sync, info, S)); }, 3);
+        int hinfo[4];
+        CK(hipMemcpy(hinfo, info, 16, hipMemcpyDeviceToHost));
+        std::vector<double> hS(LP);
+        CK(hipMemcpy(hS.data(), Sd, LP * 8, hipMemcpyDeviceToHost));
+        printf("block_jacobi LP=%d: %.1f us  sweeps=%d timeout=%d  S[0]=%.6f S[last]=%.3e\n", LP, t, hinfo[0], hinfo[2],
+               hS[0], hS[LP - 1]);
+        CK(hipFree(R)); CK(hipFree(X)); CK(hipFree(J)); CK(hipFree(Uw)); CK(hipFree(Vw)); CK(hipFree(Sd));
+        CK(hipFree(sync)); CK(hipFree(info));
+    }
+}
+
+static void bench_proj() {
+    struct Case { int64_t m, n; int LP; int fp8; };
+    for (Case c : {Case{1 << 20, 1024, 128, 0}, Case{65536, 65536, 256, 0}, Case{131072, 8192, 512, 1}}) {
+        const size_t esz = c.fp8 ? 1 : 2;
+        void* A;
+        CK(hipMalloc(&A, (size_t)c.m * c.n * esz));
+        CK(hipMemset(A, 0x3c, (size_t)c.m * c.n * esz));  // 0x3c3c: bf16 ~0.0115 / e4m3 1.5
+        const int64_t mx = std::max(c.m, c.n);
+        bf16_t* Sh = dev_random<bf16_t>((size_t)mx * c.LP);
+        bf16_t* Sl = dev_random<bf16_t>((size_t)mx * c.LP);
+        float* Out;
+        CK(hipMalloc(&Out, (size_t)mx * c.LP * 4));
+        for (int v2 = 0; v2 < (c.fp8 ? 1 : 2); ++v2) {
+            WProjPlan pnn = plan_wproj(c.m, c.n, c.LP, v2), ptn = plan_wproj(c.n, c.m, c.LP, v2);
+            float* slabs;
+            CK(hipMalloc(&slabs, (size_t)std::max<int64_t>(pnn.splits * c.m, ptn.splits * c.n) * c.LP * 4));
+            const double bytes = (double)c.m * c.n * esz, fl = 2.0 * c.m * c.n * c.LP;
+            double t1 = time_us([&] { CK(launch_wproj(1, c.fp8, A, c.m, c.m, c.n, Sh, nullptr, c.LP, pnn, slabs, Out, S)); });
+            double t2 = time_us([&] { CK(launch_wproj(1, c.fp8, A, c.m, c.m, c.n, Sh, Sl, c.LP, pnn, slabs, Out, S)); });
+            double t3 = time_us([&] { CK(launch_wproj(0, c.fp8, A, c.m, c.m, c.n, Sh, Sl, c.LP, ptn, slabs, Out, S)); });
+            printf("proj%s m=%ld n=%ld LP=%d fp8=%d: NN1 %.1f us (%.0f GB/s) NN2 %.1f us (%.0f GB/s, %.0f TF) TN2 %.1f us"
+                   " (%.0f GB/s, %.0f TF) splits nn=%d tn=%d\n",
+                   v2 ? "v2" : "v1", (long)c.m, (long)c.n, c.LP, c.fp8, t1, bytes / t1 / 1e3, t2, bytes / t2 / 1e3,
+                   2 * fl / t2 / 1e6, t3, bytes / t3 / 1e3, 2 * fl / t3 / 1e6, pnn.splits, ptn.splits);
+            CK(hipFree(slabs));
+        }
+        CK(hipFree(A)); CK(hipFree(Sh)); CK(hipFree(Sl)); CK(hipFree(Out));
+    }
+}
+
+typedef __attribute__((address_space(3))) void* lds_vp;
+__global__ void glds_probe(const uint32_t* src, uint32_t* out, int mode) {
+    extern __shared__ __attribute__((aligned(1024))) char smem[];
+    uint32_t* sm = reinterpret_cast<uint32_t*>(smem);
+    for (int i = threadIdx.x; i < 512; i += blockDim.x) sm[i] = 0xdeadbeef;
+    __syncthreads();
+    const int lane = threadIdx.x & 63;
+    if (threadIdx.x < 64) {
+        const uint32_t* g = src + 4 * (63 - lane);
+        if (mode == 0) __builtin_amdgcn_global_load_lds(g, (lds_vp)(smem + 256), 16, 0, 0);
+        else {
+            const uint32_t la = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(lds_vp)(smem + 256));
+            asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" :: "v"(g), "s"(la) : "memory");
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < 512; i += blockDim.x) out[i] = sm[i];
+}
+
+static void probe_glds() {
+    std::vector<uint32_t> h(1024);
+    for (int i = 0; i < 1024; ++i) h[i] = i;
+    uint32_t *src, *out;
+    CK(hipMalloc(&src, 4096));
+    CK(hipMalloc(&out, 2048));
+    CK(hipMemcpy(src, h.data(), 4096, hipMemcpyHostToDevice));
+    for (int mode = 0; mode < 2; ++mode) {
+        hipLaunchKernelGGL(glds_probe, dim3(1), dim3(256), 4096, S, src, out, mode);
+        CK(hipStreamSynchronize(S));
+        std::vector<uint32_t> o(512);
+        CK(hipMemcpy(o.data(), out, 2048, hipMemcpyDeviceToHost));
+        printf("glds mode %d: dwords 60..72:", mode);
+        for (int i = 60; i < 72; ++i) printf(" %x", o[i]);
+        printf("\n   first non-dead at");
+        for (int i = 0; i < 512; ++i) if (o[i] != 0xdeadbeef) { printf(" %d (val %u)", i, o[i]); break; }
+        int last = -1;
+        for (int i = 0; i < 512; ++i) if (o[i] != 0xdeadbeef) last = i;
+        printf(" last %d (val %u)\n", last, last >= 0 ? o[last] : 0);
+    }
+}
+
+static uint16_t f2bf_h(float x) {
+    uint32_t u;
+    memcpy(&u, &x, 4);
+    return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+
+static void check_proj() {  // v2 (LDS-DMA) against v1 on random bf16 data
+    for (int LP : {128, 256, 512}) {
+        const int64_t m = 2048 + 64, n = 1024 + 32;
+        std::vector<uint16_t> hA((size_t)m * n), hS((size_t)std::max(m, n) * LP), hL(hS.size());
+        std::mt19937 g(7);
+        std::normal_distribution<float> d;
+        for (auto& x : hA) x = f2bf_h(d(g));
+        for (size_t i = 0; i < hS.size(); ++i) {
+            hS[i] = f2bf_h(d(g));
+            hL[i] = f2bf_h(d(g) * 1e-3f);
+        }
+        bf16_t *A, *Sh, *Sl;
+        const size_t srows = (size_t)((std::max(m, n) + 31) / 32 * 32);
+        CK(hipMalloc(&A, hA.size() * 2));
+        CK(hipMalloc(&Sh, srows * LP * 2));
+        CK(hipMalloc(&Sl, srows * LP * 2));
+        CK(hipMemset(Sh, 0, srows * LP * 2));
+        CK(hipMemset(Sl, 0, srows * LP * 2));
+        CK(hipMemcpy(A, hA.data(), hA.size() * 2, hipMemcpyHostToDevice));
+        float *O1, *O2, *sl;
+        const int64_t mx = std::max(m, n);
+        CK(hipMalloc(&O1, mx * LP * 4));
+        CK(hipMalloc(&O2, mx * LP * 4));
+        CK(hipMalloc(&sl, (size_t)256 * mx * LP * 4));
+        for (int nn = 0; nn < 2; ++nn) {
+            const int64_t rows_s = nn ? n : m;  // S panel rows = K
+            CK(hipMemset(Sh, 0, srows * LP * 2));
+            CK(hipMemset(Sl, 0, srows * LP * 2));
+            CK(hipMemcpy(Sh, hS.data(), rows_s * LP * 2, hipMemcpyHostToDevice));
+            CK(hipMemcpy(Sl, hL.data(), rows_s * LP * 2, hipMemcpyHostToDevice));
+            const int64_t ro = nn ? m : n, K = nn ? n : m;
+            WProjPlan p1 = plan_wproj(ro, K, LP, false), p2 = plan_wproj(ro, K, LP, true);
+            CK(launch_wproj(nn, 0, A, m, m, n, Sh, Sl, LP, p1, sl, O1, S));
+            CK(launch_wproj(nn, 0, A, m, m, n, Sh, Sl, LP, p2, sl, O2, S));
+            CK(hipStreamSynchronize(S));
+            std::vector<float> a(ro * LP), b(ro * LP);
+            CK(hipMemcpy(a.data(), O1, a.size() * 4, hipMemcpyDeviceToHost));
+            CK(hipMemcpy(b.data(), O2, b.size() * 4, hipMemcpyDeviceToHost));
+            double md = 0, mx2 = 0;
+            for (size_t i = 0; i < a.size(); ++i) {
+                md = std::max(md, (double)fabs(a[i] - b[i]));
+                mx2 = std::max(mx2, (double)fabs(a[i]));
+            }
+            printf("check LP=%d %s: max|v1-v2| = %.3e (max|v1| = %.3e) v2 splits=%d chunk=%ld\n", LP, nn ? "NN" : "TN", md,
+                   mx2, p2.splits, (long)p2.chunk);
+        }
+        CK(hipFree(A)); CK(hipFree(Sh)); CK(hipFree(Sl)); CK(hipFree(O1)); CK(hipFree(O2)); CK(hipFree(sl));
+    }
+}
+
+int main(int argc, char** argv) {
+    const std::string what = argc > 1 ? argv[1] : "all";
+    CK(hipStreamCreate(&S));
+    if (what == "all" || what == "pg") bench_pg();
+    if (what == "all" || what == "gram") bench_gram();
+    if (what == "all" || what == "chol") bench_chol();
+    if (what == "all" || what == "jac") bench_jac();
+    if (what == "all" || what == "proj") bench_proj();
+    if (what == "all" || what == "check") check_proj();
+    if (what == "probe") probe_glds();
+    CK(hipStreamDestroy(S));
+    return 0;
+}
