@@ -1,0 +1,104 @@
+"""GPU, world_size 2: the row-sharded engine path end to end on one MI355X.
+
+Two processes share cuda:0 and exchange through the engine's all-reduce hook over gloo (RCCL
+refuses two ranks on one device; the hook and the engine code are the same that bench.py drives
+over RCCL on N GPUs).  Rank g owns rows rsvd_row_partition(m, 2, g) of A (src/rSVD.cpp:20-23);
+the gathered U rows, S and V must match the single-process oracle on the same A and Omega.
+Tolerances: fp64 1e-9 (S) / 1e-8 (leading half of U, V) -- the sharded CholeskyQR factors the
+all-reduced Gram (a different summation order than the single-GPU in-kernel reduction); fp32 /
+bf16 1e-4 (north_star).
+"""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+WORLD = 2
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, port, case, q):
+    try:
+        sys.path.insert(0, REPO)
+        sys.path.insert(0, os.path.join(REPO, "tests"))
+        import torch
+        import torch.distributed as dist
+
+        import rsvd_kamaneh_raganato_terrana_amd as R
+        from conftest import gapped_matrix
+
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+        torch.cuda.set_device(0)
+        m, n, l, qq, dt = case
+        A = gapped_matrix(m, n, 2 * l, decay=0.93, seed=5).astype(np.float64)
+        rows, off = R.row_partition(m, WORLD, rank)
+        tdt = {"f64": torch.float64, "f32": torch.float32, "bf16": torch.bfloat16}[dt]
+        Ag = torch.from_numpy(np.ascontiguousarray(A[off:off + rows].T)).cuda().to(tdt).t()
+        eng = R.Engine(0)
+        eng.set_comm(rank, WORLD)
+        U, S, V = eng.rsvd(Ag, l, q=qq, seed=4242)
+        torch.cuda.synchronize()
+        q.put((rank, off, U.cpu().double().numpy(), S.cpu().double().numpy(), V.cpu().double().numpy(),
+               Ag.float().cpu().double().numpy()))
+        eng.close()
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover - reported through the queue
+        import traceback
+
+        q.put((rank, None, traceback.format_exc(), None, None, None))
+
+
+@pytest.mark.parametrize("case", [(600, 300, 32, 2, "f64"), (1024, 512, 64, 2, "f32"), (2048, 1024, 128, 1, "bf16")])
+def test_row_sharded_world2_matches_oracle(case):
+    import torch.multiprocessing as mp
+
+    import oracle
+    from conftest import rel_fro, sign_align
+
+    m, n, l, qq, dt = case
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, port, case, q)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(WORLD)]
+    for p in procs:
+        p.join(timeout=60)
+    for r in res:
+        assert r[1] is not None, r[2]
+    res.sort(key=lambda t: t[1])
+    U = np.vstack([r[2] for r in res])
+    A = np.vstack([r[5] for r in res])  # the values the GPU saw (bf16 / fp32 rounded)
+    S0, V0 = res[0][3], res[0][4]
+    # every rank holds the same S and V
+    assert np.array_equal(S0, res[1][3]) and np.array_equal(V0, res[1][4])
+    # the same Omega the engine drew (Philox; rounded to bf16 for bf16 A)
+    import torch
+
+    import rsvd_kamaneh_raganato_terrana_amd as R
+
+    eng = R.Engine(0)
+    gdt = {"f64": torch.float64, "f32": torch.float32, "bf16": torch.bfloat16}[dt]
+    Om = eng.generate_omega(n, l, seed=4242, dtype=gdt).cpu().double().numpy()
+    eng.close()
+    Uo, So, Vo = oracle.rsvd(A, l, q=qq, Omega=Om)
+    tol_s, tol_uv = (1e-9, 1e-8) if dt == "f64" else (1e-4, 1e-4)
+    k = l // 2
+    assert rel_fro(S0, So) < tol_s
+    assert rel_fro(sign_align(U[:, :k], Uo[:, :k]), Uo[:, :k]) < tol_uv
+    assert rel_fro(sign_align(V0[:, :k], Vo[:, :k]), Vo[:, :k]) < tol_uv
+    # orthonormality of the gathered U: Frobenius over l^2 entries (fp32 outputs: ~1e-6 per entry)
+    assert np.linalg.norm(U.T @ U - np.eye(l)) < (1e-10 if dt == "f64" else 1e-3)
