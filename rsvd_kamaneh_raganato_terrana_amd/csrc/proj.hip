@@ -26,6 +26,7 @@ namespace rsvd {
 namespace {
 
 constexpr int kWaves = 4;
+constexpr int kPrefetch = 8;  // k-steps of A kept in flight per wave (NN; TN keeps half as many, wider)
 
 template <typename T>
 __device__ __forceinline__ typename Vec16<T>::type load_vec_guarded(const T* __restrict__ col, int64_t i,
@@ -72,11 +73,16 @@ __global__ __launch_bounds__(kWave* kWaves) void proj_nn_kernel(
 #pragma unroll
         for (int g = 0; g < G; ++g) acc[t][g] = M::zero();
 
-    for (int64_t k0 = kbeg + 4 * w; k0 < kend; k0 += 4 * kWaves) {
-        const int64_t k = k0 + h;
-        V a;
-        T b[G];
-        if (k < kend) {
+    // This wave's k-steps (4 k each, interleaved with the other waves), register-prefetched PD
+    // steps ahead so that enough A bytes are in flight per CU to cover HBM latency.
+    constexpr int PD = kPrefetch;
+    const int64_t kstep = 4 * kWaves, kfirst = kbeg + 4 * w;
+    const int nst = (kfirst < kend) ? (int)((kend - kfirst + kstep - 1) / kstep) : 0;
+    V pa[PD];
+    T pb[PD][G];
+    auto load = [&](int st, V& a, T* b) {
+        const int64_t k = kfirst + (int64_t)st * kstep + h;
+        if (st < nst && k < kend) {
             a = load_vec_guarded<T>(A + k * lda, row, m, vec_ok);
             const T* xr = X + k * ldp + r;
 #pragma unroll
@@ -88,11 +94,24 @@ __global__ __launch_bounds__(kWave* kWaves) void proj_nn_kernel(
 #pragma unroll
             for (int g = 0; g < G; ++g) b[g] = T(0);
         }
+    };
 #pragma unroll
-        for (int t = 0; t < VW; ++t) {
-            const T at = Vec16<T>::get(a, t);
+    for (int u = 0; u < PD; ++u) load(u, pa[u], pb[u]);
+    for (int base = 0; base < nst; base += PD) {
 #pragma unroll
-            for (int g = 0; g < G; ++g) acc[t][g] = M::mma(at, b[g], acc[t][g]);
+        for (int u = 0; u < PD; ++u) {
+            if (base + u >= nst) break;
+            const V a = pa[u];
+            T b[G];
+#pragma unroll
+            for (int g = 0; g < G; ++g) b[g] = pb[u][g];
+            load(base + u + PD, pa[u], pb[u]);
+#pragma unroll
+            for (int t = 0; t < VW; ++t) {
+                const T at = Vec16<T>::get(a, t);
+#pragma unroll
+                for (int g = 0; g < G; ++g) acc[t][g] = M::mma(at, b[g], acc[t][g]);
+            }
         }
     }
 
@@ -153,13 +172,18 @@ __global__ __launch_bounds__(kWave* kWaves) void proj_tn_kernel(
         for (int g = 0; g < G; ++g) acc[jt][g] = M::zero();
 
     constexpr int ISTEP = 4 * VW;  // rows of A consumed per MFMA group
-    for (int64_t i0 = ibeg + ISTEP * w; i0 < iend; i0 += ISTEP * kWaves) {
-        const int64_t ib = i0 + VW * h;
-        V a[JT];
+    constexpr int PD = kPrefetch / 2;
+    const int64_t istep = (int64_t)ISTEP * kWaves, ifirst = ibeg + ISTEP * w;
+    const int nst = (ifirst < iend) ? (int)((iend - ifirst + istep - 1) / istep) : 0;
+    V pa[PD][JT];
+    T pb[PD][VW][G];
+    auto load = [&](int st, V* a, T (*b)[G]) {
+        const int64_t ib = ifirst + (int64_t)st * istep + VW * h;
+        const bool ok = st < nst;
 #pragma unroll
         for (int jt = 0; jt < JT; ++jt) {
             const int64_t j = j0 + 16 * jt + r;
-            if (j < n) {
+            if (ok && j < n) {
                 a[jt] = load_vec_guarded<T>(A + j * lda, ib, iend, vec_ok);
             } else {
                 T* e = reinterpret_cast<T*>(&a[jt]);
@@ -170,21 +194,34 @@ __global__ __launch_bounds__(kWave* kWaves) void proj_tn_kernel(
 #pragma unroll
         for (int t = 0; t < VW; ++t) {
             const int64_t i = ib + t;
-            T b[G];
-            if (i < iend) {
-                const T* qr = Q + i * ldp + r;
+            const T* qr = Q + i * ldp + r;
 #pragma unroll
-                for (int g = 0; g < G; ++g) b[g] = qr[16 * g];
-            } else {
+            for (int g = 0; g < G; ++g) b[t][g] = (ok && i < iend) ? qr[16 * g] : T(0);
+        }
+    };
 #pragma unroll
-                for (int g = 0; g < G; ++g) b[g] = T(0);
-            }
+    for (int u = 0; u < PD; ++u) load(u, pa[u], pb[u]);
+    for (int base = 0; base < nst; base += PD) {
 #pragma unroll
-            for (int jt = 0; jt < JT; ++jt) {
-                const T at = Vec16<T>::get(a[jt], t);
+        for (int u = 0; u < PD; ++u) {
+            if (base + u >= nst) break;
+            V a[JT];
+            T b[VW][G];
 #pragma unroll
-                for (int g = 0; g < G; ++g) acc[jt][g] = M::mma(at, b[g], acc[jt][g]);
-            }
+            for (int jt = 0; jt < JT; ++jt) a[jt] = pa[u][jt];
+#pragma unroll
+            for (int t = 0; t < VW; ++t)
+#pragma unroll
+                for (int g = 0; g < G; ++g) b[t][g] = pb[u][t][g];
+            load(base + u + PD, pa[u], pb[u]);
+#pragma unroll
+            for (int t = 0; t < VW; ++t)
+#pragma unroll
+                for (int jt = 0; jt < JT; ++jt) {
+                    const T at = Vec16<T>::get(a[jt], t);
+#pragma unroll
+                    for (int g = 0; g < G; ++g) acc[jt][g] = M::mma(at, b[t][g], acc[jt][g]);
+                }
         }
     }
 
