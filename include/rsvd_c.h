@@ -12,7 +12,7 @@
  *                                                                  include/rSVD.hpp:13, src/rSVD.cpp:57-70
  *   rsvd_generate_omega            <- Mat_m generateOmega(int n, int l)
  *                                                                  include/rSVD.hpp:15, src/rSVD.cpp:12-55
- *   rsvd_qr_reduced / rsvd_qr_full <- void qr_decomposition_reduced/full(const Mat_m& A, Mat_m& Q,
+ *   rsvd_qr (full = 0 / 1)         <- void qr_decomposition_reduced/full(const Mat_m& A, Mat_m& Q,
  *                                          Mat_m& R)              include/QR.hpp:15-16, src/QR.cpp:22-80
  *   rsvd_svd                       <- template<SVDMethod> SVD::compute()/getU/getS/getV
  *                                                                  include/SVD_class.hpp:35-71,79-180
@@ -139,6 +139,30 @@ int rsvd_range_finder(rsvd_handle_t h, const rsvd_desc_t *desc, const void *A, c
  * saturates at +-448), written as fp32 -- the Omega the low-precision rsvd_run draws. */
 int rsvd_generate_omega(rsvd_handle_t h, int64_t n, int32_t l, uint64_t seed, int32_t dtype, void *omega);
 
+/* QR() boundary <- qr_decomposition_reduced / qr_decomposition_full (include/QR.hpp:15-16,
+ * src/QR.cpp:22-80).  full = 0: Q m x n (ldq), R n x n (ldr), requires m >= n (src/QR.cpp:78);
+ * full = 1: Q m x m, R m x n (upper trapezoidal).  dtype F64 / F32.  Q has orthonormal columns
+ * and A = Q R; R(j,j) >= 0 except on the leading columns of A whose sub-diagonal is already zero,
+ * where R(j,j) = A(j,j) as the Givens sweep leaves them.  For full-rank A this is the unique QR,
+ * i.e. the reference's; the complement Q[:, n:] of a full QR is an orthonormal completion
+ * (identity columns for an A with trailing zero rows).  Built for n <= 512 (reduced) and
+ * m, n <= 512 (full); larger sizes return RSVD_ERR_UNSUPPORTED. */
+int rsvd_qr(rsvd_handle_t h, int64_t m, int64_t n, const void *A, int64_t lda, int32_t dtype, int32_t full, void *Q,
+            int64_t ldq, void *R, int64_t ldr);
+
+/* SVD<method>::compute() boundary (include/SVD_class.hpp:35-97).  Jacobi / ParallelJacobi
+ * (:100-180, :223-333): U m x k (ldu), S k (descending, >= 0), V n x k (ldv), k = min(m, n)
+ * <= 512; dtype F64 / F32.  Power (:183-219 with PM, src/PM.cpp): dtype F64, n <= 512,
+ * dim = r ? r : min(m, n) deflation steps, start vectors Philox(seed + i); stops at the first
+ * sigma < 1e-12 (:198-208); *kept = triplets written (U, S, V columns 0..kept-1; V's columns are
+ * the right singular vectors -- the reference's row layout is rebuilt by include/SVD_class.hpp).
+ * Jacobi sets *kept = k without synchronising; Power synchronises the stream. */
+int rsvd_svd(rsvd_handle_t h, int64_t m, int64_t n, const void *A, int64_t lda, int32_t dtype, int32_t method,
+             int32_t r, uint64_t seed, void *U, int64_t ldu, void *S, void *V, int64_t ldv, int32_t *kept);
+/* Device workspace bytes of rsvd_qr / rsvd_svd (for rsvd_set_workspace callers). */
+int rsvd_qr_workspace_bytes(int64_t m, int64_t n, int32_t dtype, int32_t full, size_t *bytes);
+int rsvd_svd_workspace_bytes(int64_t m, int64_t n, int32_t dtype, int32_t method, size_t *bytes);
+
 /* ---- host-pointer fp64 entry points used by the C++ drop-in headers (synchronous) --------- */
 int rsvd_run_host_f64(rsvd_handle_t h, int64_t m, int64_t n, const double *A, int64_t lda, int32_t l,
                       int32_t q, int32_t method, const double *omega /* nullable, n x l, ld n */,
@@ -147,6 +171,12 @@ int rsvd_range_finder_host_f64(rsvd_handle_t h, int64_t m, int64_t n, const doub
                                const double *omega /* n x l, ld n */, int32_t l, int32_t q,
                                double *Q /* m x l */);
 int rsvd_generate_omega_host_f64(rsvd_handle_t h, int64_t n, int32_t l, uint64_t seed, double *omega);
+/* Q: m x (full ? m : n), ld m; R: (full ? m : n) x n, ld = its rows. */
+int rsvd_qr_host_f64(rsvd_handle_t h, int64_t m, int64_t n, const double *A, int64_t lda, int32_t full, double *Q,
+                     double *R);
+/* U: m x min(m,n), S: min(m,n), V: n x min(m,n) buffers (ld m, n); *kept columns are written. */
+int rsvd_svd_host_f64(rsvd_handle_t h, int64_t m, int64_t n, const double *A, int64_t lda, int32_t method, int32_t r,
+                      uint64_t seed, double *U, double *S, double *V, int32_t *kept);
 
 #ifdef __cplusplus
 }

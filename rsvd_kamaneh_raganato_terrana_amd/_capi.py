@@ -36,7 +36,8 @@ EXPORTS = (
     "rsvd_last_error", "rsvd_get_info", "rsvd_set_comm", "rsvd_row_partition",
     "rsvd_workspace_bytes", "rsvd_set_workspace", "rsvd_set_timing", "rsvd_get_timing", "rsvd_run", "rsvd_range_finder",
     "rsvd_generate_omega", "rsvd_run_host_f64", "rsvd_range_finder_host_f64",
-    "rsvd_generate_omega_host_f64",
+    "rsvd_generate_omega_host_f64", "rsvd_qr", "rsvd_svd", "rsvd_qr_workspace_bytes",
+    "rsvd_svd_workspace_bytes", "rsvd_qr_host_f64", "rsvd_svd_host_f64",
 )
 
 
@@ -121,6 +122,14 @@ def lib():
     L.rsvd_run_host_f64.argtypes = [vp, i64, i64, dp, i64, i32, i32, i32, dp, u64, dp, dp, dp]
     L.rsvd_range_finder_host_f64.argtypes = [vp, i64, i64, dp, i64, dp, i32, i32, dp]
     L.rsvd_generate_omega_host_f64.argtypes = [vp, i64, i32, u64, dp]
+    ip = ctypes.POINTER(i32)
+    L.rsvd_qr.argtypes = [vp, i64, i64, vp, i64, i32, i32, vp, i64, vp, i64]
+    L.rsvd_svd.argtypes = [vp, i64, i64, vp, i64, i32, i32, i32, u64, vp, i64, vp, vp, i64, ip]
+    szp = ctypes.POINTER(ctypes.c_size_t)
+    L.rsvd_qr_workspace_bytes.argtypes = [i64, i64, i32, i32, szp]
+    L.rsvd_svd_workspace_bytes.argtypes = [i64, i64, i32, i32, szp]
+    L.rsvd_qr_host_f64.argtypes = [vp, i64, i64, dp, i64, i32, dp, dp]
+    L.rsvd_svd_host_f64.argtypes = [vp, i64, i64, dp, i64, i32, i32, u64, dp, dp, dp, ip]
     _LIB = L
     return L
 

@@ -274,6 +274,70 @@ class Engine:
         check(lib().rsvd_generate_omega_host_f64(self.h, n, l, seed, _dp(om)), self.h)
         return om
 
+    # -- QR() and SVD<method> drop-ins (dense_api.cpp) ------------------------------------------
+    def _reserve_dense(self, fn, m, n, dt, arg):
+        nbytes = ctypes.c_size_t(0)
+        check(fn(m, n, dt, int(arg), ctypes.byref(nbytes)))
+        self._reserve_bytes(nbytes.value)
+        self._bind_stream()
+
+    def qr(self, A, full: bool = False):
+        """Device QR of A (CUDA f64/f32): (Q, R), reduced (m x n, n x n) or full (m x m, m x n)."""
+        A, lda = colmajor(A)
+        dt = self.abi_dtype(A.dtype)
+        m, n = A.shape
+        kq = m if full else n
+        self._reserve_dense(lib().rsvd_qr_workspace_bytes, m, n, dt, full)
+        Q = empty_colmajor(m, kq, A.dtype, A.device)
+        R = empty_colmajor(kq, n, A.dtype, A.device)
+        check(lib().rsvd_qr(self.h, m, n, ctypes.c_void_p(A.data_ptr()), lda, dt, int(full),
+                            ctypes.c_void_p(Q.data_ptr()), Q.stride(1), ctypes.c_void_p(R.data_ptr()),
+                            max(1, R.stride(1))), self.h)
+        return Q, R
+
+    def svd(self, A, method: int = SVDMethod.Jacobi, r: int = 0, seed: int = 0):
+        """Device SVD<method> of A (CUDA): (U m x k, S k, V n x k), k = min(m, n) (Power: the
+        triplets kept; V's columns are the right singular vectors)."""
+        torch = _torch()
+        A, lda = colmajor(A)
+        dt = self.abi_dtype(A.dtype)
+        m, n = A.shape
+        k = min(m, n)
+        self._reserve_dense(lib().rsvd_svd_workspace_bytes, m, n, dt, method)
+        U = empty_colmajor(m, k, A.dtype, A.device)
+        S = torch.empty(k, dtype=A.dtype, device=A.device)
+        V = empty_colmajor(n, k, A.dtype, A.device)
+        kept = ctypes.c_int32(0)
+        check(lib().rsvd_svd(self.h, m, n, ctypes.c_void_p(A.data_ptr()), lda, dt, int(method), r, seed,
+                             ctypes.c_void_p(U.data_ptr()), U.stride(1), ctypes.c_void_p(S.data_ptr()),
+                             ctypes.c_void_p(V.data_ptr()), V.stride(1), ctypes.byref(kept)), self.h)
+        kk = kept.value
+        return U[:, :kk], S[:kk], V[:, :kk]
+
+    def qr_host(self, A: np.ndarray, full: bool = False):
+        A = np.asfortranarray(A, dtype=np.float64)
+        m, n = A.shape
+        kq = m if full else n
+        Q = np.zeros((m, kq), order="F")
+        R = np.zeros((kq, n), order="F")
+        self._reserve_dense(lib().rsvd_qr_workspace_bytes, m, n, _capi.F64, full)
+        check(lib().rsvd_qr_host_f64(self.h, m, n, _dp(A), m, int(full), _dp(Q), _dp(R)), self.h)
+        return Q, R
+
+    def svd_host(self, A: np.ndarray, method: int = SVDMethod.Jacobi, r: int = 0, seed: int = 0):
+        A = np.asfortranarray(A, dtype=np.float64)
+        m, n = A.shape
+        k = min(m, n)
+        U = np.zeros((m, k), order="F")
+        S = np.zeros(k)
+        V = np.zeros((n, k), order="F")
+        kept = ctypes.c_int32(0)
+        self._reserve_dense(lib().rsvd_svd_workspace_bytes, m, n, _capi.F64, method)
+        check(lib().rsvd_svd_host_f64(self.h, m, n, _dp(A), m, int(method), r, seed, _dp(U), _dp(S), _dp(V),
+                                      ctypes.byref(kept)), self.h)
+        kk = kept.value
+        return U[:, :kk].copy(order="F"), S[:kk].copy(), V[:, :kk].copy(order="F")
+
 
 _DEFAULT: Optional[Engine] = None
 
@@ -309,3 +373,70 @@ def intermediate_step(A, Omega, l: int, q: int):
 def generateOmega(n: int, l: int, seed: int = 0):
     """generateOmega (src/rSVD.cpp:12-55): n x l N(0,1), reproducible from `seed`."""
     return default_engine().generate_omega_host(n, l, seed)
+
+
+def qr_decomposition_reduced(A):
+    """qr_decomposition_reduced (src/QR.cpp:43-80): (Q m x n, R n x n); requires m >= n."""
+    eng = default_engine()
+    return eng.qr(A, full=False) if _is_torch(A) else eng.qr_host(A, full=False)
+
+
+def qr_decomposition_full(A):
+    """qr_decomposition_full (src/QR.cpp:22-41): (Q m x m, R m x n)."""
+    eng = default_engine()
+    return eng.qr(A, full=True) if _is_torch(A) else eng.qr_host(A, full=True)
+
+
+class SVD:
+    """template<SVDMethod method> class SVD (include/SVD_class.hpp:35-71) on the GPU engine.
+
+    ``SVD(data, r=0, method=SVDMethod.Jacobi)``; ``compute()``; ``getU/getS/getV``; ``setData``.
+    Output shapes follow the reference: Jacobi / ParallelJacobi U m x k, S k, V n x k
+    (k = min(m, n), :107-108); Power U m x m and V n x n initialised to the identity with u_i in
+    column i of U and v_i in ROW i of V (:82-83, :213-214), S of length min(m, n); when the
+    power method stops early at sigma < 1e-12 after i triplets the three are cut to their first i
+    columns as conservativeResize does (:198-208).  ``compute()`` prints nothing (the reference
+    writes progress to stdout, :80-95).  ``seed`` replaces the power method's random_device start
+    vectors (src/PM.cpp:15-16) with Philox(seed + i).
+    """
+
+    def __init__(self, data, r: int = 0, method: SVDMethod = SVDMethod.Jacobi, seed: int = 0):
+        self._data = np.array(data, dtype=np.float64, order="F", copy=True)
+        self._r = int(r)
+        self._method = SVDMethod(method)
+        self._seed = seed
+        self._U = self._S = self._V = None
+
+    def setData(self, data):
+        self._data = np.array(data, dtype=np.float64, order="F", copy=True)
+
+    def compute(self):
+        m, n = self._data.shape
+        eng = default_engine()
+        if self._method != SVDMethod.Power:
+            self._U, self._S, self._V = eng.svd_host(self._data, self._method)
+            return
+        dim = self._r if self._r else min(m, n)
+        u, s, v = eng.svd_host(self._data, SVDMethod.Power, r=self._r, seed=self._seed)
+        k = s.shape[0]
+        if k == 0:
+            self._U, self._S, self._V = np.zeros((m, 1)), np.zeros(1), np.zeros((n, 1))
+            return
+        U = np.eye(m, order="F")
+        V = np.eye(n, order="F")
+        S = np.zeros(min(m, n))
+        U[:, :k] = u
+        V[:k, :] = v.T
+        S[:k] = s
+        if k < dim:
+            U, S, V = U[:, :k].copy(order="F"), S[:k].copy(), V[:, :k].copy(order="F")
+        self._U, self._S, self._V = U, S, V
+
+    def getU(self):
+        return self._U
+
+    def getS(self):
+        return self._S
+
+    def getV(self):
+        return self._V

@@ -1,0 +1,431 @@
+// dense.hip -- kernels of the dense drop-ins next to rSVD: QR() (src/QR.cpp:22-80) and the
+// stand-alone SVD<method> (include/SVD_class.hpp:79-219).  The heavy lifting reuses the wide
+// engine's CholeskyQR / Gram / panel-product / Jacobi kernels (wide_qr.hip, wide_svd.hip,
+// jacobi.hip); this file adds the layout helpers and the power method.
+//
+//   transpose_to_panel   A (m x n col-major) -> A^T as an n x LP row-major panel: the panel row j
+//                        is column j of A, so reads and writes are both unit-stride.
+//   upper_to_colmajor    R = Q^T A (LP x LP fp64 row-major) -> the caller's column-major R with the
+//                        strictly lower part set to 0 (Givens R is upper triangular / trapezoidal).
+//   shift_diag           G += s I, s = 11 (rows l + l (l + 1)) u tr(G): the shift of shifted
+//                        CholeskyQR3, which keeps the first pass positive definite up to
+//                        cond(A) ~ 1/u (Fukaya et al., SIAM J. Sci. Comput. 2020).
+//   power_svd_kernel     SVD<Power> (SVD_class.hpp:183-219 + src/PM.cpp:4-81): for i < dim, a
+//                        fixed number `s` of power iterations x <- B x / |B x| on the deflated
+//                        B = A^T A, v = x, sigma = |A_i v|, u = A_i v / sigma, stop when
+//                        sigma < 1e-12, deflate B -= sigma^2 (u.u) v v^T.  A_i = A - sum_j<i
+//                        sigma_j u_j v_j^T is applied implicitly (A v - sum_j sigma_j (v_j.v) u_j),
+//                        so A is never rewritten.  One workgroup; B lives in LDS when LP <= 128.
+#include "common.hpp"
+#include "dense.hpp"
+
+namespace rsvd {
+
+namespace {
+
+constexpr int kPowThreads = 1024;
+
+template <typename T>
+__global__ void transpose_to_panel_kernel(const T* __restrict__ A, int64_t lda, int64_t m, int64_t n, int LP,
+                                          T* __restrict__ P) {
+    const int64_t total = n * LP;
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t j = e / LP;
+        const int64_t i = e - j * LP;
+        P[e] = (i < m) ? A[i + j * lda] : T(0);
+    }
+}
+
+template <typename T>
+__global__ void unit_columns_kernel(T* __restrict__ P, int LP, int c0, int c1) {
+    const int j = c0 + blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < c1) P[(int64_t)j * LP + j] = T(1);
+}
+
+// One workgroup: nz[j] = column j of A has a non-zero below the diagonal; the leading run of
+// columns with nz[j] == 0 saw no Givens rotation in the reference, so R(j,j) = A(j,j).
+template <typename T>
+__global__ __launch_bounds__(256) void qr_signs_kernel(const T* __restrict__ A, int64_t lda, int64_t m, int n,
+                                                       T* __restrict__ Qp, int LP) {
+    __shared__ int nz[512];
+    __shared__ int run;
+    const int kmin = (int)(m < n ? m : n);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    for (int j = w; j < kmin; j += 4) {
+        int any = 0;
+        for (int64_t i = j + 1 + lane; i < m; i += 64) any |= A[i + j * lda] != T(0);
+        any = __any(any);
+        if (lane == 0) nz[j] = any;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int t = 0;
+        while (t < kmin && !nz[t]) ++t;
+        run = t;
+    }
+    __syncthreads();
+    for (int j = 0; j < run; ++j) {
+        if (!(A[j + j * lda] < T(0))) continue;
+        for (int64_t i = threadIdx.x; i < m; i += 256) Qp[i * LP + j] = -Qp[i * LP + j];
+    }
+}
+
+// Out = In R^-1 by forward substitution per row (R upper, LP x LP fp64): q R = a solved row by
+// row is backward stable, |a - q R| <= O(u) |q| |R|, however ill-conditioned R is -- the explicit
+// R^-1 product of the rSVD panels (wide_qr.hip panel_gemm) loses u * cond(R), which a QR() caller
+// would see as A != Q R for rank-deficient A.  One thread per row; the R columns of a 32-wide
+// chunk are staged in LDS (rows 0 .. c0 + 32), earlier outputs of the row are re-read from Out.
+template <typename T>
+__global__ __launch_bounds__(256) void trsm_rows_kernel(const T* __restrict__ In, int64_t rows, int k, int LP,
+                                                        const double* __restrict__ R, T* __restrict__ Out,
+                                                        const int* __restrict__ pred) {
+    if (pred && *pred == 0) return;
+    extern __shared__ double Rs[];  // [c0 + 32][32]
+    const int tid = threadIdx.x;
+    const int64_t row = blockIdx.x * 256ll + tid;
+    const bool live = row < rows;
+    for (int c0 = 0; c0 < LP; c0 += 32) {
+        const int cw = (LP - c0 < 32) ? LP - c0 : 32;
+        __syncthreads();
+        for (int e = tid; e < (c0 + cw) * 32; e += 256) {
+            const int t = e >> 5, j = e & 31;
+            Rs[e] = (j < cw) ? R[(int64_t)t * LP + c0 + j] : 0.0;
+        }
+        __syncthreads();
+        if (!live) continue;
+        double x[32];
+#pragma unroll
+        for (int j = 0; j < 32; ++j) x[j] = (c0 + j < k) ? (double)In[row * LP + c0 + j] : 0.0;
+        for (int t = 0; t < c0; ++t) {
+            const double q = (double)Out[row * LP + t];
+#pragma unroll
+            for (int j = 0; j < 32; ++j) x[j] -= q * Rs[t * 32 + j];
+        }
+#pragma unroll
+        for (int j = 0; j < 32; ++j) {
+            const int c = c0 + j;
+            if (c < k) {
+                x[j] /= Rs[c * 32 + j];
+#pragma unroll
+                for (int jj = j + 1; jj < 32; ++jj) x[jj] -= x[j] * Rs[c * 32 + jj];
+            } else {
+                x[j] = 0.0;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 32; ++j)
+            if (j < cw) Out[row * LP + c0 + j] = (T)x[j];
+    }
+}
+
+// det(Q) of a square Q (m x m in a row-major LP panel) by LU with partial pivoting in W (LP x LP
+// fp64 scratch, L2-resident); when det(Q) < 0 column m-1 of Q is negated.  The reference's Q is a
+// product of Givens rotations (det +1) and its last column is never rotated on its own
+// (src/QR.cpp:31-32: no row below it), so R(m-1, m-1) carries whatever sign makes det(Q) = +1.
+template <typename T>
+__global__ __launch_bounds__(1024) void det_sign_kernel(T* __restrict__ Qp, int m, int LP, double* __restrict__ W) {
+    __shared__ double bv[16];
+    __shared__ int bi[16];
+    __shared__ int piv;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    for (int e = tid; e < m * m; e += 1024) {
+        const int i = e / m, j = e - i * m;
+        W[(int64_t)i * LP + j] = (double)Qp[(int64_t)i * LP + j];
+    }
+    __syncthreads();
+    int sign = 1;
+    for (int k = 0; k < m; ++k) {
+        double v = -1.0;
+        int vi = k;
+        for (int i = k + tid; i < m; i += 1024) {
+            const double a = fabs(W[(int64_t)i * LP + k]);
+            if (a > v) {
+                v = a;
+                vi = i;
+            }
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            const double ov = __shfl_xor(v, o);
+            const int oi = __shfl_xor(vi, o);
+            if (ov > v || (ov == v && oi < vi)) {
+                v = ov;
+                vi = oi;
+            }
+        }
+        if (lane == 0) {
+            bv[w] = v;
+            bi[w] = vi;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            double b = bv[0];
+            int p = bi[0];
+            for (int t = 1; t < 16; ++t)
+                if (bv[t] > b || (bv[t] == b && bi[t] < p)) {
+                    b = bv[t];
+                    p = bi[t];
+                }
+            piv = p;
+        }
+        __syncthreads();
+        const int p = piv;
+        if (p != k) {
+            for (int j = k + tid; j < m; j += 1024) {
+                const double t = W[(int64_t)k * LP + j];
+                W[(int64_t)k * LP + j] = W[(int64_t)p * LP + j];
+                W[(int64_t)p * LP + j] = t;
+            }
+            sign = -sign;
+            __syncthreads();
+        }
+        const double d = W[(int64_t)k * LP + k];
+        if (!(d != 0.0)) {  // singular (cannot happen for an orthonormal Q): leave Q as is
+            sign = 1;
+            break;
+        }
+        if (d < 0.0) sign = -sign;
+        const int rem = m - k - 1;
+        for (int e = tid; e < rem * rem; e += 1024) {
+            const int i = k + 1 + e / rem, j = k + 1 + e % rem;
+            W[(int64_t)i * LP + j] -= (W[(int64_t)i * LP + k] / d) * W[(int64_t)k * LP + j];
+        }
+        __syncthreads();
+    }
+    if (sign < 0)
+        for (int i = tid; i < m; i += 1024) Qp[(int64_t)i * LP + m - 1] = -Qp[(int64_t)i * LP + m - 1];
+}
+
+template <typename T>
+__global__ void upper_to_colmajor_kernel(const double* __restrict__ Rf, int LP, int nr, int nc, T* __restrict__ R,
+                                         int64_t ldr) {
+    const int64_t total = (int64_t)nr * nc;
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+        const int j = (int)(e / nr), i = (int)(e - (int64_t)j * nr);
+        R[i + j * ldr] = (i <= j) ? (T)Rf[(int64_t)i * LP + j] : T(0);
+    }
+}
+
+__global__ __launch_bounds__(256) void shift_diag_kernel(double* __restrict__ G, int LP, int l, int64_t rows,
+                                                         double u) {
+    __shared__ double part[256];
+    double t = 0.0;
+    for (int i = threadIdx.x; i < l; i += 256) t += G[(int64_t)i * LP + i];
+    part[threadIdx.x] = t;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) part[threadIdx.x] += part[threadIdx.x + w];
+        __syncthreads();
+    }
+    const double sh = 11.0 * ((double)rows * l + (double)l * (l + 1)) * u * part[0];
+    for (int i = threadIdx.x; i < l; i += 256) G[(int64_t)i * LP + i] += sh;
+}
+
+// Sum over the workgroup (kPowThreads threads); every thread gets the total.  `red` >= 17 doubles.
+__device__ __forceinline__ double block_sum(double v, double* red) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    __syncthreads();  // `red` may still be read from the previous call
+    if (lane == 0) red[w] = v;
+    __syncthreads();
+    double t = 0.0;
+#pragma unroll
+    for (int i = 0; i < kPowThreads / 64; ++i) t += red[i];
+    return t;
+}
+
+// y = B x for symmetric B (row-major, ld LP): TPR consecutive threads share a row and stride the
+// columns, so a row is read with unit stride; partial sums combined with lane shuffles.
+template <bool LDSB>
+__device__ __forceinline__ void sym_matvec(const double* __restrict__ B, int n, int LP, int tpr,
+                                           const double* __restrict__ x, double* __restrict__ y) {
+    const int sub = threadIdx.x % tpr;
+    for (int r0 = threadIdx.x / tpr; r0 < n; r0 += kPowThreads / tpr) {
+        const double* row = B + (int64_t)r0 * LP;
+        double acc = 0.0;
+        for (int c = sub; c < n; c += tpr) acc += row[c] * x[c];
+        for (int o = tpr >> 1; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+        if (sub == 0) y[r0] = acc;
+    }
+}
+
+template <typename T, bool LDSB>
+__global__ __launch_bounds__(kPowThreads) void power_svd_kernel(const T* __restrict__ P, int64_t m, int n, int LP,
+                                                                double* __restrict__ Bg, int dim, uint64_t seed,
+                                                                int iters, T* __restrict__ Up, double* __restrict__ Vr,
+                                                                double* __restrict__ S, int* __restrict__ kept) {
+    extern __shared__ double lds[];
+    double* x = lds;            // LP
+    double* y = x + LP;         // LP
+    double* coef = y + LP;      // LP
+    double* red = coef + LP;    // 32
+    double* B = LDSB ? red + 32 : Bg;
+    const int tid = threadIdx.x;
+    if (LDSB) {
+        for (int e = tid; e < LP * LP; e += kPowThreads) B[e] = Bg[e];
+        __syncthreads();
+    }
+    int tpr = 1;
+    while (tpr < 16 && n * tpr * 2 <= kPowThreads) tpr *= 2;
+    int k = dim;
+    for (int i = 0; i < dim; ++i) {
+        // x0 = N(0,1) Philox stream (seed + i), normalised (src/PM.cpp:15-22)
+        double sq = 0.0;
+        for (int c = tid; c < n; c += kPowThreads) {
+            const double g = gauss_elem((uint64_t)c, seed + (uint64_t)i);
+            x[c] = g;
+            sq += g * g;
+        }
+        double nrm = sqrt(block_sum(sq, red));
+        for (int c = tid; c < n; c += kPowThreads) x[c] /= nrm;
+        __syncthreads();
+        for (int it = 0; it < iters; ++it) {  // x0 = B x0 ; x0.normalize()  (src/PM.cpp:40-69)
+            sym_matvec<LDSB>(B, n, LP, tpr, x, y);
+            __syncthreads();
+            sq = 0.0;
+            for (int c = tid; c < n; c += kPowThreads) sq += y[c] * y[c];
+            nrm = sqrt(block_sum(sq, red));
+            for (int c = tid; c < n; c += kPowThreads) x[c] = y[c] / nrm;
+            __syncthreads();
+        }
+        sq = 0.0;  // v = x0.normalized() (:72-73)
+        for (int c = tid; c < n; c += kPowThreads) sq += x[c] * x[c];
+        nrm = sqrt(block_sum(sq, red));
+        for (int c = tid; c < n; c += kPowThreads) x[c] /= nrm;
+        // coef_j = sigma_j (v_j . v): the deflations A_i = A - sum_j sigma_j u_j v_j^T applied to v
+        {
+            const int lane = tid & 63, w = tid >> 6;
+            __syncthreads();
+            for (int j = w; j < i; j += kPowThreads / 64) {
+                double d = 0.0;
+                for (int c = lane; c < n; c += 64) d += Vr[(int64_t)j * LP + c] * x[c];
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) d += __shfl_xor(d, o);
+                if (lane == 0) coef[j] = S[j] * d;
+            }
+            __syncthreads();
+        }
+        // w = A_i v (:76,79); written into column i of the U panel, normalised below
+        sq = 0.0;
+        for (int64_t r = tid; r < m; r += kPowThreads) {
+            const T* row = P + r * LP;
+            double acc = 0.0;
+            for (int c = 0; c < n; ++c) acc += (double)row[c] * x[c];
+            const T* urow = Up + r * LP;
+            for (int j = 0; j < i; ++j) acc -= coef[j] * (double)urow[j];
+            Up[r * LP + i] = (T)acc;
+            sq += acc * acc;
+        }
+        const double sigma = sqrt(block_sum(sq, red));
+        if (sigma < 1e-12) {  // SVD_class.hpp:198-208
+            k = i;
+            break;
+        }
+        sq = 0.0;
+        for (int64_t r = tid; r < m; r += kPowThreads) {
+            const double u = (double)Up[r * LP + i] / sigma;
+            Up[r * LP + i] = (T)u;
+            sq += u * u;
+        }
+        const double f = sigma * sigma * block_sum(sq, red);  // B -= update^T update (:212)
+        for (int e = tid; e < n * n; e += kPowThreads) {
+            const int r = e / n, c = e - r * n;
+            B[(int64_t)r * LP + c] -= f * (x[r] * x[c]);
+        }
+        for (int c = tid; c < n; c += kPowThreads) Vr[(int64_t)i * LP + c] = x[c];  // V_.row(i) = v (:214)
+        if (tid == 0) S[i] = sigma;
+        __syncthreads();
+    }
+    if (tid == 0) *kept = k;
+}
+
+inline int grid_of(int64_t work) {
+    int64_t g = (work + 255) / 256;
+    return (int)(g > 8192 ? 8192 : (g < 1 ? 1 : g));
+}
+
+}  // namespace
+
+template <typename T>
+hipError_t launch_transpose_to_panel(const T* A, int64_t lda, int64_t m, int64_t n, int LP, T* P, hipStream_t s) {
+    hipLaunchKernelGGL((transpose_to_panel_kernel<T>), dim3(grid_of(n * LP)), dim3(256), 0, s, A, lda, m, n, LP, P);
+    return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_unit_columns(T* P, int LP, int c0, int c1, hipStream_t s) {
+    if (c1 <= c0) return hipSuccess;
+    hipLaunchKernelGGL((unit_columns_kernel<T>), dim3((c1 - c0 + 255) / 256), dim3(256), 0, s, P, LP, c0, c1);
+    return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_qr_signs(const T* A, int64_t lda, int64_t m, int n, T* Qp, int LP, hipStream_t s) {
+    if ((m < n ? m : n) > 512) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((qr_signs_kernel<T>), dim3(1), dim3(256), 0, s, A, lda, m, n, Qp, LP);
+    return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_trsm_rows(const T* In, int64_t rows, int k, int LP, const double* R, T* Out, const int* pred,
+                            hipStream_t s) {
+    if (LP % 16 || LP > 512 || k > LP) return hipErrorInvalidValue;
+    const size_t lds = (size_t)(LP + 32) * 32 * sizeof(double);
+    hipLaunchKernelGGL((trsm_rows_kernel<T>), dim3((unsigned)((rows + 255) / 256)), dim3(256), lds, s, In, rows, k, LP,
+                       R, Out, pred);
+    return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_det_sign(T* Qp, int m, int LP, double* W, hipStream_t s) {
+    if (m > LP) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((det_sign_kernel<T>), dim3(1), dim3(1024), 0, s, Qp, m, LP, W);
+    return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_upper_to_colmajor(const double* Rf, int LP, int nr, int nc, T* R, int64_t ldr, hipStream_t s) {
+    hipLaunchKernelGGL((upper_to_colmajor_kernel<T>), dim3(grid_of((int64_t)nr * nc)), dim3(256), 0, s, Rf, LP, nr,
+                       nc, R, ldr);
+    return hipGetLastError();
+}
+
+hipError_t launch_shift_diag(double* G, int LP, int l, int64_t rows, double u, hipStream_t s) {
+    hipLaunchKernelGGL(shift_diag_kernel, dim3(1), dim3(256), 0, s, G, LP, l, rows, u);
+    return hipGetLastError();
+}
+
+int power_iterations(int64_t n) {
+    // s = ceil(log(4 log(2 n / delta) / (eps delta)) / (2 lambda)), src/PM.cpp:25-28
+    const double eps = 1.e-10, delta = 0.05, lambda = 0.1;
+    return (int)ceil(log(4.0 * log(2.0 * (double)n / delta) / (eps * delta)) / (2.0 * lambda));
+}
+
+hipError_t launch_power_svd(const double* P, int64_t m, int n, int LP, double* B, int dim, uint64_t seed, int iters,
+                            double* Up, double* Vr, double* S, int* kept, hipStream_t s) {
+    if (n > LP || LP > 512 || dim > n) return hipErrorInvalidValue;
+    const size_t small = (size_t)(3 * LP + 32) * sizeof(double);
+    if (LP <= 128) {
+        const size_t lds = small + (size_t)LP * LP * sizeof(double);
+        hipLaunchKernelGGL((power_svd_kernel<double, true>), dim3(1), dim3(kPowThreads), lds, s, P, m, n, LP, B, dim,
+                           seed, iters, Up, Vr, S, kept);
+    } else {
+        hipLaunchKernelGGL((power_svd_kernel<double, false>), dim3(1), dim3(kPowThreads), small, s, P, m, n, LP, B,
+                           dim, seed, iters, Up, Vr, S, kept);
+    }
+    return hipGetLastError();
+}
+
+#define RSVD_INST(T)                                                                                         \
+    template hipError_t launch_transpose_to_panel<T>(const T*, int64_t, int64_t, int64_t, int, T*, hipStream_t); \
+    template hipError_t launch_upper_to_colmajor<T>(const double*, int, int, int, T*, int64_t, hipStream_t); \
+    template hipError_t launch_unit_columns<T>(T*, int, int, int, hipStream_t);                               \
+    template hipError_t launch_det_sign<T>(T*, int, int, double*, hipStream_t);                               \
+    template hipError_t launch_trsm_rows<T>(const T*, int64_t, int, int, const double*, T*, const int*, hipStream_t); \
+    template hipError_t launch_qr_signs<T>(const T*, int64_t, int64_t, int, T*, int, hipStream_t);
+RSVD_INST(float)
+RSVD_INST(double)
+#undef RSVD_INST
+
+}  // namespace rsvd

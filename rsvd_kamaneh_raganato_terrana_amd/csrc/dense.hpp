@@ -1,0 +1,41 @@
+// dense.hpp -- launch wrappers of dense.hip (the QR() and SVD<method> drop-ins, dense.cpp).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rsvd {
+
+// P (n x LP row-major) = A^T for A m x n column-major (lda); columns m..LP-1 of P are zero.
+template <typename T>
+hipError_t launch_transpose_to_panel(const T* A, int64_t lda, int64_t m, int64_t n, int LP, T* P, hipStream_t s);
+// P[j][j] = 1 for j in [c0, c1) (identity completion columns of the full QR basis).
+template <typename T>
+hipError_t launch_unit_columns(T* P, int LP, int c0, int c1, hipStream_t s);
+// R (nr x nc column-major, ldr) = upper triangle of Rf (LP x LP fp64 row-major), zeros below.
+template <typename T>
+hipError_t launch_upper_to_colmajor(const double* Rf, int LP, int nr, int nc, T* R, int64_t ldr, hipStream_t s);
+// G[:l,:l] += 11 (rows l + l (l+1)) u tr(G) I  (shifted CholeskyQR3, first pass)
+hipError_t launch_shift_diag(double* G, int LP, int l, int64_t rows, double u, hipStream_t s);
+// Givens sign convention (src/QR.cpp:31-39): a leading column whose sub-diagonal is already zero
+// gets no rotation, so R(j,j) keeps the sign of A(j,j).  For the leading run of such columns of A
+// (m x n, lda), negate column j of the Q panel (m x LP) where A(j,j) < 0.
+template <typename T>
+hipError_t launch_qr_signs(const T* A, int64_t lda, int64_t m, int n, T* Qp, int LP, hipStream_t s);
+// Out (rows x LP) = In R^-1, R upper LP x LP fp64, by row-wise forward substitution (backward
+// stable for any cond(R)); columns >= k of Out are 0.  `pred`: skip unless *pred != 0.
+template <typename T>
+hipError_t launch_trsm_rows(const T* In, int64_t rows, int k, int LP, const double* R, T* Out, const int* pred,
+                            hipStream_t s);
+// Square Q (m x m panel): negate column m-1 when det(Q) < 0 (the Givens Q has det +1).  W: LP x
+// LP fp64 scratch.  One workgroup, LU with partial pivoting.
+template <typename T>
+hipError_t launch_det_sign(T* Qp, int m, int LP, double* W, hipStream_t s);
+// Iterations per singular value of the reference power method (src/PM.cpp:25-28).
+int power_iterations(int64_t n);
+// SVD<Power> on A (m x LP fp64 panel, n used columns) with B = A^T A (LP x LP, overwritten):
+// u_i -> column i of Up (m x LP panel), v_i -> row i of Vr (LP x LP), S[i]; *kept = triplets
+// found (< dim when sigma < 1e-12 stops it).  One workgroup.  n <= LP <= 512.
+hipError_t launch_power_svd(const double* P, int64_t m, int n, int LP, double* B, int dim, uint64_t seed, int iters,
+                            double* Up, double* Vr, double* S, int* kept, hipStream_t s);
+
+}  // namespace rsvd
