@@ -113,6 +113,112 @@ Mat generate_omega(int n, int l) {
     return Om;
 }
 
+// qr_decomposition_reduced(A, Q, R) (src/QR.cpp:43-80): Q m x n, R n x n; requires m >= n.
+template <class Mat>
+void qr_reduced(const Mat& A, Mat& Q, Mat& R) {
+    const int64_t m = A.rows(), n = A.cols();
+    Q.resize(m, n);
+    R.resize(n, n);
+    check(rsvd_qr_host_f64(Context::instance().handle(), m, n, A.data(), m, 0, Q.data(), R.data()),
+          "qr_decomposition_reduced");
+}
+
+// qr_decomposition_full(A, Q, R) (src/QR.cpp:22-41): Q m x m, R m x n.
+template <class Mat>
+void qr_full(const Mat& A, Mat& Q, Mat& R) {
+    const int64_t m = A.rows(), n = A.cols();
+    Q.resize(m, m);
+    R.resize(m, n);
+    check(rsvd_qr_host_f64(Context::instance().handle(), m, n, A.data(), m, 1, Q.data(), R.data()),
+          "qr_decomposition_full");
+}
+
+// SVD<method> (include/SVD_class.hpp:35-219) over any Mat / Vec pair of the kind above.
+// Jacobi / ParallelJacobi: U m x k, S k, V n x k (k = min(m, n), :107-108).  Power: U m x m and
+// V n x n start as identities, u_i goes to column i of U and v_i to ROW i of V (:82-83, :213-214),
+// S has min(m, n) entries; an early stop after i < dim triplets (sigma < 1e-12) keeps the first i
+// columns of each, as conservativeResize does (:198-208).  compute() prints nothing.
+template <Method M, class Mat, class Vec>
+class SVDT {
+public:
+    explicit SVDT(const Mat& data, const int& r = 0) : data_(data), r_(r) {}
+    void compute() {
+        const int64_t m = data_.rows(), n = data_.cols(), k = m < n ? m : n;
+        Context& c = Context::instance();
+        if (M != Method::Power) {
+            U_.resize(m, k);
+            S_.resize(k);
+            V_.resize(n, k);
+            int32_t kept = 0;
+            check(rsvd_svd_host_f64(c.handle(), m, n, data_.data(), m, static_cast<int32_t>(M), 0, 0, U_.data(),
+                                    S_.data(), V_.data(), &kept),
+                  "SVD::compute");
+            return;
+        }
+        const int64_t dim = r_ ? r_ : k;
+        Mat u, v;
+        Vec s;
+        u.resize(m, k);
+        v.resize(n, k);
+        s.resize(k);
+        int32_t kept = 0;
+        check(rsvd_svd_host_f64(c.handle(), m, n, data_.data(), m, RSVD_SVD_POWER, r_, c.next_seed(), u.data(),
+                                s.data(), v.data(), &kept),
+              "SVD::compute");
+        if (kept == 0) {  // :199-202
+            U_.resize(m, 1);
+            S_.resize(1);
+            V_.resize(n, 1);
+            fill(U_, 0.0), fill(V_, 0.0), fill(S_, 0.0);
+            return;
+        }
+        U_.resize(m, m);
+        V_.resize(n, n);
+        S_.resize(k);
+        identity(U_), identity(V_), fill(S_, 0.0);
+        for (int64_t i = 0; i < kept; ++i) {
+            for (int64_t t = 0; t < m; ++t) U_.data()[t + i * m] = u.data()[t + i * m];
+            for (int64_t t = 0; t < n; ++t) V_.data()[i + t * n] = v.data()[t + i * n];
+            S_.data()[i] = s.data()[i];
+        }
+        if (kept < dim) {  // conservativeResize to the first `kept` columns
+            U_ = leading_cols(U_, kept);
+            V_ = leading_cols(V_, kept);
+            Vec s2;
+            s2.resize(kept);
+            for (int64_t i = 0; i < kept; ++i) s2.data()[i] = S_.data()[i];
+            S_ = s2;
+        }
+    }
+    Mat getU() const { return U_; }
+    Vec getS() const { return S_; }
+    Mat getV() const { return V_; }
+
+protected:
+    void setData(const Mat& data) { data_ = data; }
+
+private:
+    template <class X>
+    static void fill(X& x, double v) {
+        const int64_t nn = (int64_t)x.size();
+        for (int64_t i = 0; i < nn; ++i) x.data()[i] = v;
+    }
+    static void identity(Mat& x) {
+        fill(x, 0.0);
+        const int64_t r = x.rows(), cc = x.cols();
+        for (int64_t i = 0; i < r && i < cc; ++i) x.data()[i + i * r] = 1.0;
+    }
+    static Mat leading_cols(const Mat& x, int64_t cols) {
+        Mat y;
+        y.resize(x.rows(), cols);
+        for (int64_t i = 0; i < x.rows() * cols; ++i) y.data()[i] = x.data()[i];
+        return y;
+    }
+    Mat U_, V_, data_;
+    Vec S_;
+    int r_;
+};
+
 }  // namespace rsvd
 
 #endif  // RSVD_HPP

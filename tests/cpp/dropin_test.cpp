@@ -1,7 +1,9 @@
-// dropin_test.cpp -- exercises include/rsvd.hpp (the generic C++ adapter under include/rSVD.hpp)
-// with a minimal column-major matrix type, the way tests/rSVD_test.cpp calls rSVD() on Eigen
-// matrices: I_100 with l = 16 must give S == 1 and ||A - U S V^T||_F = sqrt(100 - 16); an
-// unsupported method must throw std::invalid_argument("Unsupported SVD method").
+// dropin_test.cpp -- exercises include/rsvd.hpp (the generic C++ adapter under include/rSVD.hpp,
+// include/QR.hpp and include/SVD_class.hpp) with a minimal column-major matrix type, the way
+// tests/rSVD_test.cpp calls rSVD() on Eigen matrices: I_100 with l = 16 must give S == 1 and
+// ||A - U S V^T||_F = sqrt(100 - 16); an unsupported method must throw
+// std::invalid_argument("Unsupported SVD method").  Also: QR() (A = Q R, Q^T Q = I, R upper)
+// and SVD<method> (reconstruction; the Power layouts and early stop of SVD_class.hpp:183-219).
 // Build: make -C tests/cpp ; run on a GPU: tests/cpp/dropin_test  (exit 0 = pass)
 #include <cmath>
 #include <cstdio>
@@ -15,6 +17,7 @@ struct HostMat {  // column-major, ld == rows
     std::vector<double> v;
     long rows() const { return r; }
     long cols() const { return c; }
+    long size() const { return r * c; }
     double* data() { return v.data(); }
     const double* data() const { return v.data(); }
     void resize(long rr, long cc) { r = rr; c = cc; v.assign((size_t)rr * cc, 0.0); }
@@ -78,6 +81,91 @@ int main() {
         threw = std::string(e.what()) == "Unsupported SVD method";
     }
     CHECK(threw, "unsupported method throws std::invalid_argument");
+    // ---- QR(): reduced and full ----------------------------------------------------------------
+    {
+        const int qm = 50, qn = 20;
+        HostMat B;
+        B.resize(qm, qn);
+        unsigned st = 12345u;
+        for (auto& x : B.v) x = ((st = st * 1664525u + 1013904223u) >> 8) / 16777216.0 - 0.5;
+        for (int full = 0; full < 2; ++full) {
+            HostMat Q, R;
+            if (full) rsvd::qr_full(B, Q, R); else rsvd::qr_reduced(B, Q, R);
+            const long kq = full ? qm : qn;
+            CHECK(Q.rows() == qm && Q.cols() == kq && R.rows() == kq && R.cols() == qn, "QR shapes (full=%d)", full);
+            double oe = 0, re = 0, lo = 0;
+            for (long a = 0; a < kq; ++a)
+                for (long b = 0; b < kq; ++b) {
+                    double d = 0;
+                    for (long i = 0; i < qm; ++i) d += Q(i, a) * Q(i, b);
+                    oe = std::fmax(oe, std::fabs(d - (a == b)));
+                }
+            for (long i = 0; i < qm; ++i)
+                for (long j = 0; j < qn; ++j) {
+                    double d = 0;
+                    for (long t = 0; t < kq; ++t) d += Q(i, t) * R(t, j);
+                    re = std::fmax(re, std::fabs(d - B(i, j)));
+                }
+            for (long i = 0; i < kq; ++i)
+                for (long j = 0; j < qn && j < i; ++j) lo = std::fmax(lo, std::fabs(R(i, j)));
+            CHECK(oe < 1e-13 && re < 1e-13 && lo == 0.0, "QR full=%d: orth %g recon %g lower %g", full, oe, re, lo);
+        }
+        bool threw = false;
+        try {
+            HostMat W, Q, R;
+            W.resize(3, 5);
+            rsvd::qr_reduced(W, Q, R);
+        } catch (const std::invalid_argument&) {
+            threw = true;
+        }
+        CHECK(threw, "reduced QR of a wide matrix throws std::invalid_argument");
+    }
+    // ---- SVD<Jacobi>: reconstruction; SVD<Power>: layouts and early stop ----------------------------
+    {
+        const int sm = 40, sn = 25;
+        HostMat B;
+        B.resize(sm, sn);
+        unsigned st = 777u;
+        for (auto& x : B.v) x = ((st = st * 1664525u + 1013904223u) >> 8) / 16777216.0 - 0.5;
+        rsvd::SVDT<rsvd::Method::Jacobi, HostMat, HostVec> sj(B);
+        sj.compute();
+        HostMat Uj = sj.getU(), Vj = sj.getV();
+        HostVec Sj = sj.getS();
+        CHECK(Uj.rows() == sm && Uj.cols() == sn && Vj.rows() == sn && Vj.cols() == sn && Sj.size() == sn, "SVD shapes");
+        double re = 0;
+        for (long i = 0; i < sm; ++i)
+            for (long j = 0; j < sn; ++j) {
+                double d = 0;
+                for (long t = 0; t < sn; ++t) d += Uj(i, t) * Sj.v[t] * Vj(j, t);
+                re = std::fmax(re, std::fabs(d - B(i, j)));
+            }
+        CHECK(re < 1e-13, "SVD<Jacobi> reconstruction %g", re);
+        rsvd::SVDT<rsvd::Method::Power, HostMat, HostVec> sp(B, 4);
+        sp.compute();
+        HostMat Up = sp.getU(), Vp = sp.getV();
+        HostVec Sp = sp.getS();
+        CHECK(Up.rows() == sm && Up.cols() == sm && Vp.rows() == sn && Vp.cols() == sn && Sp.size() == sn,
+              "SVD<Power> layouts: U m x m, V n x n, S min(m, n)");
+        double sd = 0, vd = 0;
+        for (int i = 0; i < 4; ++i) {
+            sd = std::fmax(sd, std::fabs(Sp.v[i] - Sj.v[i]) / Sj.v[0]);
+            double dot = 0;  // v_i is ROW i of the Power V
+            for (long t = 0; t < sn; ++t) dot += Vp(i, t) * Vj(t, i);
+            vd = std::fmax(vd, 1.0 - std::fabs(dot));
+        }
+        // the power method runs a fixed iteration count (src/PM.cpp:25-28), so on the clustered
+        // spectrum of a random matrix it is only partly converged (measured: S 1.3e-7, v 4e-6)
+        CHECK(sd < 1e-5 && vd < 1e-3, "SVD<Power> vs SVD<Jacobi>: S %g, v %g", sd, vd);
+        CHECK(Up(0, sm - 1) == 0.0 && Up(sm - 1, sm - 1) == 1.0 && Vp(sn - 1, sn - 1) == 1.0, "identity beyond dim");
+        HostMat R2;  // rank 2: the power method stops after two triplets
+        R2.resize(sm, sn);
+        for (long i = 0; i < sm; ++i)
+            for (long j = 0; j < sn; ++j) R2(i, j) = 0.01 * ((i + 1.0) * (j % 3 + 1.0) + 0.5 * (i % 2) * (j + 1.0));
+        rsvd::SVDT<rsvd::Method::Power, HostMat, HostVec> se(R2);
+        se.compute();
+        CHECK(se.getU().cols() == 2 && se.getV().cols() == 2 && se.getS().size() == 2 && se.getV().rows() == sn,
+              "SVD<Power> early stop keeps 2 columns");
+    }
     std::printf("%s (%d failures)\n", fails ? "FAILED" : "PASSED", fails);
     return fails ? 1 : 0;
 }
