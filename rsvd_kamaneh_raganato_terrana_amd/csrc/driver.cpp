@@ -130,45 +130,69 @@ struct Engine {
     int orth_index = 0;
     int* cur_flag = nullptr;
 
-    // One CholeskyQR pass: R = chol(P^T P) (Gram summed over ranks when `sharded`), Out = P R^-1.
-    // The factorisation runs in fp32 on the fp32 path (see qr.hip), in fp64 on the fp64 path.
-    int cholqr_pass(const T* P, int64_t rows, T* Out, bool sharded) {
+    // One CholeskyQR pass: R = chol(P^T P) (Gram summed over ranks when `sharded`), Out = P R^-1
+    // (Out may alias P: panel_small stages its rows before writing).  f32: factor in fp32 (the
+    // subspace-only intermediates of the fp32 path, see qr.hip) or fp64.  pred: a predicated pass
+    // (skipped unless *pred != 0) on counters of its own.  refine: receives the need for a second
+    // pass (cond_F(R) too large for one, or a breakdown).
+    int npred = 0, nref = 0;
+    int cholqr_pass(const T* P, int64_t rows, T* Out, bool sharded, int f32, const int* pred = nullptr,
+                    int* refine = nullptr) {
         const int nb = plan_gram_blocks(rows);
         double* tiles = gram + 32 * (size_t)L.LP * L.LP;
-        const int f32 = sizeof(T) == 4;
-        tgt0 += nb;
-        tgt1 += gram_tiles(L.LP, 0);
+        unsigned* c = ctr;
+        unsigned t0, t1;
+        if (pred) {  // private arrival counters (ctr[8 ..]): skipping this launch leaves the others' targets intact
+            c = ctr + 8 + 2 * (npred++ % 26);
+            t0 = (unsigned)nb;
+            t1 = (unsigned)gram_tiles(L.LP, 0);
+        } else {
+            tgt0 += nb;
+            tgt1 += gram_tiles(L.LP, 0);
+            t0 = tgt0;
+            t1 = tgt1;
+        }
         if (sharded && h->world > 1) {
-            RSVD_CK(launch_gram_chol<T>(P, rows, L.LP, nb, gram, tiles, ctr, tgt0, tgt1, 0, f32, Gsum, L.l, nullptr,
-                                        nullptr, cur_flag, s));
+            RSVD_CK(launch_gram_chol<T>(P, rows, L.LP, nb, gram, tiles, c, t0, t1, 0, f32, Gsum, L.l, nullptr,
+                                        nullptr, cur_flag, s, pred));
             RSVD_TRY(allreduce(Gsum, (int64_t)L.LP * L.LP, RSVD_F64));
             RSVD_CK(launch_chol(Gsum, L.l, L.LP, f32, R1, Rinv, cur_flag, s));
         } else {
-            RSVD_CK(launch_gram_chol<T>(P, rows, L.LP, nb, gram, tiles, ctr, tgt0, tgt1, 1, f32, nullptr, L.l, R1, Rinv,
-                                        cur_flag, s));
+            RSVD_CK(launch_gram_chol<T>(P, rows, L.LP, nb, gram, tiles, c, t0, t1, 1, f32, nullptr, L.l, R1, Rinv,
+                                        cur_flag, s, pred, refine));
         }
-        RSVD_CK(launch_panel_small<T>(P, rows, L.LP, Rinv, Out, 0, 0, 0, s));
+        RSVD_CK(launch_panel_small<T>(P, rows, L.LP, Rinv, Out, 0, 0, 0, s, pred));
         return RSVD_OK;
     }
 
-    // CholeskyQR (passes = 1) or CholeskyQR2 (passes = 2): Q = orth(P).  If any pass flags a bad
-    // pivot, the predicated fallback rebuilds Q from P (CGS2 + random completion, util.hip).
+    // CholeskyQR (passes = 1: the subspace-only intermediates) or an output panel (passes = 2).
+    // Output panels of the fp32 path factor in fp64 and run the second CholeskyQR pass only when
+    // the first one's R is too ill-conditioned for one pass (device-side predicate); fp64 panels
+    // and qr_mode CHOLQR2 always run two.  Output panels keep the predicated fallback that
+    // rebuilds Q from P (CGS2 + random completion, util.hip) if any pass flagged a bad pivot.
     int orth(const T* P, int64_t rows, T* Q, bool sharded, int passes) {
         cur_flag = h->dflags + 4 + (orth_index < 12 ? orth_index : 11);
         ++orth_index;
-        if (qr_mode == RSVD_QR_GS2 && !(sharded && h->world > 1)) {  // always the Gram-Schmidt path
+        const bool dist = sharded && h->world > 1;
+        if (qr_mode == RSVD_QR_GS2 && !dist) {  // always the Gram-Schmidt path
             RSVD_CK(hipMemsetAsync(cur_flag, 0xFF, sizeof(int), s));
             RSVD_CK(launch_robust_orth<T>(P, rows, L.l, L.LP, Q, cur_flag, 0x5EEDull + orth_index, s));
             return RSVD_OK;
         }
         if (qr_mode == RSVD_QR_CHOLQR2) passes = 2;
-        if (passes <= 1) {
-            RSVD_TRY(cholqr_pass(P, rows, Q, sharded));
+        const bool output = passes >= 2;
+        const int f32 = sizeof(T) == 4;
+        if (!output) {
+            RSVD_TRY(cholqr_pass(P, rows, Q, sharded, f32));
+        } else if (f32 && qr_mode == RSVD_QR_AUTO && !dist) {
+            int* refine = reinterpret_cast<int*>(ctr + 62 + (nref++ & 1));
+            RSVD_TRY(cholqr_pass(P, rows, Q, sharded, 0, nullptr, refine));
+            RSVD_TRY(cholqr_pass(Q, rows, Q, sharded, 0, refine, nullptr));
         } else {
-            RSVD_TRY(cholqr_pass(P, rows, T1, sharded));
-            RSVD_TRY(cholqr_pass(T1, rows, Q, sharded));
+            RSVD_TRY(cholqr_pass(P, rows, T1, sharded, f32));
+            RSVD_TRY(cholqr_pass(T1, rows, Q, sharded, f32));
         }
-        if (!(sharded && h->world > 1)) {  // the sharded fallback is not implemented: the flag reports it
+        if (output && !dist) {  // the sharded fallback is not implemented: the flag reports it
             RSVD_CK(launch_robust_orth<T>(P, rows, L.l, L.LP, Q, cur_flag, 0x5EEDull + orth_index, s));
         }
         return RSVD_OK;

@@ -82,33 +82,37 @@ __device__ __forceinline__ void rr_pair(int round, int k, int N, int& p, int& q)
     if (k == 0) {
         p = round;
         q = N - 1;
-    } else {
-        p = (round + k) % (N - 1);
-        q = (round - k + (N - 1)) % (N - 1);
+    } else {  // (round + k) mod (N - 1), (round - k) mod (N - 1) without an integer division
+        p = round + k;
+        p -= (p >= N - 1) ? N - 1 : 0;
+        q = round - k + (N - 1);
+        q -= (q >= N - 1) ? N - 1 : 0;
     }
 }
 
-template <int LP>
+// Thread layout: TPP threads per column pair, thread `sub` of a pair owns the CH = LP / TPP
+// contiguous rows sub * CH .. (vector LDS accesses); columns are CS apart.
+template <typename C, int LP>
 struct JacobiShape {
-    static constexpr int TPP = (LP == 32) ? 16 : 8;  // threads per column pair
-    static constexpr int CH = LP / TPP;              // contiguous rows per thread (even)
-    static constexpr int CS = LP + 2;                // column stride: aligned pairs, staggers banks
+    static constexpr int TPP = (LP <= 32 || sizeof(C) == 8) ? 16 : 8;  // threads per column pair
+    static constexpr int CH = LP / TPP;                                // rows per thread (even)
+    static constexpr int CS = LP + 2;                                  // column stride: aligned pairs, staggered banks
+    static constexpr int NTHR = (LP / 2) * TPP;                        // one pair per TPP threads
 };
 
 template <typename C, int LP>
 constexpr size_t svd_lds_bytes() {
-    // X, J (C) -- later reused as the fp64 LP x LP U_w image -- then sig, v, nrm, rank, flags, ptab
-    const size_t xj = (size_t)2 * LP * JacobiShape<LP>::CS * sizeof(C);
+    // X, J (C) -- later reused as the fp64 LP x LP U_w image -- then sig, v, nrm, rank, flags
+    const size_t xj = (size_t)2 * LP * JacobiShape<C, LP>::CS * sizeof(C);
     const size_t ud = (size_t)LP * LP * sizeof(double);
-    return (xj > ud ? xj : ud) + (size_t)3 * LP * sizeof(double) + (size_t)(LP + 4) * sizeof(int) +
-           (size_t)LP * (LP / 2) * sizeof(short2) + 64;
+    return (xj > ud ? xj : ud) + (size_t)3 * LP * sizeof(double) + (size_t)(LP + 4) * sizeof(int) + 64;
 }
 
 template <typename T, typename C, int LP>
-__global__ __launch_bounds__(256) void small_svd_kernel(const double* __restrict__ R, int l,
+__global__ __launch_bounds__((JacobiShape<C, LP>::NTHR)) void small_svd_kernel(const double* __restrict__ R, int l,
                                                         double* __restrict__ Uw, double* __restrict__ Vw,
                                                         T* __restrict__ S, int* __restrict__ info) {
-    typedef JacobiShape<LP> SH;
+    typedef JacobiShape<C, LP> SH;
     typedef typename Two<C>::type C2;
     constexpr int TPP = SH::TPP, CH = SH::CH, CS = SH::CS;
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
@@ -121,7 +125,6 @@ __global__ __launch_bounds__(256) void small_svd_kernel(const double* __restrict
     C* nrm = reinterpret_cast<C*>(v + LP);                  // [LP] squared column norms
     int* rank = reinterpret_cast<int*>(nrm + LP);           // [LP]
     int* flags = rank + LP;                                 // [4]
-    short2* ptab = reinterpret_cast<short2*>(flags + 4);    // [LP-1][LP/2] round-robin pairs
     const int tid = threadIdx.x, nt = blockDim.x;
 
     // X = W (W[i][c] = R[c][i]), J = I
@@ -134,14 +137,8 @@ __global__ __launch_bounds__(256) void small_svd_kernel(const double* __restrict
     const int npairs = N / 2;
     const int pi = tid / TPP, sub = tid % TPP;
     const bool active = pi < npairs;
-    const int i0 = sub * CH;
     const C tol = (C)((double)l * Eps<C>::eps);
     const C tol2 = tol * tol;
-    for (int e = tid; e < (N - 1) * npairs; e += nt) {
-        int p, q;
-        rr_pair(e / npairs, e % npairs, N, p, q);
-        ptab[e] = make_short2((short)p, (short)q);
-    }
     int sweeps = 0;
     C negl = C(0);
     __syncthreads();
@@ -164,10 +161,11 @@ __global__ __launch_bounds__(256) void small_svd_kernel(const double* __restrict
         }
         for (int round = 0; round < N - 1; ++round) {
             if (active) {
-                const short2 pq = ptab[round * npairs + pi];
-                const int p = pq.x, q = pq.y;
+                int p, q;
+                rr_pair(round, pi, N, p, q);
                 // every LDS operand of the round is requested up front: one exposed latency
                 C xp[CH], xq[CH], jp[CH], jq[CH];
+                const int i0 = sub * CH;
 #pragma unroll
                 for (int t = 0; t < CH; t += 2) {
                     const C2 a2 = *reinterpret_cast<const C2*>(X + p * CS + i0 + t);
@@ -182,9 +180,9 @@ __global__ __launch_bounds__(256) void small_svd_kernel(const double* __restrict
                 const C a = nrm[p], b = nrm[q];
                 C g0 = C(0), g1 = C(0);
 #pragma unroll
-                for (int t = 0; t < CH; t += 2) {
-                    g0 += xp[t] * xq[t];
-                    g1 += xp[t + 1] * xq[t + 1];
+                for (int t = 0; t < CH; ++t) {
+                    if (t & 1) g1 += xp[t] * xq[t];
+                    else g0 += xp[t] * xq[t];
                 }
                 const C g = group_sum<TPP>(g0 + g1);
                 const C gg = g * g, ab = a * b;
@@ -265,12 +263,12 @@ __global__ __launch_bounds__(256) void small_svd_kernel(const double* __restrict
         Vw[i * LP + rank[c]] = (double)J[c * CS + i];
     }
     // stash the normalised columns in registers before Ud overwrites X/J
-    constexpr int PER = (LP * LP + 255) / 256;
+    constexpr int PER = (LP * LP + SH::NTHR - 1) / SH::NTHR;
     double ureg[PER];
     int kreg[PER];
 #pragma unroll
     for (int t = 0; t < PER; ++t) {
-        const int e = tid + 256 * t;
+        const int e = tid + SH::NTHR * t;
         const int c = e / LP, i = e % LP;
         kreg[t] = -1;
         ureg[t] = 0.0;
@@ -352,7 +350,7 @@ hipError_t launch_small_svd(const double* R, int l, int LP, double* Uw, double* 
     switch (LP) {
 #define CASE(L)                                                                                              \
     case L:                                                                                                  \
-        hipLaunchKernelGGL((small_svd_kernel<T, C, L>), dim3(1), dim3(256), (svd_lds_bytes<C, L>()), s, R, l, Uw, Vw, \
+        hipLaunchKernelGGL((small_svd_kernel<T, C, L>), dim3(1), dim3(JacobiShape<C, L>::NTHR), (svd_lds_bytes<C, L>()), s, R, l, Uw, Vw, \
                            S, info);                                                                         \
         break;
         CASE(16) CASE(32) CASE(48) CASE(64)

@@ -58,10 +58,13 @@ int gram_tiles(int LP, int cross);
 // compute_f32 else fp64; mode 0: the summed Gram to Gsum (distributed path).  flag[0] += 1 on a
 // bad pivot.  ctr[0..1] are run-cumulative arrival counters (zeroed per run): t0 = ctr[0] after
 // this launch's nb arrivals, t1 = ctr[1] after its tile reducers (gram_tiles(LP, 0)).
+// pred (nullable): the whole launch is skipped unless *pred != 0 (give such a launch counters of its
+// own).  refine (nullable, mode 1): set to 1 when cond_F(R) > 2e4 or a pivot broke down -- the
+// predicate of an optional second CholeskyQR pass.
 template <typename T>
 hipError_t launch_gram_chol(const T* P, int64_t rows, int LP, int nb, double* slabs, double* tiles, unsigned* ctr,
                             unsigned t0, unsigned t1, int mode, int compute_f32, double* Gsum, int l, double* R,
-                            double* Rinv, int* flag, hipStream_t s);
+                            double* Rinv, int* flag, hipStream_t s, const int* pred = nullptr, int* refine = nullptr);
 // Cross-Gram Gout = P^T P2 (LP x LP fp64, zero outside l x l); t1 advances by gram_tiles(LP, 1).
 template <typename T>
 hipError_t launch_cross_gram(const T* P, const T* P2, int64_t rows, int LP, int nb, double* slabs, double* tiles,
@@ -73,7 +76,7 @@ hipError_t launch_chol(const double* G, int l, int LP, int compute_f32, double* 
 // out_colmajor: write Out's first `cols` columns col-major with leading dim ld instead.
 template <typename T>
 hipError_t launch_panel_small(const T* In, int64_t rows, int LP, const double* M, T* Out,
-                              int out_colmajor, int cols, int64_t ld, hipStream_t s);
+                              int out_colmajor, int cols, int64_t ld, hipStream_t s, const int* pred = nullptr);
 
 // ---- jacobi.hip: small SVD of W = R^T (l x l) ---------------------------------------------------
 // One-sided Jacobi (round-robin order) in fp64 on one workgroup.  Outputs U_w, V_w (LP x LP

@@ -31,6 +31,11 @@ namespace rsvd {
 namespace {
 
 constexpr int kGramWaves = 4;
+constexpr int kMaxGramBlocks = 32;
+// A final fp32 panel factored in fp64 is orthonormal to ~u64 cond(R)^2 after ONE pass: below this
+// Frobenius condition estimate (u64 * 2e4^2 ~ 4e-8 < fp32 storage rounding) the second CholeskyQR
+// pass is skipped (gram_kernel `refine`).
+constexpr double kRefineCond = 2e4;  // plan_gram_blocks() cap: the tile reducers keep one load per slab in flight
 
 template <int LP, bool FULL>
 struct Tiles {
@@ -252,8 +257,9 @@ __global__ __launch_bounds__(kWave* kGramWaves) void gram_kernel(
     const T* __restrict__ P, const T* __restrict__ P2, int64_t rows, int64_t chunk, int nb,
     double* __restrict__ slabs, double* __restrict__ tiles, unsigned* __restrict__ ctr, unsigned target0,
     unsigned target1, int mode, double* __restrict__ Gsum, int l, double* __restrict__ Rout,
-    double* __restrict__ Rinv, int* __restrict__ flag) {
+    double* __restrict__ Rinv, int* __restrict__ flag, const int* __restrict__ pred, int* __restrict__ refine) {
     constexpr int G = Tiles<LP, CROSS>::G, NT = Tiles<LP, CROSS>::NT;
+    if (pred && *pred == 0) return;  // predicated pass (private counters: skipping disturbs no other launch)
     typedef Mfma<double> M;
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
     double* red = reinterpret_cast<double*>(smem_raw);  // [kGramWaves][NT][256]
@@ -326,16 +332,20 @@ __global__ __launch_bounds__(kWave* kGramWaves) void gram_kernel(
     if (*ticket == 0) return;
     {
         const int e = threadIdx.x;  // 256 elements per tile, one per thread
+        // every slab load in flight at once (nb <= kMaxGramBlocks): one L2 round trip instead
+        // of nb / 4 dependent ones; then a fixed-order sum (bitwise reproducible)
+        double v[kMaxGramBlocks];
+#pragma unroll
+        for (int sb = 0; sb < kMaxGramBlocks; ++sb)
+            v[sb] = (sb < nb) ? slabs[(size_t)sb * NT * 256 + b * 256 + e] : 0.0;
         double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
-        int sb = 0;
-        for (; sb + 4 <= nb; sb += 4) {  // 4 independent loads in flight, fixed summation order
-            const double v0 = slabs[(size_t)(sb + 0) * NT * 256 + b * 256 + e];
-            const double v1 = slabs[(size_t)(sb + 1) * NT * 256 + b * 256 + e];
-            const double v2 = slabs[(size_t)(sb + 2) * NT * 256 + b * 256 + e];
-            const double v3 = slabs[(size_t)(sb + 3) * NT * 256 + b * 256 + e];
-            s0 += v0; s1 += v1; s2 += v2; s3 += v3;
+#pragma unroll
+        for (int sb = 0; sb < kMaxGramBlocks; sb += 4) {
+            s0 += v[sb];
+            s1 += v[sb + 1];
+            s2 += v[sb + 2];
+            s3 += v[sb + 3];
         }
-        for (; sb < nb; ++sb) s0 += slabs[(size_t)sb * NT * 256 + b * 256 + e];
         tiles[b * 256 + e] = (s0 + s1) + (s2 + s3);
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -384,6 +394,38 @@ __global__ __launch_bounds__(kWave* kGramWaves) void gram_kernel(
     const bool bad = tile_cholesky_inverse<C, LP>(Gs, prow, d0, Rout ? Rs : nullptr, RIs, l);
     write_factor<LP>(Rs, RIs, l, Rout, Rinv);
     if (threadIdx.x == 0 && bad) atomicAdd(flag, 1);
+    if (refine) {
+        // cond_F(R) = |R|_F |R^-1|_F >= cond_2(R): one pass left Q orthonormal to ~u cond^2, so a
+        // second pass is requested when that exceeds what the panel's storage precision resolves
+        double a = 0.0, c = 0.0;
+        for (int e = threadIdx.x; e < LP * LP; e += blockDim.x) {
+            const int i = e / LP, j = e % LP;
+            if (i < l && j < l) {
+                a += Rs[e] * Rs[e];
+                c += RIs[e] * RIs[e];
+            }
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            a += __shfl_xor(a, o);
+            c += __shfl_xor(c, o);
+        }
+        double* part = reinterpret_cast<double*>(prow);
+        if (lane == 0) {
+            part[w] = a;
+            part[kGramWaves + w] = c;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            double sa = 0.0, sc = 0.0;
+            for (int t = 0; t < kGramWaves; ++t) {
+                sa += part[t];
+                sc += part[kGramWaves + t];
+            }
+            const double cond = sqrt(sa * sc);
+            *refine = (bad || !(cond <= kRefineCond)) ? 1 : 0;
+        }
+    }
 }
 
 // Factor an already-summed Gram (distributed path: after the all-reduce).
@@ -412,7 +454,9 @@ __global__ __launch_bounds__(256) void chol_kernel(const double* __restrict__ Gi
 template <typename T, int LP>
 __global__ __launch_bounds__(256) void panel_small_kernel(const T* __restrict__ In, int64_t rows,
                                                           const double* __restrict__ Mg, T* __restrict__ Out,
-                                                          int out_colmajor, int cols, int64_t ld) {
+                                                          int out_colmajor, int cols, int64_t ld,
+                                                          const int* __restrict__ pred) {
+    if (pred && *pred == 0) return;
     typedef Mfma<double> M;
     constexpr int G = LP / 16;
     constexpr int RPB = 64;  // rows per block
@@ -474,12 +518,12 @@ size_t gram_lds_bytes() {
 template <typename T, typename C, int LP, bool CROSS>
 hipError_t gram_launch(const T* P, const T* P2, int64_t rows, int nb, double* slabs, double* tiles, unsigned* ctr,
                        unsigned t0, unsigned t1, int mode, double* Gsum, int l, double* R, double* Rinv, int* flag,
-                       hipStream_t s) {
+                       hipStream_t s, const int* pred = nullptr, int* refine = nullptr) {
     const int64_t chunk = (rows + nb - 1) / nb;
     const int NT = Tiles<LP, CROSS>::NT;
     const int grid = nb > NT ? nb : NT;
     hipLaunchKernelGGL((gram_kernel<T, C, LP, CROSS>), dim3(grid), dim3(kWave * kGramWaves), (gram_lds_bytes<LP, CROSS>()),
-                       s, P, P2, rows, chunk, nb, slabs, tiles, ctr, t0, t1, mode, Gsum, l, R, Rinv, flag);
+                       s, P, P2, rows, chunk, nb, slabs, tiles, ctr, t0, t1, mode, Gsum, l, R, Rinv, flag, pred, refine);
     return hipGetLastError();
 }
 
@@ -487,7 +531,7 @@ hipError_t gram_launch(const T* P, const T* P2, int64_t rows, int nb, double* sl
 
 int plan_gram_blocks(int64_t rows) {
     int64_t blocks = (rows + 127) / 128;  // >= 128 rows per workgroup
-    if (blocks > 32) blocks = 32;
+    if (blocks > kMaxGramBlocks) blocks = kMaxGramBlocks;
     if (blocks < 1) blocks = 1;
     return (int)blocks;
 }
@@ -500,14 +544,14 @@ int gram_tiles(int LP, int cross) {
 template <typename T>
 hipError_t launch_gram_chol(const T* P, int64_t rows, int LP, int nb, double* slabs, double* tiles, unsigned* ctr,
                             unsigned t0, unsigned t1, int mode, int compute_f32, double* Gsum, int l, double* R,
-                            double* Rinv, int* flag, hipStream_t s) {
+                            double* Rinv, int* flag, hipStream_t s, const int* pred, int* refine) {
     switch (LP) {
 #define CASE(L)                                                                                                   \
     case L:                                                                                                       \
         return compute_f32 ? gram_launch<T, float, L, false>(P, nullptr, rows, nb, slabs, tiles, ctr, t0, t1, mode, \
-                                                              Gsum, l, R, Rinv, flag, s)                           \
+                                                              Gsum, l, R, Rinv, flag, s, pred, refine)             \
                            : gram_launch<T, double, L, false>(P, nullptr, rows, nb, slabs, tiles, ctr, t0, t1, mode, \
-                                                               Gsum, l, R, Rinv, flag, s);
+                                                               Gsum, l, R, Rinv, flag, s, pred, refine);
         CASE(16) CASE(32) CASE(48) CASE(64)
 #undef CASE
         default: return hipErrorInvalidValue;
@@ -548,14 +592,14 @@ hipError_t launch_chol(const double* G, int l, int LP, int compute_f32, double* 
 
 template <typename T>
 hipError_t launch_panel_small(const T* In, int64_t rows, int LP, const double* Mat, T* Out, int out_colmajor,
-                              int cols, int64_t ld, hipStream_t s) {
+                              int cols, int64_t ld, hipStream_t s, const int* pred) {
     const int blocks = (int)((rows + 63) / 64);
     const size_t lds = (size_t)(LP * LP + std::max(64 * (LP + 1), LP * 65)) * sizeof(double);
     switch (LP) {
 #define CASE(L)                                                                                          \
     case L:                                                                                              \
         hipLaunchKernelGGL((panel_small_kernel<T, L>), dim3(blocks), dim3(256), lds, s, In, rows, Mat, Out, \
-                           out_colmajor, cols, ld);                                                      \
+                           out_colmajor, cols, ld, pred);                                                \
         break;
         CASE(16) CASE(32) CASE(48) CASE(64)
 #undef CASE
@@ -566,11 +610,12 @@ hipError_t launch_panel_small(const T* In, int64_t rows, int LP, const double* M
 
 #define RSVD_INST(T)                                                                                             \
     template hipError_t launch_gram_chol<T>(const T*, int64_t, int, int, double*, double*, unsigned*, unsigned,    \
-                                            unsigned, int, int, double*, int, double*, double*, int*, hipStream_t); \
+                                            unsigned, int, int, double*, int, double*, double*, int*, hipStream_t, \
+                                            const int*, int*);                                                    \
     template hipError_t launch_cross_gram<T>(const T*, const T*, int64_t, int, int, double*, double*, unsigned*,   \
                                              unsigned, unsigned, double*, int, int*, hipStream_t);               \
     template hipError_t launch_panel_small<T>(const T*, int64_t, int, const double*, T*, int, int, int64_t,       \
-                                              hipStream_t);
+                                              hipStream_t, const int*);
 RSVD_INST(float)
 RSVD_INST(double)
 #undef RSVD_INST

@@ -155,7 +155,7 @@ static void bench_chol() {
 }
 
 static void bench_jac() {
-    for (int LP : {128, 256, 512}) {
+    for (int LP : {64, 128, 256, 512}) {
         // R: upper triangular with a 0.97^i graded diagonal + noise (like a QR-preconditioned B^T)
         std::vector<double> hR((size_t)LP * LP, 0.0);
         std::mt19937 g(5);
