@@ -80,6 +80,9 @@ inline void check(int status, const char* what) {
 }
 
 // rSVD(A, U, S, V, l, method) with q power iterations (the reference hard-codes q = 2).
+// Method::Power returns what the reference's rSVD returns for it (src/rSVD.cpp:106-113 with
+// SVD_class.hpp:183-219): U m x l, S l and V = the n x n V_ of SVD<Power> (v_i^T in row i, identity
+// rows beyond), each cut to the first `kept` columns when the power method stops early.
 template <class Mat, class Vec>
 void rsvd(const Mat& A, Mat& U, Vec& S, Mat& V, int l, Method method, int q = 2) {
     const int64_t m = A.rows(), n = A.cols();
@@ -91,6 +94,32 @@ void rsvd(const Mat& A, Mat& U, Vec& S, Mat& V, int l, Method method, int q = 2)
     check(rsvd_run_host_f64(c.handle(), m, n, A.data(), m, l, q, static_cast<int32_t>(method), nullptr,
                             c.next_seed(), U.data(), S.data(), V.data()),
           "rSVD");
+    if (method != Method::Power) return;
+    rsvd_info_t info{};
+    check(rsvd_get_info(c.handle(), &info), "rSVD");
+    const int64_t kept = info.power_kept;
+    Mat Vf;  // V_ (n x n): identity, v_i^T in row i < kept
+    Vf.resize(n, n);
+    for (int64_t e = 0; e < n * n; ++e) Vf.data()[e] = 0.0;
+    for (int64_t i = 0; i < n; ++i) Vf.data()[i + i * n] = 1.0;
+    for (int64_t i = 0; i < kept; ++i)
+        for (int64_t t = 0; t < n; ++t) Vf.data()[i + t * n] = V.data()[t + i * n];
+    if (kept >= d) {
+        V = Vf;
+        return;
+    }
+    const int64_t kk = kept > 0 ? kept : 1;  // SVD_class.hpp:199-206: zero 1-column result at i == 0
+    Mat U2, V2;
+    Vec S2;
+    U2.resize(m, kk);
+    V2.resize(n, kk);
+    S2.resize(kk);
+    for (int64_t e = 0; e < m * kk; ++e) U2.data()[e] = kept ? U.data()[e] : 0.0;
+    for (int64_t e = 0; e < n * kk; ++e) V2.data()[e] = kept ? Vf.data()[e] : 0.0;
+    for (int64_t i = 0; i < kk; ++i) S2.data()[i] = kept ? S.data()[i] : 0.0;
+    U = U2;
+    V = V2;
+    S = S2;
 }
 
 // intermediate_step(A, Q, Omega, l, q): Q (m x l) orthonormal basis of range((A A^T)^q A Omega).

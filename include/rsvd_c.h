@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define RSVD_ABI_VERSION 2
+#define RSVD_ABI_VERSION 3
 
 typedef enum {
     RSVD_OK = 0,
@@ -82,6 +82,7 @@ typedef struct {
     int32_t cholqr_fallbacks;  /* panels re-orthonormalised by the CGS2 fallback                 */
     int32_t jacobi_sweeps;     /* sweeps of the small SVD                                      */
     int32_t splits_nn, splits_tn; /* K splits chosen for the projections                         */
+    int32_t power_kept;        /* SVDMethod::Power: triplets found before sigma < 1e-12 (else 0)  */
 } rsvd_info_t;
 
 typedef struct rsvd_handle_s *rsvd_handle_t;
@@ -124,7 +125,11 @@ int rsvd_set_workspace(rsvd_handle_t h, void *ptr, size_t bytes);
 /* ---- device-pointer entry points (asynchronous on the handle stream) ---------------------- */
 
 /* rSVD: U (m x d, ldu), S (d), V (n x d, ldv), d = min(l, n); element type = desc->dtype (fp32
- * for BF16 / FP8_E4M3).  omega: optional n x l column-major (ld = ldo) sketch in that element
+ * for BF16 / FP8_E4M3).  method POWER (src/rSVD.cpp:106-113): the reference's power method with
+ * deflation on B = Q^T A (start vectors: Philox stream (seed ^ 0x504F574552) + i, the reference's
+ * s(n) iterations); V's columns are the right singular vectors (the reference returns them as the
+ * rows of an n x n V_ -- include/SVD_class.hpp rebuilds that layout); triplets past an early stop
+ * (sigma < 1e-12) are zero and rsvd_get_info reports how many were kept.  omega: optional n x l column-major (ld = ldo) sketch in that element
  * type (rounded to bf16 / e4m3 for the low-precision types); NULL => Philox(desc->seed).
  * l <= 512. */
 int rsvd_run(rsvd_handle_t h, const rsvd_desc_t *desc, const void *A, const void *omega, int64_t ldo,

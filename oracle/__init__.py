@@ -66,6 +66,8 @@ def lib(opt: str = "O3"):
     L.orc_intermediate_step.argtypes = [i64, i64, dp, i64, dp, i64, i64, i64, dp, i64]
     L.orc_rsvd.argtypes = [i64, i64, dp, i64, i64, i64, dp, i64, i32, dp, dp, dp]
     L.orc_rsvd.restype = i32
+    L.orc_rsvd_power.argtypes = [i64, i64, dp, i64, i64, i64, dp, i64, u64, dp, dp, dp]
+    L.orc_rsvd_power.restype = i64
     if opt == "O3":
         _LIB = L
     return L
@@ -191,6 +193,25 @@ def rsvd(A, l: int, q: int = 2, Omega=None, seed: int = 0, method: int = SVD_JAC
     if rc != 0:
         raise ValueError("Unsupported SVD method")
     return U, S, V
+
+
+def rsvd_power(A, l: int, q: int = 2, Omega=None, seed: int = 0, pm_seed: int = 0):
+    """rSVD(A, U, S, V, l, SVDMethod::Power) (src/rSVD.cpp:106-113): U (m x l), S (l), V (n x n,
+    v_i^T in rows i < l, identity rows beyond -- SVD_class.hpp:82-83, 213-214), cut to the
+    triplets kept on an early stop as conservativeResize does (:198-208).  Start vectors of the
+    power method: Philox(pm_seed + i)."""
+    A = _f(A)
+    m, n = A.shape
+    Om = _f(Omega) if Omega is not None else generate_omega(n, l, seed)
+    U = np.zeros((m, l), order="F")
+    S = np.zeros(l)
+    V = np.zeros((n, n), order="F")
+    k = lib().orc_rsvd_power(m, n, _p(A), m, l, q, _p(Om), n, pm_seed, _p(U), _p(S), _p(V))
+    if k == l:
+        return U, S, V
+    if k == 0:
+        return np.zeros((m, 1)), np.zeros(1), np.zeros((n, 1))
+    return U[:, :k].copy(order="F"), S[:k].copy(), V[:, :k].copy(order="F")
 
 
 def read_matrix_market(path: str) -> np.ndarray:

@@ -523,3 +523,20 @@ int orc_rsvd(int64_t m, int64_t n, const double *A, int64_t lda, int64_t l, int6
     free(Ut); free(B); free(Q);
     return 0;
 }
+
+/* rSVD with SVDMethod::Power (src/rSVD.cpp:106-113): SVD<Power> svd(B) on B = Q^T A (l x n), start
+ * vectors Philox(pm_seed + i); Utilde = U_ (l x l), V = V_ (n x n, v_i in rows), U = Q Utilde.
+ * U: m x l, S: l, V: n x n (all written in full, as before any conservativeResize); returns the
+ * number of triplets kept (the caller cuts to it as SVD_class.hpp:198-208 does). */
+int64_t orc_rsvd_power(int64_t m, int64_t n, const double *A, int64_t lda, int64_t l, int64_t q,
+                       const double *Omega, int64_t ldo, uint64_t pm_seed, double *U, double *S, double *V) {
+    double *Q = (double *)malloc(sizeof(double) * (size_t)(m * l));
+    orc_intermediate_step(m, n, A, lda, Omega, ldo, l, q, Q, m);
+    double *B = (double *)malloc(sizeof(double) * (size_t)(l * n));
+    orc_gemm('T', 'N', l, n, m, Q, m, A, lda, 0.0, B, l); /* B = Q^T A (:89) */
+    double *Ut = (double *)malloc(sizeof(double) * (size_t)(l * l));
+    const int64_t kept = orc_power_svd(l, n, B, l, 0, pm_seed, Ut, S, V);
+    orc_gemm('N', 'N', m, l, l, Q, m, Ut, l, 0.0, U, m); /* U = Q * Utilde (:128) */
+    free(Ut); free(B); free(Q);
+    return kept;
+}

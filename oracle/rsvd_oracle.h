@@ -84,6 +84,10 @@ void orc_intermediate_step(int64_t m, int64_t n, const double *A, int64_t lda,
  * U (m x d), S (d), V (n x d), ld = rows.  Returns 0, or -1 for an unsupported method. */
 int orc_rsvd(int64_t m, int64_t n, const double *A, int64_t lda, int64_t l, int64_t q,
              const double *Omega, int64_t ldo, int method, double *U, double *S, double *V);
+/* rSVD with SVDMethod::Power (src/rSVD.cpp:106-113); start vectors Philox(pm_seed + i).
+ * U m x l, S l, V n x n (v_i in rows); returns the triplets kept. */
+int64_t orc_rsvd_power(int64_t m, int64_t n, const double *A, int64_t lda, int64_t l, int64_t q,
+                       const double *Omega, int64_t ldo, uint64_t pm_seed, double *U, double *S, double *V);
 
 #ifdef __cplusplus
 }

@@ -53,7 +53,7 @@ class Desc(ctypes.Structure):
 class Info(ctypes.Structure):
     _fields_ = [
         ("cholqr_fallbacks", ctypes.c_int32), ("jacobi_sweeps", ctypes.c_int32),
-        ("splits_nn", ctypes.c_int32), ("splits_tn", ctypes.c_int32),
+        ("splits_nn", ctypes.c_int32), ("splits_tn", ctypes.c_int32), ("power_kept", ctypes.c_int32),
     ]
 
 

@@ -355,11 +355,29 @@ def _is_torch(x) -> bool:
 
 # ---- reference-named free functions ------------------------------------------------------------
 def rSVD(A, l: int, method: SVDMethod = SVDMethod.Jacobi, q: int = 2, omega=None, seed: int = 0):
-    """rSVD (src/rSVD.cpp:72-133). Returns (U, S, V); q defaults to the reference's hard-coded 2."""
+    """rSVD (src/rSVD.cpp:72-133). Returns (U, S, V); q defaults to the reference's hard-coded 2.
+
+    SVDMethod.Power returns the reference's layouts (src/rSVD.cpp:106-113): U m x l, S l and V the
+    n x n V_ of SVD<Power> (v_i in row i, identity rows beyond), cut to the triplets kept on an
+    early stop (SVD_class.hpp:198-208).  Engine.rsvd returns V as columns instead."""
     eng = default_engine()
     if _is_torch(A):
-        return eng.rsvd(A, l, q=q, method=method, omega=omega, seed=seed)
-    return eng.rsvd_host(A, l, q=q, method=method, omega=omega, seed=seed)
+        U, S, V = eng.rsvd(A, l, q=q, method=method, omega=omega, seed=seed)
+    else:
+        U, S, V = eng.rsvd_host(A, l, q=q, method=method, omega=omega, seed=seed)
+    if int(method) != SVDMethod.Power:
+        return U, S, V
+    kept = eng.info()["power_kept"]
+    xp = _torch() if _is_torch(A) else np
+    n = V.shape[0]
+    Vf = xp.eye(n, dtype=V.dtype, **({"device": V.device} if _is_torch(A) else {}))
+    Vf[:kept, :] = V[:, :kept].T
+    if kept >= S.shape[0]:
+        return U, S, Vf
+    if kept == 0:
+        z = xp.zeros
+        return z((U.shape[0], 1), dtype=U.dtype), z(1, dtype=S.dtype), z((n, 1), dtype=V.dtype)
+    return U[:, :kept], S[:kept], Vf[:, :kept]
 
 
 def intermediate_step(A, Omega, l: int, q: int):

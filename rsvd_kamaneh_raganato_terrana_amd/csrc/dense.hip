@@ -254,7 +254,8 @@ template <typename T, bool LDSB>
 __global__ __launch_bounds__(kPowThreads) void power_svd_kernel(const T* __restrict__ P, int64_t m, int n, int LP,
                                                                 double* __restrict__ Bg, int dim, uint64_t seed,
                                                                 int iters, T* __restrict__ Up, double* __restrict__ Vr,
-                                                                double* __restrict__ S, int* __restrict__ kept) {
+                                                                double* __restrict__ S, int* __restrict__ kept,
+                                                                const double* __restrict__ x0, int rsvd_mode) {
     extern __shared__ double lds[];
     double* x = lds;            // LP
     double* y = x + LP;         // LP
@@ -273,7 +274,7 @@ __global__ __launch_bounds__(kPowThreads) void power_svd_kernel(const T* __restr
         // x0 = N(0,1) Philox stream (seed + i), normalised (src/PM.cpp:15-22)
         double sq = 0.0;
         for (int c = tid; c < n; c += kPowThreads) {
-            const double g = gauss_elem((uint64_t)c, seed + (uint64_t)i);
+            const double g = x0 ? x0[(int64_t)i * LP + c] : gauss_elem((uint64_t)c, seed + (uint64_t)i);
             x[c] = g;
             sq += g * g;
         }
@@ -299,7 +300,8 @@ __global__ __launch_bounds__(kPowThreads) void power_svd_kernel(const T* __restr
             __syncthreads();
             for (int j = w; j < i; j += kPowThreads / 64) {
                 double d = 0.0;
-                for (int c = lane; c < n; c += 64) d += Vr[(int64_t)j * LP + c] * x[c];
+                for (int c = lane; c < n; c += 64)
+                    d += Vr[rsvd_mode ? (int64_t)c * LP + j : (int64_t)j * LP + c] * x[c];
 #pragma unroll
                 for (int o = 32; o > 0; o >>= 1) d += __shfl_xor(d, o);
                 if (lane == 0) coef[j] = S[j] * d;
@@ -333,11 +335,53 @@ __global__ __launch_bounds__(kPowThreads) void power_svd_kernel(const T* __restr
             const int r = e / n, c = e - r * n;
             B[(int64_t)r * LP + c] -= f * (x[r] * x[c]);
         }
-        for (int c = tid; c < n; c += kPowThreads) Vr[(int64_t)i * LP + c] = x[c];  // V_.row(i) = v (:214)
+        for (int c = tid; c < n; c += kPowThreads)  // V_.row(i) = v (:214); rsvd mode: column i
+            Vr[rsvd_mode ? (int64_t)c * LP + i : (int64_t)i * LP + c] = x[c];
         if (tid == 0) S[i] = sigma;
         __syncthreads();
     }
+    if (rsvd_mode) {  // triplets past an early stop are zero (the reference drops them)
+        for (int i = k; i < dim; ++i) {
+            for (int64_t r = tid; r < m; r += kPowThreads) Up[r * LP + i] = T(0);
+            for (int c = tid; c < n; c += kPowThreads) Vr[(int64_t)c * LP + i] = 0.0;
+            if (tid == 0) S[i] = 0.0;
+        }
+    }
     if (tid == 0) *kept = k;
+}
+
+// rSVD with SVDMethod::Power (src/rSVD.cpp:106-113) in the coordinates of Q_B: B = R^T Q_B^T with
+// R = Q_B^T B^T (LP x LP, R[i][j] = q_i . b_j).  The power iteration x <- B^T B x of the reference
+// stays in span(Q_B) after its first product, so with x = Q_B y it is y <- (R R^T) y, sigma =
+// |R^T y|, u = R^T y / sigma, and the deflation of B is R^T -= sigma u y^T.  This kernel writes
+// P = R^T (row-major, the power kernel's "A"), Bpm = R R^T, and the start vectors
+// X0s[i] = Q_B^T x0_i from Y0 = Q_B^T X0 (Y0[c][i] = q_c . x0_i).  One workgroup.
+__global__ __launch_bounds__(1024) void power_prep_kernel(const double* __restrict__ R, const double* __restrict__ Y0,
+                                                          int l, int LP, double* __restrict__ P,
+                                                          double* __restrict__ X0s, double* __restrict__ Bpm) {
+    const int tid = threadIdx.x;
+    for (int e = tid; e < LP * LP; e += 1024) {
+        const int i = e / LP, j = e - i * LP;
+        const bool in = i < l && j < l;
+        P[e] = in ? R[(int64_t)j * LP + i] : 0.0;
+        X0s[e] = in ? Y0[(int64_t)j * LP + i] : 0.0;
+        double acc = 0.0;
+        if (in)
+            for (int c = 0; c < l; ++c) acc += R[(int64_t)i * LP + c] * R[(int64_t)j * LP + c];
+        Bpm[e] = acc;
+    }
+}
+
+// X0 (rows x LP, row-major): X0[r][i] = N(0,1) Philox element r of stream (seed + i), i < l --
+// the reference's random start vector of the i-th power-method triplet (src/PM.cpp:15-21).
+template <typename T>
+__global__ void power_start_kernel(T* __restrict__ X0, int64_t rows, int l, int LP, uint64_t seed) {
+    const int64_t total = rows * LP;
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = e / LP;
+        const int i = (int)(e - r * LP);
+        X0[e] = (i < l) ? (T)gauss_elem((uint64_t)r, seed + (uint64_t)i) : T(0);
+    }
 }
 
 inline int grid_of(int64_t work) {
@@ -403,25 +447,41 @@ int power_iterations(int64_t n) {
 }
 
 hipError_t launch_power_svd(const double* P, int64_t m, int n, int LP, double* B, int dim, uint64_t seed, int iters,
-                            double* Up, double* Vr, double* S, int* kept, hipStream_t s) {
+                            double* Up, double* Vr, double* S, int* kept, hipStream_t s, const double* x0,
+                            int rsvd_mode) {
     if (n > LP || LP > 512 || dim > n) return hipErrorInvalidValue;
     const size_t small = (size_t)(3 * LP + 32) * sizeof(double);
     if (LP <= 128) {
         const size_t lds = small + (size_t)LP * LP * sizeof(double);
         hipLaunchKernelGGL((power_svd_kernel<double, true>), dim3(1), dim3(kPowThreads), lds, s, P, m, n, LP, B, dim,
-                           seed, iters, Up, Vr, S, kept);
+                           seed, iters, Up, Vr, S, kept, x0, rsvd_mode);
     } else {
         hipLaunchKernelGGL((power_svd_kernel<double, false>), dim3(1), dim3(kPowThreads), small, s, P, m, n, LP, B,
-                           dim, seed, iters, Up, Vr, S, kept);
+                           dim, seed, iters, Up, Vr, S, kept, x0, rsvd_mode);
     }
     return hipGetLastError();
 }
+
+hipError_t launch_power_prep(const double* R, const double* Y0, int l, int LP, double* P, double* X0s, double* Bpm,
+                             hipStream_t s) {
+    hipLaunchKernelGGL(power_prep_kernel, dim3(1), dim3(1024), 0, s, R, Y0, l, LP, P, X0s, Bpm);
+    return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_power_start(T* X0, int64_t rows, int l, int LP, uint64_t seed, hipStream_t s) {
+    hipLaunchKernelGGL((power_start_kernel<T>), dim3(grid_of(rows * LP)), dim3(256), 0, s, X0, rows, l, LP, seed);
+    return hipGetLastError();
+}
+
+uint64_t power_seed(uint64_t seed) { return seed ^ 0x504F574552ull; }
 
 #define RSVD_INST(T)                                                                                         \
     template hipError_t launch_transpose_to_panel<T>(const T*, int64_t, int64_t, int64_t, int, T*, hipStream_t); \
     template hipError_t launch_upper_to_colmajor<T>(const double*, int, int, int, T*, int64_t, hipStream_t); \
     template hipError_t launch_unit_columns<T>(T*, int, int, int, hipStream_t);                               \
     template hipError_t launch_det_sign<T>(T*, int, int, double*, hipStream_t);                               \
+    template hipError_t launch_power_start<T>(T*, int64_t, int, int, uint64_t, hipStream_t);                   \
     template hipError_t launch_trsm_rows<T>(const T*, int64_t, int, int, const double*, T*, const int*, hipStream_t); \
     template hipError_t launch_qr_signs<T>(const T*, int64_t, int64_t, int, T*, int, hipStream_t);
 RSVD_INST(float)

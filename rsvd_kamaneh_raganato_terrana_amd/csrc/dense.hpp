@@ -35,7 +35,19 @@ int power_iterations(int64_t n);
 // SVD<Power> on A (m x LP fp64 panel, n used columns) with B = A^T A (LP x LP, overwritten):
 // u_i -> column i of Up (m x LP panel), v_i -> row i of Vr (LP x LP), S[i]; *kept = triplets
 // found (< dim when sigma < 1e-12 stops it).  One workgroup.  n <= LP <= 512.
+// x0 (nullable): start vectors as rows of an LP x LP matrix instead of Philox(seed + i).
+// rsvd_mode: v_i goes to COLUMN i of Vr, and triplets past an early stop are written as zeros.
 hipError_t launch_power_svd(const double* P, int64_t m, int n, int LP, double* B, int dim, uint64_t seed, int iters,
-                            double* Up, double* Vr, double* S, int* kept, hipStream_t s);
+                            double* Up, double* Vr, double* S, int* kept, hipStream_t s, const double* x0 = nullptr,
+                            int rsvd_mode = 0);
+// rSVD(..., SVDMethod::Power) in Q_B coordinates (dense.hip power_prep_kernel): from R = Q_B^T B^T
+// and Y0 = Q_B^T X0 build P = R^T, the start-vector rows X0s and Bpm = R R^T (all LP x LP fp64).
+hipError_t launch_power_prep(const double* R, const double* Y0, int l, int LP, double* P, double* X0s, double* Bpm,
+                             hipStream_t s);
+// X0 (rows x LP): column i = Philox stream (seed + i), the reference's random start vectors.
+template <typename T>
+hipError_t launch_power_start(T* X0, int64_t rows, int l, int LP, uint64_t seed, hipStream_t s);
+// The Philox key of the power method's start vectors inside rSVD (documented in rsvd_c.h).
+uint64_t power_seed(uint64_t seed);
 
 }  // namespace rsvd

@@ -148,7 +148,7 @@ bool ok_dtype(int dt) { return dt == RSVD_F64 || dt == RSVD_F32; }
 int prepare(rsvd_handle_t h, size_t bytes) {
     RSVD_CK(hipSetDevice(h->device));
     RSVD_TRY(ensure_ws(h, bytes));
-    RSVD_CK(hipMemsetAsync(h->dflags, 0, 16 * sizeof(int), h->stream));
+    RSVD_CK(hipMemsetAsync(h->dflags, 0, kFlagWords * sizeof(int), h->stream));
     return RSVD_OK;
 }
 
@@ -223,7 +223,7 @@ int svd_power(rsvd_handle_t h, int64_t m, int64_t n, const double* A, int64_t ld
     RSVD_CK(launch_colmajor_to_panel<double>(A, lda, m, (int)n, L.LP, E.P, s));
     RSVD_CK(launch_gram_wide<double>(E.P, nullptr, m, L.LP, L.gp, E.gslab, E.G, nullptr, s));  // B = A^T A (:193)
     RSVD_CK(hipMemsetAsync(E.Q, 0, sizeof(double) * m * L.LP, s));
-    int* dk = h->dflags + 8;
+    int* dk = h->dflags + 16;
     RSVD_CK(launch_power_svd(E.P, m, (int)n, L.LP, E.G, dim, seed, power_iterations(n), E.Q, E.Vw, E.Sd, dk, s));
     int k = 0;
     RSVD_CK(hipMemcpyAsync(&k, dk, sizeof(int), hipMemcpyDeviceToHost, s));

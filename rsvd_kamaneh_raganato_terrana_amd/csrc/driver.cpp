@@ -27,6 +27,7 @@
 #include "../../include/rsvd_c.h"
 #include "handle.hpp"
 #include "kernels.hpp"
+#include "dense.hpp"
 #include "wide.hpp"
 
 using namespace rsvd;
@@ -71,7 +72,7 @@ int check_desc_msg(const rsvd_desc_t* d, const char** err) {
     }
     if (d->dtype < RSVD_F64 || d->dtype > RSVD_FP8_E4M3) { *err = "unsupported dtype"; return RSVD_ERR_UNSUPPORTED; }
     if (d->qr_mode < RSVD_QR_AUTO || d->qr_mode > RSVD_QR_CHOLQR2) { *err = "bad qr_mode"; return RSVD_ERR_INVALID_ARG; }
-    if (d->method != RSVD_SVD_JACOBI && d->method != RSVD_SVD_PARALLEL_JACOBI) {
+    if (d->method != RSVD_SVD_JACOBI && d->method != RSVD_SVD_PARALLEL_JACOBI && d->method != RSVD_SVD_POWER) {
         *err = "Unsupported SVD method";  // src/rSVD.cpp:123 wording
         return RSVD_ERR_UNSUPPORTED;
     }
@@ -264,12 +265,31 @@ struct Engine {
         return RSVD_OK;
     }
 
+    // SVDMethod::Power (src/rSVD.cpp:106-113): the reference's power method on B = Q^T A, run in
+    // the coordinates of Q_B (dense.hip power_prep_kernel): start vectors Philox(power_seed(seed)
+    // + i) projected on span(Q_B), s(n) iterations (src/PM.cpp:25-28), U = Q Utilde, V = Q_B Y.
+    int power_stage(const rsvd_desc_t* d, void* U, int64_t ldu, T* S, void* V, int64_t ldv) {
+        const int64_t q2 = (int64_t)L.LP * L.LP;
+        double* sm = R1;  // R1 .. sm + 7 q2: the small-matrix area
+        double *Y0 = Gsum, *Pp = R2, *X0s = Rinv, *Bpm = sm + 6 * q2, *Up = Uw, *Vc = Vw, *Sd = sm + 7 * q2;
+        RSVD_CK(launch_power_start<T>(T1, L.n, L.l, L.LP, power_seed(d->seed), s));
+        RSVD_TRY(cross_gram(Xn, T1, L.n, Y0));  // Y0 = Q_B^T X0
+        RSVD_CK(launch_power_prep(R1, Y0, L.l, L.LP, Pp, X0s, Bpm, s));
+        RSVD_CK(launch_power_svd(Pp, L.l, L.l, L.LP, Bpm, L.l, 0, power_iterations(L.n), Up, Vc, Sd, h->dflags + 16,
+                                 s, X0s, 1));
+        RSVD_CK(launch_convert_scale<T>(Sd, S, L.l, 1.0, s));
+        RSVD_CK(launch_panel_small<T>(Qm, L.m, L.LP, Up, reinterpret_cast<T*>(U), 1, L.l, ldu, s));
+        RSVD_CK(launch_panel_small<T>(Xn, L.n, L.LP, Vc, reinterpret_cast<T*>(V), 1, L.l, ldv, s));
+        return RSVD_OK;
+    }
+
     int run(const rsvd_desc_t* d, const T* A, void* U, int64_t ldu, T* S, void* V, int64_t ldv) {
         RSVD_TRY(range_finder(A, d->lda, d->q));
         // Stage B: B^T = A^T Q, QR-preconditioned as in SVD_class.hpp:116-123.
         RSVD_TRY(proj_tn(A, d->lda, Qm, Zn));
         RSVD_TRY(orth(Zn, L.n, Xn, false, 2));  // Xn = Q_B
         RSVD_TRY(cross_gram(Xn, Zn, L.n, R1));    // R = Q_B^T B^T exactly (fp64), W = R^T
+        if (d->method == RSVD_SVD_POWER) return power_stage(d, U, ldu, S, V, ldv);
         RSVD_CK(launch_small_svd<T>(R1, L.l, L.LP, Uw, Vw, S, h->dflags + 1, s));
         const int dcols = L.l;  // d = min(l, n) = l (l <= n enforced)
         RSVD_CK(launch_panel_small<T>(Qm, L.m, L.LP, Uw, reinterpret_cast<T*>(U), 1, dcols, ldu, s));
@@ -283,7 +303,7 @@ int run_typed(rsvd_handle_t h, const rsvd_desc_t* d, const void* A, const void* 
               int64_t ldu, void* S, void* V, int64_t ldv, void* Qout, int64_t ldq) {
     Layout<T> L(d->m, d->n, d->l);
     RSVD_TRY(ensure_ws(h, L.total));
-    RSVD_CK(hipMemsetAsync(h->dflags, 0, 16 * sizeof(int), h->stream));
+    RSVD_CK(hipMemsetAsync(h->dflags, 0, kFlagWords * sizeof(int), h->stream));
     RSVD_CK(hipMemsetAsync(h->ws + L.off_ctr, 0, 64 * sizeof(unsigned), h->stream));
     h->info.splits_nn = L.pnn.splits;
     h->info.splits_tn = L.ptn.splits;
@@ -346,7 +366,7 @@ int rsvd_create(int device, rsvd_handle_t* out) {
     rsvd_handle_t h = new rsvd_handle_s();
     h->device = device;
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipMalloc(&h->dflags, 16 * sizeof(int)) != hipSuccess) {
+        hipMalloc(&h->dflags, kFlagWords * sizeof(int)) != hipSuccess) {
         delete h;
         return RSVD_ERR_HIP;
     }
@@ -383,8 +403,8 @@ const char* rsvd_last_error(rsvd_handle_t h) { return h ? h->err.c_str() : "null
 int rsvd_get_info(rsvd_handle_t h, rsvd_info_t* info) {
     if (!h || !info) return RSVD_ERR_INVALID_ARG;
     RSVD_TRY(set_device(h));
-    int flags[16] = {0};
-    RSVD_CK(hipMemcpyAsync(flags, h->dflags, 16 * sizeof(int), hipMemcpyDeviceToHost, h->stream));
+    int flags[kFlagWords] = {0};
+    RSVD_CK(hipMemcpyAsync(flags, h->dflags, kFlagWords * sizeof(int), hipMemcpyDeviceToHost, h->stream));
     RSVD_CK(hipStreamSynchronize(h->stream));
     if (flags[2]) {
         h->err = "a Gram reduction timed out waiting for its producers";
@@ -398,6 +418,7 @@ int rsvd_get_info(rsvd_handle_t h, rsvd_info_t* info) {
     for (int k = 4; k < 16; ++k) fallbacks += flags[k] != 0;
     h->info.cholqr_fallbacks = fallbacks;
     h->info.jacobi_sweeps = flags[1];
+    h->info.power_kept = flags[16];
     *info = h->info;
     return RSVD_OK;
 }

@@ -18,7 +18,9 @@ struct rsvd_handle_s {
     char* ws = nullptr;
     size_t ws_bytes = 0;
     bool ws_external = false;  // workspace supplied by the caller (rsvd_set_workspace)
-    int* dflags = nullptr;  // [0] cholqr breakdown count, [1] jacobi sweeps
+    // device flags: [1] jacobi sweeps, [2] Gram hand-off timeout, [3] block-Jacobi barrier timeout,
+    // [4..15] per-orthonormalisation breakdown flags, [16] power-method triplets kept
+    int* dflags = nullptr;
     rsvd_info_t info{};
     int rank = 0, world = 1;
     rsvd_allreduce_fn allreduce = nullptr;
@@ -46,6 +48,8 @@ struct rsvd_handle_s {
         int _s = (expr);                 \
         if (_s != RSVD_OK) return _s;    \
     } while (0)
+
+constexpr int kFlagWords = 32;
 
 inline int lp_of(int l) { return (l + 15) / 16 * 16; }
 inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }

@@ -19,6 +19,7 @@
 #include <string>
 
 #include "handle.hpp"
+#include "dense.hpp"
 #include "kernels.hpp"
 #include "wide.hpp"
 
@@ -278,11 +279,34 @@ struct WideEngine {
         return RSVD_OK;
     }
 
+    // SVDMethod::Power on B = Q^T A in Q_B coordinates (driver.cpp power_stage, dense.hip).
+    int power_stage(const rsvd_desc_t* d, void* U, int64_t ldu, T* S, void* V, int64_t ldv) {
+        double *Y0 = G, *Pp = R, *X0s = Rinv, *Bpm = W, *Up = Uw, *Vc = Vw, *Sd = JX;
+        RSVD_CK(launch_power_start<T>(T1, L.n, L.l, L.LP, power_seed(d->seed), s));
+        RSVD_CK(launch_gram_wide<T>(Xn, T1, L.n, L.LP, L.gx, gslab, Y0, nullptr, s));  // Y0 = Q_B^T X0
+        RSVD_CK(launch_power_prep(R1, Y0, L.l, L.LP, Pp, X0s, Bpm, s));
+        RSVD_CK(launch_power_svd(Pp, L.l, L.l, L.LP, Bpm, L.l, 0, power_iterations(L.n), Up, Vc, Sd, h->dflags + 16,
+                                 s, X0s, 1));
+        const double sc = (d->a_scale != 0.0) ? d->a_scale : 1.0;
+        RSVD_CK(launch_convert_scale<T>(Sd, S, L.l, sc, s));
+        if (sizeof(T) == 4) {
+            const int L2 = L.LP * L.LP;
+            RSVD_CK(launch_convert_scale<float>(Up, Uw32, L2, 1.0, s));
+            RSVD_CK(launch_convert_scale<float>(Vc, Vw32, L2, 1.0, s));
+        }
+        RSVD_CK(launch_panel_gemm<T>(Qm, L.m, L.LP, mat(Up, Uw32), 0, reinterpret_cast<T*>(U), ldu, L.l, nullptr,
+                                     nullptr, nullptr, s));
+        RSVD_CK(launch_panel_gemm<T>(Xn, L.n, L.LP, mat(Vc, Vw32), 0, reinterpret_cast<T*>(V), ldv, L.l, nullptr,
+                                     nullptr, nullptr, s));
+        return RSVD_OK;
+    }
+
     int run(const rsvd_desc_t* d, const void* A, void* U, int64_t ldu, T* S, void* V, int64_t ldv) {
         RSVD_TRY(range_finder(A, d->lda, d->q));
         RSVD_TRY(proj_tn(A, d->lda, Qm, Qh, Ql, Zn));               // B^T = A^T Q
         RSVD_TRY(orth(Zn, false, Xn, 2, nullptr, nullptr, true));  // Q_B
         RSVD_CK(launch_gram_wide<T>(Xn, Zn, L.n, L.LP, L.gx, gslab, R1, nullptr, s));  // R = Q_B^T B^T
+        if (d->method == RSVD_SVD_POWER) return power_stage(d, U, ldu, S, V, ldv);
         // the small SVD always runs in fp64 (U_w, V_w feed the fp32 panel products of U and V)
         double* Sd = G;  // free scratch by now
         if (L.LP <= 64) {
@@ -310,7 +334,7 @@ int wide_typed(rsvd_handle_t h, const rsvd_desc_t* d, const void* A, const void*
                int64_t ldu, void* S, void* V, int64_t ldv, void* Qout, int64_t ldq) {
     WideLayout<T> L(d, (reinterpret_cast<uintptr_t>(A) & 15) == 0);
     RSVD_TRY(ensure_ws(h, L.total));
-    RSVD_CK(hipMemsetAsync(h->dflags, 0, 16 * sizeof(int), h->stream));
+    RSVD_CK(hipMemsetAsync(h->dflags, 0, kFlagWords * sizeof(int), h->stream));
     if (L.lowp) {  // the zero padding rows of the bf16 panels (never written by the kernels)
         const size_t bpr = (size_t)2 * L.LP;
         for (size_t off : {L.off_Xh, L.off_Xl})

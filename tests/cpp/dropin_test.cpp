@@ -74,6 +74,13 @@ int main() {
         }
     CHECK(orth < 1e-12, "Q^T Q == I (dev %g)", orth);
 
+    // rSVD with Method::Power: the reference's layouts (U m x l, S l, V = the n x n V_, rows v_i)
+    rsvd::rsvd(A, U, S, V, l, rsvd::Method::Power);
+    CHECK(U.rows() == n && U.cols() == l && S.size() == l && V.rows() == n && V.cols() == n, "Power rSVD shapes");
+    double pdev = 0;
+    for (int i = 0; i < l; ++i) pdev = std::fmax(pdev, std::fabs(S.v[i] - 1.0));
+    CHECK(pdev < 1e-12 && V(n - 1, n - 1) == 1.0, "Power rSVD on I: S == 1 (dev %g), identity rows of V_", pdev);
+
     bool threw = false;
     try {
         rsvd::rsvd(A, U, S, V, l, static_cast<rsvd::Method>(7));

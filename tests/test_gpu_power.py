@@ -1,0 +1,66 @@
+"""GPU parity of rSVD with SVDMethod::Power (src/rSVD.cpp:106-113 -> SVD<Power>, SVD_class.hpp:183-219,
+PM src/PM.cpp:4-81) against the oracle (oracle.rsvd_power: the reference's power method with
+deflation on the n x n B^T B).  The engine runs the same iteration in the coordinates of Q_B
+(DESIGN.md §3.5), with the start vectors Philox(seed ^ 0x504F574552 + i) the oracle also draws.
+
+Compared: the leading triplets of a gapped spectrum (ratio 0.8 per index: the fixed s(n)
+power iterations converge them to rounding).  Tolerances: fp64 1e-10 (S) / 1e-8 (U, V); fp32
+and bf16 1e-4 (north star)."""
+import numpy as np
+import pytest
+
+from conftest import gapped_matrix, rel_fro, sign_align
+
+pytestmark = pytest.mark.gpu
+
+import oracle  # noqa: E402  (test infrastructure)
+
+PM_KEY = 0x504F574552
+
+
+@pytest.mark.parametrize("m,n,l,dt", [(300, 200, 16, "f64"), (600, 500, 32, "f32"), (700, 400, 96, "f64"),
+                                      (1024, 768, 64, "bf16")])
+def test_rsvd_power_matches_oracle(engine, m, n, l, dt):
+    import torch
+
+    import rsvd_kamaneh_raganato_terrana_amd as R
+
+    tdt = {"f64": torch.float64, "f32": torch.float32, "bf16": torch.bfloat16}[dt]
+    A = gapped_matrix(m, n, 2 * l, decay=0.8, seed=m + n)
+    At = torch.from_numpy(A).cuda().to(tdt)
+    seed = 4321
+    U, S, V = engine.rsvd(At, l, q=2, method=R.SVDMethod.Power, seed=seed)
+    kept = engine.info()["power_kept"]
+    assert kept == l
+    U, S, V = (x.cpu().double().numpy() for x in (U, S, V))
+    Om = engine.generate_omega(n, l, seed=seed, dtype=tdt).cpu().double().numpy()
+    Aused = At.cpu().double().numpy()
+    Uo, So, Vf = oracle.rsvd_power(Aused, l, q=2, Omega=Om, pm_seed=seed ^ PM_KEY)
+    Vo = Vf[:l, :].T  # the reference's V_ holds v_i in rows
+    k = min(16, l // 2)
+    ts, tv = (1e-10, 1e-8) if dt == "f64" else (1e-4, 1e-4)
+    assert rel_fro(S[:k], So[:k]) < ts
+    assert rel_fro(sign_align(V[:, :k], Vo[:, :k]), Vo[:, :k]) < tv
+    assert rel_fro(sign_align(U[:, :k], Uo[:, :k]), Uo[:, :k]) < tv
+
+
+def test_rsvd_power_reference_layout_and_early_stop(engine):
+    import rsvd_kamaneh_raganato_terrana_amd as R
+
+    # rank 3: after three triplets sigma < 1e-12 stops the power method (SVD_class.hpp:198-208)
+    rng = np.random.default_rng(3)
+    m, n, l = 120, 90, 8
+    A = np.asfortranarray((rng.standard_normal((m, 3)) * [3.0, 2.0, 1.0]) @ rng.standard_normal((3, n)) * 1e-3)
+    U, S, V = R.rSVD(A, l, R.SVDMethod.Power, seed=77)
+    Uo, So, Vo = oracle.rsvd_power(A, l, q=2, Omega=R.generateOmega(n, l, seed=77), pm_seed=77 ^ PM_KEY)
+    assert U.shape == Uo.shape == (m, 3) and S.shape == So.shape == (3,) and V.shape == Vo.shape == (n, 3)
+    assert rel_fro(S, So) < 1e-10
+    # full run: V is the n x n V_ with v_i^T in rows i < l and identity rows beyond
+    B = gapped_matrix(m, n, 2 * l, decay=0.75, seed=9)
+    U, S, V = R.rSVD(B, l, R.SVDMethod.Power, seed=5)
+    assert U.shape == (m, l) and S.shape == (l,) and V.shape == (n, n)
+    assert np.array_equal(V[l:, :], np.eye(n)[l:, :])
+    Uo, So, Vo = oracle.rsvd_power(B, l, q=2, Omega=R.generateOmega(n, l, seed=5), pm_seed=5 ^ PM_KEY)
+    k = l // 2
+    assert rel_fro(S[:k], So[:k]) < 1e-10
+    assert rel_fro(sign_align(V[:k, :].T, Vo[:k, :].T), Vo[:k, :].T) < 1e-8
