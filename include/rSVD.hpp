@@ -4,6 +4,7 @@
 //   void intermediate_step(const Mat_m &A, Mat_m &Q, const Mat_m &Omega, int l, int q);  rSVD.hpp:13
 //   void rSVD(Mat_m &A, Mat_m &U, Vec_v &S, Mat_m &V, int l, SVDMethod method);         rSVD.hpp:14
 //   Mat_m generateOmega(int n, int l);                                                   rSVD.hpp:15
+//   void rSVD(Mat_m &A, Mat_m &U, Vec_v &S, Mat_m &V, int l);  image_compression/include/rSVD.hpp
 //
 // Link with -lrsvd_hip (rsvd_kamaneh_raganato_terrana_amd/librsvd_hip.so).  Needs Eigen >= 3.3
 // (as the reference does); no MPI requirement.  SVDMethod is declared here (the reference declares
@@ -32,5 +33,12 @@ inline void rSVD(Mat_m &A, Mat_m &U, Vec_v &S, Mat_m &V, int l, SVDMethod method
 }
 
 inline Mat_m generateOmega(int n, int l) { return rsvd::generate_omega<Mat_m>(n, l); }
+
+// image_compression/include/rSVD.hpp: void rSVD(MatrixXd& A, MatrixXd& U, VectorXd& S, MatrixXd& V,
+// int l) -- q = 1 and the power-method small SVD with V = VT^T in columns
+// (image_compression/src/rSVD.cpp:77-118, src/SVD.cpp:31-55).  An overload of the 6-argument form.
+inline void rSVD(Mat_m &A, Mat_m &U, Vec_v &S, Mat_m &V, int l) {
+    rsvd::rsvd_columns(A, U, S, V, l, rsvd::Method::Power, /*q=*/1);
+}
 
 #endif

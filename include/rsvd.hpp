@@ -80,11 +80,12 @@ inline void check(int status, const char* what) {
 }
 
 // rSVD(A, U, S, V, l, method) with q power iterations (the reference hard-codes q = 2).
-// Method::Power returns what the reference's rSVD returns for it (src/rSVD.cpp:106-113 with
-// SVD_class.hpp:183-219): U m x l, S l and V = the n x n V_ of SVD<Power> (v_i^T in row i, identity
-// rows beyond), each cut to the first `kept` columns when the power method stops early.
+// rSVD with the outputs as the C ABI returns them: U m x d, S d, V n x d with the right singular
+// vectors in COLUMNS for every method (d = min(l, n)).  With Method::Power and q = 1 this is
+// image_compression's 5-argument rSVD(A, U, S, V, l) (image_compression/src/rSVD.cpp:77-118:
+// q = 1, power-method small SVD with V = VT^T, image_compression/src/SVD.cpp:31-55).
 template <class Mat, class Vec>
-void rsvd(const Mat& A, Mat& U, Vec& S, Mat& V, int l, Method method, int q = 2) {
+void rsvd_columns(const Mat& A, Mat& U, Vec& S, Mat& V, int l, Method method, int q) {
     const int64_t m = A.rows(), n = A.cols();
     const int64_t d = l < n ? l : n;
     U.resize(m, d);
@@ -94,7 +95,18 @@ void rsvd(const Mat& A, Mat& U, Vec& S, Mat& V, int l, Method method, int q = 2)
     check(rsvd_run_host_f64(c.handle(), m, n, A.data(), m, l, q, static_cast<int32_t>(method), nullptr,
                             c.next_seed(), U.data(), S.data(), V.data()),
           "rSVD");
+}
+
+// Method::Power returns what the reference's rSVD returns for it (src/rSVD.cpp:106-113 with
+// SVD_class.hpp:183-219): U m x l, S l and V = the n x n V_ of SVD<Power> (v_i^T in row i, identity
+// rows beyond), each cut to the first `kept` columns when the power method stops early.
+template <class Mat, class Vec>
+void rsvd(const Mat& A, Mat& U, Vec& S, Mat& V, int l, Method method, int q = 2) {
+    rsvd_columns(A, U, S, V, l, method, q);
     if (method != Method::Power) return;
+    const int64_t m = A.rows(), n = A.cols();
+    const int64_t d = l < n ? l : n;
+    Context& c = Context::instance();
     rsvd_info_t info{};
     check(rsvd_get_info(c.handle(), &info), "rSVD");
     const int64_t kept = info.power_kept;

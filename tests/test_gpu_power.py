@@ -64,3 +64,19 @@ def test_rsvd_power_reference_layout_and_early_stop(engine):
     k = l // 2
     assert rel_fro(S[:k], So[:k]) < 1e-10
     assert rel_fro(sign_align(V[:k, :].T, Vo[:k, :].T), Vo[:k, :].T) < 1e-8
+
+
+def test_image_compression_rsvd_q1_power(engine):
+    # image_compression/src/rSVD.cpp:77-118: q = 1, power-method small SVD, V = VT^T (columns)
+    import rsvd_kamaneh_raganato_terrana_amd as R
+
+    m, n, l = 512, 384, 24
+    A = gapped_matrix(m, n, 2 * l, decay=0.8, seed=21)
+    U, S, V = engine.rsvd_host(A, l, q=1, method=R.SVDMethod.Power, seed=99)
+    assert U.shape == (m, l) and S.shape == (l,) and V.shape == (n, l)
+    Om = engine.generate_omega_host(n, l, seed=99)
+    Uo, So, Vf = oracle.rsvd_power(A, l, q=1, Omega=Om, pm_seed=99 ^ PM_KEY)
+    k = 12
+    assert rel_fro(S[:k], So[:k]) < 1e-10
+    assert rel_fro(sign_align(V[:, :k], Vf[:k, :].T), Vf[:k, :].T) < 1e-8
+    assert rel_fro(sign_align(U[:, :k], Uo[:, :k]), Uo[:, :k]) < 1e-8
