@@ -26,7 +26,13 @@ namespace rsvd {
 namespace {
 
 constexpr int kWaves = 4;
-constexpr int kPrefetch = 8;  // k-steps of A kept in flight per wave (NN; TN keeps half as many, wider)
+#ifndef RSVD_PDTN
+#define RSVD_PDTN 8
+#endif
+// k-steps of A kept in flight per wave (register prefetch ring); measured on C2 (kernel_lab):
+// NN 8 with the loads issued before the step's MFMAs, TN 8 (its steps are twice as wide)
+constexpr int kPrefetchNN = 8;
+constexpr int kPrefetchTN = RSVD_PDTN;
 
 template <typename T>
 __device__ __forceinline__ typename Vec16<T>::type load_vec_guarded(const T* __restrict__ col, int64_t i,
@@ -55,6 +61,10 @@ __global__ __launch_bounds__(kWave* kWaves) void proj_nn_kernel(
     constexpr int VW = Vec16<T>::N;
     constexpr int WR = 16 * VW;
     constexpr int G = LP / 16;
+    // PERM (fp32, LP = 64): MFMA tile g, column r holds panel column 4r + g, so a lane's four
+    // B values of a k are one 16-B load; the epilogue maps the columns back.
+    constexpr bool PERM = sizeof(T) == 4 && G == 4;
+    auto pcol = [](int rr, int g) { return PERM ? 4 * rr + g : 16 * g + rr; };
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
     T* red = reinterpret_cast<T*>(smem_raw);  // [kWaves][WR][LP]
 
@@ -74,19 +84,67 @@ __global__ __launch_bounds__(kWave* kWaves) void proj_nn_kernel(
         for (int g = 0; g < G; ++g) acc[t][g] = M::zero();
 
     // This wave's k-steps (4 k each, interleaved with the other waves), register-prefetched PD
-    // steps ahead so that enough A bytes are in flight per CU to cover HBM latency.
-    constexpr int PD = kPrefetch;
+    // steps ahead so that enough A bytes are in flight per CU to cover HBM latency.  Steps whose
+    // 4 k values are all in range (and the row tile full, vector loads legal) run a branch-free
+    // ring with pointer-bumped loads; the remaining steps take the guarded path.
+    constexpr int PD = kPrefetchNN;
     const int64_t kstep = 4 * kWaves, kfirst = kbeg + 4 * w;
     const int nst = (kfirst < kend) ? (int)((kend - kfirst + kstep - 1) / kstep) : 0;
-    V pa[PD];
-    T pb[PD][G];
-    auto load = [&](int st, V& a, T* b) {
-        const int64_t k = kfirst + (int64_t)st * kstep + h;
-        if (st < nst && k < kend) {
-            a = load_vec_guarded<T>(A + k * lda, row, m, vec_ok);
-            const T* xr = X + k * ldp + r;
+    const bool fast_rows = vec_ok && i0 + WR <= m;  // wave-uniform: MFMAs need every lane on one path
+    const int nfull = (fast_rows && kfirst + 3 < kend) ? (int)((kend - kfirst - 4) / kstep) + 1 : 0;
+    auto mma_step = [&](const V& a, const T* b) {
 #pragma unroll
-            for (int g = 0; g < G; ++g) b[g] = xr[16 * g];
+        for (int t = 0; t < VW; ++t) {
+            const T at = Vec16<T>::get(a, t);
+#pragma unroll
+            for (int g = 0; g < G; ++g) acc[t][g] = M::mma(at, b[g], acc[t][g]);
+        }
+    };
+    int st = 0;
+    if (nfull >= PD) {
+        V pa[PD];
+        T pb[PD][G];
+        const int64_t astride = kstep * lda, xstride = kstep * ldp;
+        const T* ap = A + (kfirst + h) * lda + row;
+        const T* xp = X + (kfirst + h) * ldp + (PERM ? 4 * r : r);
+        auto load_fast = [&](V& a, T* b) {
+            a = *reinterpret_cast<const V*>(ap);
+            if constexpr (PERM) {
+                const float4 x4 = *reinterpret_cast<const float4*>(xp);
+                b[0] = x4.x; b[1] = x4.y; b[2] = x4.z; b[3] = x4.w;
+            } else {
+#pragma unroll
+                for (int g = 0; g < G; ++g) b[g] = xp[16 * g];
+            }
+            ap += astride;
+            xp += xstride;
+        };
+#pragma unroll
+        for (int u = 0; u < PD; ++u) load_fast(pa[u], pb[u]);
+        for (; st + 2 * PD <= nfull; st += PD) {
+#pragma unroll
+            for (int u = 0; u < PD; ++u) {
+                const V a = pa[u];  // next load issued before this step's MFMAs
+                T b[G];
+#pragma unroll
+                for (int g = 0; g < G; ++g) b[g] = pb[u][g];
+                load_fast(pa[u], pb[u]);
+                mma_step(a, b);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < PD; ++u) mma_step(pa[u], pb[u]);
+        st += PD;
+    }
+    for (; st < nst; ++st) {  // guarded tail (and short K ranges)
+        const int64_t k = kfirst + (int64_t)st * kstep + h;
+        V a;
+        T b[G];
+        if (k < kend) {
+            a = load_vec_guarded<T>(A + k * lda, row, m, vec_ok);
+            const T* xr = X + k * ldp;
+#pragma unroll
+            for (int g = 0; g < G; ++g) b[g] = xr[pcol(r, g)];
         } else {
             T* e = reinterpret_cast<T*>(&a);
 #pragma unroll
@@ -94,25 +152,7 @@ __global__ __launch_bounds__(kWave* kWaves) void proj_nn_kernel(
 #pragma unroll
             for (int g = 0; g < G; ++g) b[g] = T(0);
         }
-    };
-#pragma unroll
-    for (int u = 0; u < PD; ++u) load(u, pa[u], pb[u]);
-    for (int base = 0; base < nst; base += PD) {
-#pragma unroll
-        for (int u = 0; u < PD; ++u) {
-            if (base + u >= nst) break;
-            const V a = pa[u];
-            T b[G];
-#pragma unroll
-            for (int g = 0; g < G; ++g) b[g] = pb[u][g];
-            load(base + u + PD, pa[u], pb[u]);
-#pragma unroll
-            for (int t = 0; t < VW; ++t) {
-                const T at = Vec16<T>::get(a, t);
-#pragma unroll
-                for (int g = 0; g < G; ++g) acc[t][g] = M::mma(at, b[g], acc[t][g]);
-            }
-        }
+        mma_step(a, b);
     }
 
     // wave partials -> LDS [w][local row][col]
@@ -124,7 +164,7 @@ __global__ __launch_bounds__(kWave* kWaves) void proj_nn_kernel(
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const int lr = VW * M::row(h, j) + t;
-                mine[lr * LP + 16 * g + r] = acc[t][g][j];
+                mine[lr * LP + pcol(r, g)] = acc[t][g][j];
             }
     __syncthreads();
     T* dst = out + (int64_t)s * slab_stride;
@@ -172,18 +212,80 @@ __global__ __launch_bounds__(kWave* kWaves) void proj_tn_kernel(
         for (int g = 0; g < G; ++g) acc[jt][g] = M::zero();
 
     constexpr int ISTEP = 4 * VW;  // rows of A consumed per MFMA group
-    constexpr int PD = kPrefetch / 2;
+    constexpr int PD = kPrefetchTN;
+    constexpr bool PERM = sizeof(T) == 4 && G == 4;  // as in proj_nn: column 4r + g of the panel
     const int64_t istep = (int64_t)ISTEP * kWaves, ifirst = ibeg + ISTEP * w;
     const int nst = (ifirst < iend) ? (int)((iend - ifirst + istep - 1) / istep) : 0;
-    V pa[PD][JT];
-    T pb[PD][VW][G];
-    auto load = [&](int st, V* a, T (*b)[G]) {
+    auto mma_step = [&](const V* a, T (*b)[G]) {
+#pragma unroll
+        for (int t = 0; t < VW; ++t)
+#pragma unroll
+            for (int jt = 0; jt < JT; ++jt) {
+                const T at = Vec16<T>::get(a[jt], t);
+#pragma unroll
+                for (int g = 0; g < G; ++g) acc[jt][g] = M::mma(at, b[t][g], acc[jt][g]);
+            }
+    };
+    // full steps: all ISTEP rows below iend, all JT column tiles inside n, vector loads legal
+    const bool fast_cols = vec_ok && j0 + WJ <= n;
+    const int nfull = (fast_cols && ifirst + ISTEP <= iend) ? (int)((iend - ifirst - ISTEP) / istep) + 1 : 0;
+    int st = 0;
+    if (nfull >= PD) {
+        V pa[PD][JT];
+        T pb[PD][VW][G];
+        const T* ap = A + (j0 + r) * lda + ifirst + VW * h;
+        const T* qp = Q + (ifirst + VW * h) * ldp + (PERM ? 4 * r : r);
+        const int64_t qstride = istep * ldp;
+        auto load_fast = [&](V* a, T (*b)[G]) {
+#pragma unroll
+            for (int jt = 0; jt < JT; ++jt) a[jt] = *reinterpret_cast<const V*>(ap + (int64_t)16 * jt * lda);
+#pragma unroll
+            for (int t = 0; t < VW; ++t) {
+                if constexpr (PERM) {
+                    const float4 q4 = *reinterpret_cast<const float4*>(qp + t * ldp);
+                    b[t][0] = q4.x; b[t][1] = q4.y; b[t][2] = q4.z; b[t][3] = q4.w;
+                } else {
+#pragma unroll
+                    for (int g = 0; g < G; ++g) b[t][g] = qp[t * ldp + 16 * g];
+                }
+            }
+            ap += istep;
+            qp += qstride;
+        };
+#pragma unroll
+        for (int u = 0; u < PD; ++u) load_fast(pa[u], pb[u]);
+        for (; st + 2 * PD <= nfull; st += PD) {
+#pragma unroll
+            for (int u = 0; u < PD; ++u) {
+#ifdef RSVD_LFTN
+                V a[JT];
+                T b[VW][G];
+#pragma unroll
+                for (int jt = 0; jt < JT; ++jt) a[jt] = pa[u][jt];
+#pragma unroll
+                for (int t = 0; t < VW; ++t)
+#pragma unroll
+                    for (int g = 0; g < G; ++g) b[t][g] = pb[u][t][g];
+                load_fast(pa[u], pb[u]);
+                mma_step(a, b);
+#else
+                mma_step(pa[u], pb[u]);
+                load_fast(pa[u], pb[u]);
+#endif
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < PD; ++u) mma_step(pa[u], pb[u]);
+        st += PD;
+    }
+    for (; st < nst; ++st) {  // guarded tail
         const int64_t ib = ifirst + (int64_t)st * istep + VW * h;
-        const bool ok = st < nst;
+        V a[JT];
+        T b[VW][G];
 #pragma unroll
         for (int jt = 0; jt < JT; ++jt) {
             const int64_t j = j0 + 16 * jt + r;
-            if (ok && j < n) {
+            if (j < n) {
                 a[jt] = load_vec_guarded<T>(A + j * lda, ib, iend, vec_ok);
             } else {
                 T* e = reinterpret_cast<T*>(&a[jt]);
@@ -194,35 +296,11 @@ __global__ __launch_bounds__(kWave* kWaves) void proj_tn_kernel(
 #pragma unroll
         for (int t = 0; t < VW; ++t) {
             const int64_t i = ib + t;
-            const T* qr = Q + i * ldp + r;
+            const T* qr = Q + i * ldp;
 #pragma unroll
-            for (int g = 0; g < G; ++g) b[t][g] = (ok && i < iend) ? qr[16 * g] : T(0);
+            for (int g = 0; g < G; ++g) b[t][g] = (i < iend) ? qr[PERM ? 4 * r + g : 16 * g + r] : T(0);
         }
-    };
-#pragma unroll
-    for (int u = 0; u < PD; ++u) load(u, pa[u], pb[u]);
-    for (int base = 0; base < nst; base += PD) {
-#pragma unroll
-        for (int u = 0; u < PD; ++u) {
-            if (base + u >= nst) break;
-            V a[JT];
-            T b[VW][G];
-#pragma unroll
-            for (int jt = 0; jt < JT; ++jt) a[jt] = pa[u][jt];
-#pragma unroll
-            for (int t = 0; t < VW; ++t)
-#pragma unroll
-                for (int g = 0; g < G; ++g) b[t][g] = pb[u][t][g];
-            load(base + u + PD, pa[u], pb[u]);
-#pragma unroll
-            for (int t = 0; t < VW; ++t)
-#pragma unroll
-                for (int jt = 0; jt < JT; ++jt) {
-                    const T at = Vec16<T>::get(a[jt], t);
-#pragma unroll
-                    for (int g = 0; g < G; ++g) acc[jt][g] = M::mma(at, b[t][g], acc[jt][g]);
-                }
-        }
+        mma_step(a, b);
     }
 
     T* mine = red + (size_t)w * WJ * LP;
@@ -231,7 +309,8 @@ __global__ __launch_bounds__(kWave* kWaves) void proj_tn_kernel(
 #pragma unroll
         for (int g = 0; g < G; ++g)
 #pragma unroll
-            for (int j = 0; j < 4; ++j) mine[(16 * jt + M::row(h, j)) * LP + 16 * g + r] = acc[jt][g][j];
+            for (int j = 0; j < 4; ++j)
+                mine[(16 * jt + M::row(h, j)) * LP + (PERM ? 4 * r + g : 16 * g + r)] = acc[jt][g][j];
     __syncthreads();
     T* dst = out + (int64_t)s * slab_stride;
     for (int e = threadIdx.x * VW; e < WJ * LP; e += blockDim.x * VW) {
