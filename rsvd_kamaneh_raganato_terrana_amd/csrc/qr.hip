@@ -448,9 +448,11 @@ __global__ __launch_bounds__(256) void chol_kernel(const double* __restrict__ Gi
     if (threadIdx.x == 0 && bad) atomicAdd(flag, 1);
 }
 
-// Out = In * M: 16 rows per wave, 4 waves per workgroup; In tile and M staged in LDS as fp64 and
-// multiplied on the f64 MFMA, so applying R^-1 does not amplify storage rounding by cond(R);
-// only the result is rounded to T.
+// Out = In * M (M: LP x LP fp64): one wave per 16 x 16 output tile (rows/16 x LP/16 waves, four
+// per workgroup), so even a 4096-row panel spreads over every CU.  A wave issues all of its
+// operand loads at once -- LP/4 In values (converted to fp64) and LP/4 M values per lane, M
+// being L2-resident -- and then runs LP/4 f64 MFMAs: applying R^-1 in fp64 keeps storage
+// rounding from being amplified by cond(R); only the result is rounded to T.
 template <typename T, int LP>
 __global__ __launch_bounds__(256) void panel_small_kernel(const T* __restrict__ In, int64_t rows,
                                                           const double* __restrict__ Mg, T* __restrict__ Out,
@@ -458,54 +460,32 @@ __global__ __launch_bounds__(256) void panel_small_kernel(const T* __restrict__ 
                                                           const int* __restrict__ pred) {
     if (pred && *pred == 0) return;
     typedef Mfma<double> M;
-    constexpr int G = LP / 16;
-    constexpr int RPB = 64;  // rows per block
-    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-    double* Ms = reinterpret_cast<double*>(smem_raw);  // [LP][LP]
-    double* Is = Ms + LP * LP;                         // [RPB][LP + 1] (padded: fragment reads are column-wise)
-    constexpr int IS = LP + 1;
-    const int tid = threadIdx.x;
-    const int lane = tid & 63, w = tid >> 6;
+    constexpr int G = LP / 16, KS = LP / 4;
+    const int lane = threadIdx.x & 63;
     const int r = lane & 15, h = lane >> 4;
-    const int64_t row0 = (int64_t)blockIdx.x * RPB;
-    for (int e = tid; e < LP * LP; e += blockDim.x) Ms[e] = Mg[e];
-    for (int e = tid; e < RPB * LP; e += blockDim.x) {
-        const int lr = e / LP, c = e % LP;
-        Is[lr * IS + c] = (row0 + lr < rows) ? (double)In[(row0 + lr) * LP + c] : 0.0;
+    const int64_t wave = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int g = (int)(wave % G);
+    const int64_t r0 = (wave / G) * 16;
+    if (r0 >= rows) return;
+    const int64_t arow = r0 + r;
+    double a[KS], b[KS];
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+        a[k] = (arow < rows) ? (double)In[arow * LP + 4 * k + h] : 0.0;
+        b[k] = Mg[(4 * k + h) * LP + 16 * g + r];
     }
-    __syncthreads();
-    f64x4 acc[G];
+    f64x4 acc = M::zero();
 #pragma unroll
-    for (int g = 0; g < G; ++g) acc[g] = M::zero();
-    const int lr0 = w * 16;
+    for (int k = 0; k < KS; ++k) acc = M::mma(a[k], b[k], acc);
+    const int col = 16 * g + r;
 #pragma unroll
-    for (int k0 = 0; k0 < LP; k0 += 4) {
-        const double a = Is[(lr0 + r) * IS + k0 + h];
-#pragma unroll
-        for (int g = 0; g < G; ++g) acc[g] = M::mma(a, Ms[(k0 + h) * LP + 16 * g + r], acc[g]);
-    }
-    if (!out_colmajor) {
-#pragma unroll
-        for (int g = 0; g < G; ++g)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int64_t row = row0 + lr0 + M::row(h, j);
-                if (row < rows) Out[row * LP + 16 * g + r] = (T)acc[g][j];
-            }
-        return;
-    }
-    // column-major output: transpose through LDS so each column segment is stored contiguously
-    __syncthreads();
-    double* Ts = Is;  // [LP][RPB + 1]
-    constexpr int TS = RPB + 1;
-#pragma unroll
-    for (int g = 0; g < G; ++g)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) Ts[(16 * g + r) * TS + lr0 + M::row(h, j)] = acc[g][j];
-    __syncthreads();
-    for (int e = tid; e < cols * RPB; e += blockDim.x) {
-        const int c = e / RPB, lr = e % RPB;
-        if (row0 + lr < rows) Out[row0 + lr + (int64_t)c * ld] = (T)Ts[c * TS + lr];
+    for (int j = 0; j < 4; ++j) {
+        const int64_t row = r0 + M::row(h, j);
+        if (row >= rows) continue;
+        if (!out_colmajor)
+            Out[row * LP + col] = (T)acc[j];
+        else if (col < cols)
+            Out[row + (int64_t)col * ld] = (T)acc[j];
     }
 }
 
@@ -593,12 +573,12 @@ hipError_t launch_chol(const double* G, int l, int LP, int compute_f32, double* 
 template <typename T>
 hipError_t launch_panel_small(const T* In, int64_t rows, int LP, const double* Mat, T* Out, int out_colmajor,
                               int cols, int64_t ld, hipStream_t s, const int* pred) {
-    const int blocks = (int)((rows + 63) / 64);
-    const size_t lds = (size_t)(LP * LP + std::max(64 * (LP + 1), LP * 65)) * sizeof(double);
+    const int64_t waves = (rows + 15) / 16 * (LP / 16);
+    const int blocks = (int)((waves + 3) / 4);
     switch (LP) {
 #define CASE(L)                                                                                          \
     case L:                                                                                              \
-        hipLaunchKernelGGL((panel_small_kernel<T, L>), dim3(blocks), dim3(256), lds, s, In, rows, Mat, Out, \
+        hipLaunchKernelGGL((panel_small_kernel<T, L>), dim3(blocks), dim3(256), 0, s, In, rows, Mat, Out, \
                            out_colmajor, cols, ld, pred);                                                \
         break;
         CASE(16) CASE(32) CASE(48) CASE(64)
