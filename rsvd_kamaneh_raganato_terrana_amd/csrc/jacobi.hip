@@ -77,6 +77,18 @@ template <> struct Eps<float> {
 template <typename C> struct Two;
 template <> struct Two<double> { typedef double2 type; };
 template <> struct Two<float> { typedef float2 type; };
+// LDS vector of the column accesses: up to 16 B per lane, N elements dividing the CH rows a
+// thread owns (so every access stays aligned)
+template <typename C, int N> struct VecT { typedef C type; };
+template <> struct VecT<float, 2> { typedef float2 type; };
+template <> struct VecT<float, 4> { typedef float4 type; };
+template <> struct VecT<double, 2> { typedef double2 type; };
+template <typename C, int CH>
+struct JVec {
+    static constexpr int W = 16 / (int)sizeof(C);
+    static constexpr int N = (CH % W == 0) ? W : ((CH % 2 == 0) ? 2 : 1);
+    typedef typename VecT<C, N>::type type;
+};
 
 __device__ __forceinline__ void rr_pair(int round, int k, int N, int& p, int& q) {
     if (k == 0) {
@@ -96,7 +108,7 @@ template <typename C, int LP>
 struct JacobiShape {
     static constexpr int TPP = (LP <= 32 || sizeof(C) == 8) ? 16 : 8;  // threads per column pair
     static constexpr int CH = LP / TPP;                                // rows per thread (even)
-    static constexpr int CS = LP + 2;                                  // column stride: aligned pairs, staggered banks
+    static constexpr int CS = LP + 16 / (int)sizeof(C);                // column stride: 16-B aligned, staggered banks
     static constexpr int NTHR = (LP / 2) * TPP;                        // one pair per TPP threads
 };
 
@@ -113,7 +125,6 @@ __global__ __launch_bounds__((JacobiShape<C, LP>::NTHR)) void small_svd_kernel(c
                                                         double* __restrict__ Uw, double* __restrict__ Vw,
                                                         T* __restrict__ S, int* __restrict__ info) {
     typedef JacobiShape<C, LP> SH;
-    typedef typename Two<C>::type C2;
     constexpr int TPP = SH::TPP, CH = SH::CH, CS = SH::CS;
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
     C* X = reinterpret_cast<C*>(smem_raw);                  // [LP][CS]   X[c*CS + i]
@@ -166,16 +177,25 @@ __global__ __launch_bounds__((JacobiShape<C, LP>::NTHR)) void small_svd_kernel(c
                 // every LDS operand of the round is requested up front: one exposed latency
                 C xp[CH], xq[CH], jp[CH], jq[CH];
                 const int i0 = sub * CH;
+                typedef typename JVec<C, CH>::type CV;
+                constexpr int NV = JVec<C, CH>::N;
 #pragma unroll
-                for (int t = 0; t < CH; t += 2) {
-                    const C2 a2 = *reinterpret_cast<const C2*>(X + p * CS + i0 + t);
-                    const C2 b2 = *reinterpret_cast<const C2*>(X + q * CS + i0 + t);
-                    const C2 c2 = *reinterpret_cast<const C2*>(J + p * CS + i0 + t);
-                    const C2 d2 = *reinterpret_cast<const C2*>(J + q * CS + i0 + t);
-                    xp[t] = a2.x; xp[t + 1] = a2.y;
-                    xq[t] = b2.x; xq[t + 1] = b2.y;
-                    jp[t] = c2.x; jp[t + 1] = c2.y;
-                    jq[t] = d2.x; jq[t + 1] = d2.y;
+                for (int t = 0; t < CH; t += NV) {
+                    const CV a4 = *reinterpret_cast<const CV*>(X + p * CS + i0 + t);
+                    const CV b4 = *reinterpret_cast<const CV*>(X + q * CS + i0 + t);
+                    const CV c4 = *reinterpret_cast<const CV*>(J + p * CS + i0 + t);
+                    const CV d4 = *reinterpret_cast<const CV*>(J + q * CS + i0 + t);
+                    const C* ap = reinterpret_cast<const C*>(&a4);
+                    const C* bp = reinterpret_cast<const C*>(&b4);
+                    const C* cp = reinterpret_cast<const C*>(&c4);
+                    const C* dp = reinterpret_cast<const C*>(&d4);
+#pragma unroll
+                    for (int v = 0; v < NV; ++v) {
+                        xp[t + v] = ap[v];
+                        xq[t + v] = bp[v];
+                        jp[t + v] = cp[v];
+                        jq[t + v] = dp[v];
+                    }
                 }
                 const C a = nrm[p], b = nrm[q];
                 C g0 = C(0), g1 = C(0);
@@ -203,20 +223,23 @@ __global__ __launch_bounds__((JacobiShape<C, LP>::NTHR)) void small_svd_kernel(c
                     const C t = ((d >= C(0)) == (g >= C(0))) ? tmag : -tmag;
                     const C cs = rsqrt_c(C(1) + t * t), sn = cs * t;
 #pragma unroll
-                    for (int u = 0; u < CH; u += 2) {
-                        C2 np, nq, mp, mq;
-                        np.x = cs * xp[u] - sn * xq[u];
-                        np.y = cs * xp[u + 1] - sn * xq[u + 1];
-                        nq.x = sn * xp[u] + cs * xq[u];
-                        nq.y = sn * xp[u + 1] + cs * xq[u + 1];
-                        mp.x = cs * jp[u] - sn * jq[u];
-                        mp.y = cs * jp[u + 1] - sn * jq[u + 1];
-                        mq.x = sn * jp[u] + cs * jq[u];
-                        mq.y = sn * jp[u + 1] + cs * jq[u + 1];
-                        *reinterpret_cast<C2*>(X + p * CS + i0 + u) = np;
-                        *reinterpret_cast<C2*>(X + q * CS + i0 + u) = nq;
-                        *reinterpret_cast<C2*>(J + p * CS + i0 + u) = mp;
-                        *reinterpret_cast<C2*>(J + q * CS + i0 + u) = mq;
+                    for (int u = 0; u < CH; u += NV) {
+                        CV np, nq, mp, mq;
+                        C* npp = reinterpret_cast<C*>(&np);
+                        C* nqp = reinterpret_cast<C*>(&nq);
+                        C* mpp = reinterpret_cast<C*>(&mp);
+                        C* mqp = reinterpret_cast<C*>(&mq);
+#pragma unroll
+                        for (int v = 0; v < NV; ++v) {
+                            npp[v] = cs * xp[u + v] - sn * xq[u + v];
+                            nqp[v] = sn * xp[u + v] + cs * xq[u + v];
+                            mpp[v] = cs * jp[u + v] - sn * jq[u + v];
+                            mqp[v] = sn * jp[u + v] + cs * jq[u + v];
+                        }
+                        *reinterpret_cast<CV*>(X + p * CS + i0 + u) = np;
+                        *reinterpret_cast<CV*>(X + q * CS + i0 + u) = nq;
+                        *reinterpret_cast<CV*>(J + p * CS + i0 + u) = mp;
+                        *reinterpret_cast<CV*>(J + q * CS + i0 + u) = mq;
                     }
                     if (sub == 0) {
                         nrm[p] = a - t * g;
