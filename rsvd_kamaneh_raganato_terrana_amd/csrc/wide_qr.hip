@@ -130,28 +130,18 @@ __global__ void gram_reduce_kernel(const double* __restrict__ slabs, int nblk, i
 }
 
 // ------------------------------------------------------------------------------------------------
-// Cholesky + inverse, one workgroup of kCholThreads threads.  W (work) holds the Gram being
-// reduced; R and Rinv are the outputs; the 16x16 inverse diagonal blocks stay in LDS.  Per 16-
-// column block p: wave 0 factors the diagonal block in registers (lane j owns column j, pivots and
-// rows broadcast with v_readlane: no workgroup barriers inside), all waves then form the strip
-// R[p][p+1..] = D^-T W[p][p+1..] and the trailing update W -= R[p]^T R[p] on the fp64 MFMA
-// (3 barriers per block).  R^-1 is assembled bottom-up by block rows (1 barrier per block).
+// Cholesky, one workgroup of kCholThreads threads.  W (work) holds the Gram being reduced (upper
+// block triangle only); R gets the factor's upper block triangle, Rinv the inverse diagonal blocks
+// (rinv_wide_kernel fills the rest).  Per 16-column block p: the strip R[p][p+1..] = D_p^-T W[p][p+1..]
+// (to global R and an LDS copy), then the trailing update W -= R[p]^T R[p] on the fp64 MFMA with both
+// operands from the LDS strip, each wave keeping kCholBatch W tiles' read-modify-write in flight (one
+// CU's update is latency-bound otherwise).  Look-ahead: wave 0 updates tile (p+1, p+1) first and
+// factors it -- 16x16 upper Cholesky and inverse in registers, lane j owning column j, pivots and rows
+// broadcast with v_readlane, rsqrt + Newton pivots -- while the other waves finish the update.  Two
+// workgroup barriers per block.
 constexpr int kCholThreads = 512;
-
-// acc += X^T Y for 16x16 fp64 blocks X (ldx), Y (ldy) given row-major: acc[i][j] += sum_k X[k][i] Y[k][j]
-__device__ __forceinline__ f64x4 mma_tn16(const double* X, int64_t ldx, const double* Y, int64_t ldy, f64x4 acc,
-                                          int r, int h) {
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) acc = MD::mma(X[(4 * kk + h) * ldx + r], Y[(4 * kk + h) * ldy + r], acc);
-    return acc;
-}
-// acc += X Y for 16x16 blocks: acc[i][j] += sum_k X[i][k] Y[k][j]
-__device__ __forceinline__ f64x4 mma_nn16(const double* X, int64_t ldx, const double* Y, int64_t ldy, f64x4 acc,
-                                          int r, int h) {
-#pragma unroll
-    for (int kk = 0; kk < 4; ++kk) acc = MD::mma(X[r * ldx + 4 * kk + h], Y[(4 * kk + h) * ldy + r], acc);
-    return acc;
-}
+constexpr int kCholBatch = 6;
+constexpr int kCholPad = 16;  // LDS strip pitch LP + 16 doubles: the 4 k-rows of a tile read hit different banks
 
 __device__ __forceinline__ double readlane_d(double v, int lane) {
     const unsigned long long u = __builtin_bit_cast(unsigned long long, v);
@@ -160,154 +150,395 @@ __device__ __forceinline__ double readlane_d(double v, int lane) {
     return __builtin_bit_cast(double, ((unsigned long long)hi << 32) | lo);
 }
 
+__device__ __forceinline__ void tri_decode(int t, int nt2, int& ib, int& jb) {  // t -> (ib <= jb) in [0, nt2)
+    int rem = t, i = 0;
+    while (rem >= nt2 - i) {
+        rem -= nt2 - i;
+        ++i;
+    }
+    ib = i;
+    jb = i + rem;
+}
+
+// 1/sqrt(d) to fp64 accuracy: hardware estimate + two Newton steps
+__device__ __forceinline__ double rsqrt_nr(double d) {
+    double y = __builtin_amdgcn_rsq(d);
+    y = y * fma(-0.5 * d * y, y, 1.5);
+    y = y * fma(-0.5 * d * y, y, 1.5);
+    return y;
+}
+
+// Wave-level factor of the 16x16 diagonal block p (lane j: col[i] = D[i][j], upper part valid):
+// R block and D^-1 block to global (R, Rinv diagonal blocks) and D^-1 to the LDS buffer Di;
+// breakdown rows to bad[16] and the flags.
+__device__ __forceinline__ void chol_diag16(double (&col)[16], int p16, int l, int LP, double tol,
+                                            const double* d0, double* Di, int* bad, double* R, double* Rinv,
+                                            int* colflag, int* flag, int lane) {
+    const int j = lane & 15;
+    int badmask = 0;
+    double inv[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int gk = p16 + k;
+        const double dkk = readlane_d(col[k], k);
+        const bool pad = gk >= l;
+        const bool isbad = !pad && (!(dkk > tol * d0[gk]) || !(d0[gk] > 0.0) || !isfinite(dkk));
+        if (isbad) badmask |= 1 << k;
+        const bool unit = pad || isbad;
+        const double y = unit ? 1.0 : rsqrt_nr(dkk);
+        inv[k] = y;
+        const double rk = unit ? 1.0 : dkk * y;
+        if (j > k) col[k] = unit ? 0.0 : col[k] * y;
+        if (j == k) col[k] = rk;
+#pragma unroll
+        for (int i = k + 1; i < 16; ++i) {
+            const double dki = readlane_d(col[k], i);  // D[k][i]
+            if (j >= i) col[i] -= dki * col[k];
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+        if (i > j) col[i] = 0.0;
+    // D^-1 column j by back substitution: x[i] = -(sum_{k>i} D[i][k] x[k]) / D[i][i]
+    double x[16];
+#pragma unroll
+    for (int i = 15; i >= 0; --i) {
+        double s = 0.0;
+#pragma unroll
+        for (int k = i + 1; k < 16; ++k) s += readlane_d(col[i], k) * x[k];  // D[i][k] from lane k
+        x[i] = (i == j) ? inv[i] : ((i < j) ? -s * inv[i] : 0.0);
+    }
+    if (lane < 16) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            Di[i * 16 + j] = x[i];
+            Rinv[(int64_t)(p16 + i) * LP + p16 + j] = x[i];
+            R[(int64_t)(p16 + i) * LP + p16 + j] = col[i];
+        }
+        bad[lane] = (badmask >> lane) & 1;
+    }
+    if (lane == 0 && badmask) {
+        atomicAdd(flag, __popc(badmask));
+        for (int k = 0; k < 16; ++k)
+            if (badmask & (1 << k)) colflag[p16 + k] = 1;
+    }
+}
+
+#ifdef RSVD_CHOL_PROF
+__device__ long long g_chol_prof[256];
+#define CHOL_TS(k)                                               \
+    do {                                                         \
+        if (threadIdx.x == 0) g_chol_prof[(k)] = wall_clock64(); \
+    } while (0)
+#else
+#define CHOL_TS(k) \
+    do {           \
+    } while (0)
+#endif
+
+// Upper block-triangle walk (ib <= jb < n): advance by `step` tiles; ib >= n marks the end.
+struct TriWalk {
+    int ib, jb, n;
+    __device__ __forceinline__ TriWalk(int t, int n_) : ib(n_), jb(0), n(n_) {
+        if (t < n_ * (n_ + 1) / 2) tri_decode(t, n_, ib, jb);
+    }
+    __device__ __forceinline__ void advance(int step) {
+        jb += step;
+        while (ib < n && jb >= n) {
+            const int over = jb - n;
+            ++ib;
+            jb = ib + over;
+        }
+    }
+};
+
+// W is kept tile-major in MFMA output order: tile (ib, jb) at (ib * np + jb) * 256, lane (r, h)'s
+// four values (rows h + 4 j, column r) contiguous -- one 32-B access per lane per tile, and the
+// same registers serve as the B operand (rows 4 kk + h) of the strip product.
+__device__ __forceinline__ double* wtile(double* W, int np, int ib, int jb, int lane) {
+    return W + ((int64_t)ib * np + jb) * 256 + lane * 4;
+}
+
 __global__ __launch_bounds__(kCholThreads) void chol_wide_kernel(const double* __restrict__ G, int l, int LP,
                                                                  double tol, double* __restrict__ W,
                                                                  double* __restrict__ R, double* __restrict__ Rinv,
-                                                                 float* __restrict__ Rinv32, int* __restrict__ colflag,
-                                                                 int* __restrict__ flag, const int* __restrict__ pred) {
+                                                                 int* __restrict__ colflag, int* __restrict__ flag,
+                                                                 const int* __restrict__ pred) {
     if (pred && *pred == 0) return;
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
     const int np = LP / 16;
-    double* Dinv = reinterpret_cast<double*>(smem_raw);  // [np][16][16]
-    double* d0 = Dinv + np * 256;                        // [LP] original diagonal of G
-    double* Tsc = d0 + LP;                               // [waves][16][16] per-wave scratch
-    int* bad = reinterpret_cast<int*>(Tsc + (kCholThreads / 64) * 256);  // [16]
-    const int tid = threadIdx.x, nt = blockDim.x;
-    const int lane = tid & 63, wv = tid >> 6, nw = nt >> 6;
+    const int ldr = LP + kCholPad;
+    constexpr int nw = kCholThreads / 64;
+    constexpr int B = kCholBatch;
+    double* Dd = reinterpret_cast<double*>(smem_raw);  // [2][16][16] D^-1 of blocks p, p+1
+    double* d0 = Dd + 512;                             // [LP] original diagonal of G
+    double* Rs = d0 + LP;                              // [16][ldr] current R row strip
+    double* Tsc = Rs + 16 * ldr;                       // [16][16] wave 0's look-ahead tile
+    int* bad = reinterpret_cast<int*>(Tsc + 256);      // [2][16]
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, wv = tid >> 6;
     const int r = lane & 15, h = lane >> 4;
-    const int64_t L2 = (int64_t)LP * LP;
+    CHOL_TS(97);
 
-    for (int64_t e = tid; e < L2; e += nt) {
-        const int i = (int)(e / LP), j = (int)(e % LP);
-        W[e] = (i < l && j < l) ? G[e] : 0.0;
-        R[e] = 0.0;
-        Rinv[e] = 0.0;
+    // W := upper block triangle of G (zero beyond l), tile-major; B tiles per wave in flight
+    {
+        TriWalk tw(wv, np);
+        while (tw.ib < np) {
+            double v[B][4];
+            int tix[B];
+#pragma unroll
+            for (int b = 0; b < B; ++b) {
+                tix[b] = tw.ib < np ? tw.ib * 64 + tw.jb : -1;
+                if (tw.ib < np) {
+                    const int c = 16 * tw.jb + r;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int i = 16 * tw.ib + h + 4 * j;
+                        v[b][j] = (i < l && c < l) ? G[(int64_t)i * LP + c] : 0.0;
+                    }
+                }
+                tw.advance(nw);
+            }
+#pragma unroll
+            for (int b = 0; b < B; ++b)
+                if (tix[b] >= 0) {
+                    double* dst = wtile(W, np, tix[b] >> 6, tix[b] & 63, lane);
+                    *reinterpret_cast<double2*>(dst) = make_double2(v[b][0], v[b][1]);
+                    *reinterpret_cast<double2*>(dst + 2) = make_double2(v[b][2], v[b][3]);
+                }
+        }
     }
-    for (int i = tid; i < LP; i += nt) {
+    for (int i = tid; i < LP; i += kCholThreads) {
         d0[i] = (i < l) ? G[(int64_t)i * LP + i] : 0.0;
         colflag[i] = 0;
     }
     __syncthreads();
+    CHOL_TS(0);
 
-    for (int p = 0; p < np; ++p) {
+    for (int p = -1; p < np; ++p) {  // p = -1: only the factor of diagonal block 0
         const int p16 = 16 * p;
-        double* Di = Dinv + p * 256;
-        // (1) wave 0: upper Cholesky of the 16x16 diagonal block and its inverse, in registers
-        if (wv == 0) {
-            const int j = lane & 15;
-            double col[16];
+        const double* Di = Dd + (p & 1) * 256;
+        const int* bd = bad + (p & 1) * 16;
+        // (1) strip R[p][jb] = D_p^-T W[p][jb] (0 for rows that broke down), to R and the LDS strip
+        if (p >= 0) {
+            double x[4];
 #pragma unroll
-            for (int i = 0; i < 16; ++i) col[i] = W[(int64_t)(p16 + i) * LP + p16 + j];  // D[i][j]
-            int badmask = 0;
+            for (int kk = 0; kk < 4; ++kk) x[kk] = Di[(4 * kk + h) * 16 + r];
+            int zero_rows = 0;
 #pragma unroll
-            for (int k = 0; k < 16; ++k) {
-                const int gk = p16 + k;
-                const double dkk = readlane_d(col[k], k);
-                const bool pad = gk >= l;
-                const bool isbad = !pad && (!(dkk > tol * d0[gk]) || !(d0[gk] > 0.0) || !isfinite(dkk));
-                if (isbad) badmask |= 1 << k;
-                const bool unit = pad || isbad;
-                const double rk = unit ? 1.0 : sqrt(dkk);
-                const double inv = 1.0 / rk;
-                if (j > k) col[k] = unit ? 0.0 : col[k] * inv;
-                if (j == k) col[k] = rk;
+            for (int j = 0; j < 4; ++j) zero_rows |= (bd[h + 4 * j] || p16 + h + 4 * j >= l) << j;
+            for (int jb0 = p + 1 + wv; jb0 < np; jb0 += nw * 4) {
+                double2 y[4][2];
 #pragma unroll
-                for (int i = k + 1; i < 16; ++i) {
-                    const double dki = readlane_d(col[k], i);  // D[k][i]
-                    if (j >= i) col[i] -= dki * col[k];
+                for (int b = 0; b < 4; ++b) {
+                    const int jb = jb0 + nw * b;
+                    if (jb < np) {
+                        const double* src = wtile(W, np, p, jb, lane);
+                        y[b][0] = *reinterpret_cast<const double2*>(src);
+                        y[b][1] = *reinterpret_cast<const double2*>(src + 2);
+                    }
                 }
-            }
-            // zero the strictly lower part of this column (it held the symmetric copy)
 #pragma unroll
-            for (int i = 0; i < 16; ++i)
-                if (i > j) col[i] = 0.0;
-            // Dinv column j by back substitution: x[i] = -(sum_{k>i} D[i][k] x[k]) / D[i][i]
-            double x[16];
+                for (int b = 0; b < 4; ++b) {
+                    const int jb = jb0 + nw * b;
+                    if (jb < np) {
+                        f64x4 acc = MD::zero();
+                        acc = MD::mma(x[0], y[b][0].x, acc);
+                        acc = MD::mma(x[1], y[b][0].y, acc);
+                        acc = MD::mma(x[2], y[b][1].x, acc);
+                        acc = MD::mma(x[3], y[b][1].y, acc);
 #pragma unroll
-            for (int i = 15; i >= 0; --i) {
-                double s = 0.0;
-#pragma unroll
-                for (int k = i + 1; k < 16; ++k) s += readlane_d(col[i], k) * x[k];  // D[i][k] from lane k
-                const double dii = readlane_d(col[i], i);
-                x[i] = (i == j) ? 1.0 / dii : ((i < j) ? -s / dii : 0.0);
-            }
-            if (lane < 16) {
-#pragma unroll
-                for (int i = 0; i < 16; ++i) {
-                    Di[i * 16 + j] = x[i];
-                    R[(int64_t)(p16 + i) * LP + p16 + j] = col[i];
+                        for (int j = 0; j < 4; ++j) {
+                            const int i = h + 4 * j;
+                            const double v = ((zero_rows >> j) & 1) ? 0.0 : acc[j];
+                            R[(int64_t)(p16 + i) * LP + 16 * jb + r] = v;
+                            Rs[i * ldr + 16 * jb + r] = v;
+                        }
+                    }
                 }
-            }
-            if (lane < 16) bad[lane] = (badmask >> lane) & 1;
-            if (lane == 0 && badmask) {
-                atomicAdd(flag, __popc(badmask));
-                for (int k = 0; k < 16; ++k)
-                    if (badmask & (1 << k)) colflag[p16 + k] = 1;
             }
         }
         __syncthreads();
-        // (2) strip: R[p][jb] = Dinv^T W[p][jb], or 0 for rows that broke down (one wave per block)
-        for (int jb = p + 1 + wv; jb < np; jb += nw) {
-            f64x4 acc = MD::zero();
-            acc = mma_tn16(Di, 16, W + (int64_t)p16 * LP + 16 * jb, LP, acc, r, h);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int i = MD::row(h, j);
-                R[(int64_t)(p16 + i) * LP + 16 * jb + r] = (bad[i] || p16 + i >= l) ? 0.0 : acc[j];
-            }
-        }
-        __syncthreads();
-        // (3) trailing update W[ib][jb] -= R[p][ib]^T R[p][jb], p < ib <= jb
+        if (p >= 0) CHOL_TS(1 + 2 * p);
+        // (2) trailing update W[ib][jb] -= R[p][ib]^T R[p][jb], p < ib <= jb.  Tile (p+1, p+1) goes to
+        // wave 0, which then factors it (look-ahead); the other tiles to waves 1.., software-pipelined
+        // in batches of B (loads of batch i+1 in flight while batch i is updated and stored).
         const int nt2 = np - p - 1;
-        const int ntri = nt2 * (nt2 + 1) / 2;
-        for (int t = wv; t < ntri; t += nw) {
-            int rem = t, ib = 0;
-            while (rem >= nt2 - ib) {
-                rem -= nt2 - ib;
-                ++ib;
-            }
-            const int jb = ib + rem + p + 1;
-            ib += p + 1;
-            f64x4 acc = MD::zero();
-            acc = mma_tn16(R + (int64_t)p16 * LP + 16 * ib, LP, R + (int64_t)p16 * LP + 16 * jb, LP, acc, r, h);
+        if (nt2 > 0) {
+            if (wv == 0) {
+                const int b1 = p + 1;
+                const double* src = wtile(W, np, b1, b1, lane);
+                const double2 w0 = *reinterpret_cast<const double2*>(src);
+                const double2 w1 = *reinterpret_cast<const double2*>(src + 2);
+                f64x4 acc = MD::zero();
+                if (p >= 0) {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int i = MD::row(h, j);
-                W[(int64_t)(16 * ib + i) * LP + 16 * jb + r] -= acc[j];
+                    for (int kk = 0; kk < 4; ++kk)
+                        acc = MD::mma(Rs[(4 * kk + h) * ldr + 16 * b1 + r], Rs[(4 * kk + h) * ldr + 16 * b1 + r], acc);
+                }
+                Tsc[h * 16 + r] = w0.x - acc[0];
+                Tsc[(h + 4) * 16 + r] = w0.y - acc[1];
+                Tsc[(h + 8) * 16 + r] = w1.x - acc[2];
+                Tsc[(h + 12) * 16 + r] = w1.y - acc[3];
+                __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's LDS stores landed
+                __builtin_amdgcn_wave_barrier();
+                double col[16];
+#pragma unroll
+                for (int i = 0; i < 16; ++i) col[i] = Tsc[i * 16 + r];
+                chol_diag16(col, 16 * b1, l, LP, tol, d0, Dd + (b1 & 1) * 256, bad + (b1 & 1) * 16, R, Rinv,
+                            colflag, flag, lane);
+            } else if (p >= 0) {
+                // local tile t of the (nt2 x nt2) upper triangle; t = 0 is wave 0's
+                TriWalk tw(wv, nt2);
+                double2 wa[B][2], wb[B][2];
+                int ta[B], tb[B];
+                auto load = [&](double2 (&w)[B][2], int (&tt)[B]) {
+#pragma unroll
+                    for (int b = 0; b < B; ++b) {
+                        tt[b] = tw.ib < nt2 ? tw.ib * 64 + tw.jb : -1;
+                        if (tw.ib < nt2) {
+                            const double* src = wtile(W, np, p + 1 + tw.ib, p + 1 + tw.jb, lane);
+                            w[b][0] = *reinterpret_cast<const double2*>(src);
+                            w[b][1] = *reinterpret_cast<const double2*>(src + 2);
+                        }
+                        tw.advance(nw - 1);
+                    }
+                };
+                auto update = [&](double2 (&w)[B][2], int (&tt)[B]) {
+#pragma unroll
+                    for (int b = 0; b < B; ++b)
+                        if (tt[b] >= 0) {
+                            const int ib = p + 1 + (tt[b] >> 6), jb = p + 1 + (tt[b] & 63);
+                            f64x4 acc = MD::zero();
+#pragma unroll
+                            for (int kk = 0; kk < 4; ++kk)
+                                acc = MD::mma(Rs[(4 * kk + h) * ldr + 16 * ib + r], Rs[(4 * kk + h) * ldr + 16 * jb + r],
+                                              acc);
+                            double* dst = wtile(W, np, ib, jb, lane);
+                            *reinterpret_cast<double2*>(dst) = make_double2(w[b][0].x - acc[0], w[b][0].y - acc[1]);
+                            *reinterpret_cast<double2*>(dst + 2) = make_double2(w[b][1].x - acc[2], w[b][1].y - acc[3]);
+                        }
+                };
+                load(wa, ta);
+                for (;;) {
+                    if (ta[0] < 0) break;
+                    load(wb, tb);
+                    update(wa, ta);
+                    if (tb[0] < 0) break;
+                    load(wa, ta);
+                    update(wb, tb);
+                }
             }
         }
         __syncthreads();
+        if (p >= 0) CHOL_TS(2 + 2 * p);
     }
-    // Rinv, bottom block row first: Rinv[p][p] = Dinv_p, Rinv[p][jb] = -Dinv_p sum_{p<k<=jb} R[p][k] Rinv[k][jb]
-    double* Tw = Tsc + wv * 256;
-    for (int p = np - 1; p >= 0; --p) {
-        const double* Di = Dinv + p * 256;
-        const int p16 = 16 * p;
-        for (int e = tid; e < 256; e += nt) Rinv[(int64_t)(p16 + e / 16) * LP + p16 + e % 16] = Di[e];
-        for (int jb = p + 1 + wv; jb < np; jb += nw) {
-            f64x4 acc = MD::zero();
-            for (int kb = p + 1; kb <= jb; ++kb)
-                acc = mma_nn16(R + (int64_t)p16 * LP + 16 * kb, LP, Rinv + (int64_t)(16 * kb) * LP + 16 * jb, LP, acc,
-                               r, h);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) Tw[MD::row(h, j) * 16 + r] = acc[j];
-            __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the wave's LDS stores landed
-            __builtin_amdgcn_wave_barrier();
-            f64x4 o = MD::zero();
-            o = mma_nn16(Di, 16, Tw, 16, o, r, h);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) Rinv[(int64_t)(p16 + MD::row(h, j)) * LP + 16 * jb + r] = -o[j];
-            __builtin_amdgcn_wave_barrier();
-        }
-        __syncthreads();
-    }
-    if (Rinv32)
-        for (int64_t e = tid; e < L2; e += nt) Rinv32[e] = (float)Rinv[e];
 }
 
 size_t chol_lds_bytes(int LP) {
-    const int np = LP / 16;
-    return (size_t)np * 256 * 8 + (size_t)LP * 8 + (size_t)(kCholThreads / 64) * 256 * 8 + 16 * 4 + 64;
+    return (size_t)512 * 8 + (size_t)LP * 8 + (size_t)16 * (LP + kCholPad) * 8 + 256 * 8 + 32 * 4 + 64;
+}
+
+// R^-1 = blocked back substitution, one workgroup (4 waves) per 16-column block jb, all block
+// columns in parallel:  X[jb] = D_jb^-1,  X[p] = -D_p^-1 T[p],  T[p] = sum_{p<k<=jb} R[p][k] X[k].
+// Right-looking: as soon as X[k] is known every wave adds R[p][k] X[k] to the accumulators T[p] it
+// owns (p = wave + 4 s, in registers), so each step is one MFMA group per owned block, one 16x16
+// product on the owner wave and ONE barrier (X double-buffered in LDS); the R tiles of the next step are loaded a step ahead.
+// (An accumulator in MFMA output layout -- row h + 4 j, column r in lane (r, h) -- is already the
+// B operand of the next product: rows 4 kk + h.)  Also: zeros below the block diagonal of R and
+// R^-1, and the fp32 copy of this block column of R^-1.
+constexpr int kRinvSlots = 8;  // LP <= 512: 32 block rows over 4 waves
+
+__global__ __launch_bounds__(256) void rinv_wide_kernel(int LP, double* __restrict__ R, double* __restrict__ Rinv,
+                                                        float* __restrict__ Rinv32, const int* __restrict__ pred) {
+    if (pred && *pred == 0) return;
+    __shared__ double Xs[2][256];  // X[k] of the current step (buffer k & 1), row-major
+    const int jb = blockIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int r = lane & 15, h = lane >> 4;
+    const int c0 = 16 * jb;
+    // below the block diagonal: zeros
+    for (int e = tid; e < (LP - c0 - 16) * 16; e += 256) {
+        const int i = c0 + 16 + e / 16, c = c0 + e % 16;
+        R[(int64_t)i * LP + c] = 0.0;
+        Rinv[(int64_t)i * LP + c] = 0.0;
+        if (Rinv32) Rinv32[(int64_t)i * LP + c] = 0.0f;
+    }
+    f64x4 T[kRinvSlots];
+    double Rc[kRinvSlots][4], Rn[kRinvSlots][4], Dn[4];
+#pragma unroll
+    for (int s = 0; s < kRinvSlots; ++s) T[s] = MD::zero();
+    // R[p][k] A-operands (row r, column 4 kk + h) of the step k for the blocks p < k this wave owns
+    auto load_r = [&](double (&dst)[kRinvSlots][4], int k) {
+#pragma unroll
+        for (int s = 0; s < kRinvSlots; ++s) {
+            const int p = wv + 4 * s;
+            if (p < k) {
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk) dst[s][kk] = R[(int64_t)(16 * p + r) * LP + 16 * k + 4 * kk + h];
+            }
+        }
+    };
+    // D_k^-1 as the A operand (row r, column 4 kk + h), loaded one owned step ahead
+    auto load_d = [&](int k) {
+        if (k >= 0) {
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) Dn[kk] = Rinv[(int64_t)(16 * k + r) * LP + 16 * k + 4 * kk + h];
+        }
+    };
+    {
+        int k1 = jb - 1;
+        while (k1 >= 0 && (k1 & 3) != wv) --k1;
+        load_d(k1);
+    }
+    load_r(Rc, jb);
+    for (int k = jb; k >= 0; --k) {
+        const int own = k & 3;
+        if (k > 0) load_r(Rn, k - 1);
+        if (wv == own) {
+            f64x4 x;
+            if (k == jb) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) x[j] = Rinv[(int64_t)(c0 + h + 4 * j) * LP + c0 + r];
+            } else {
+                f64x4 t = MD::zero();
+#pragma unroll
+                for (int s = 0; s < kRinvSlots; ++s)
+                    if (wv + 4 * s == k) t = T[s];
+                f64x4 o = MD::zero();
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk) o = MD::mma(Dn[kk], t[kk], o);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) x[j] = -o[j];
+                load_d(k - 4);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int i = h + 4 * j;
+                Xs[k & 1][i * 16 + r] = x[j];
+                if (k != jb) Rinv[(int64_t)(16 * k + i) * LP + c0 + r] = x[j];
+                if (Rinv32) Rinv32[(int64_t)(16 * k + i) * LP + c0 + r] = (float)x[j];
+            }
+        }
+        __syncthreads();
+        if (k > 0) {
+            double xb[4];
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) xb[kk] = Xs[k & 1][(4 * kk + h) * 16 + r];
+#pragma unroll
+            for (int s = 0; s < kRinvSlots; ++s) {
+                const int p = wv + 4 * s;
+                if (p < k) {
+#pragma unroll
+                    for (int kk = 0; kk < 4; ++kk) T[s] = MD::mma(Rc[s][kk], xb[kk], T[s]);
+                }
+            }
+#pragma unroll
+            for (int s = 0; s < kRinvSlots; ++s)
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk) Rc[s][kk] = Rn[s][kk];
+        }
+    }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -562,7 +793,10 @@ hipError_t launch_chol_wide(const double* G, int l, int LP, double tol, double* 
                             int* colflag, int* flag, double* work, const int* pred, hipStream_t s) {
     if (LP % 16 || LP > 512) return hipErrorInvalidValue;
     hipLaunchKernelGGL(chol_wide_kernel, dim3(1), dim3(kCholThreads), chol_lds_bytes(LP), s, G, l, LP, tol, work, R,
-                       Rinv, Rinv32, colflag, flag, pred);
+                       Rinv, colflag, flag, pred);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(rinv_wide_kernel, dim3(LP / 16), dim3(256), 0, s, LP, R, Rinv, Rinv32, pred);
     return hipGetLastError();
 }
 
@@ -635,3 +869,23 @@ RSVD_INST(double)
 #undef RSVD_INST
 
 }  // namespace rsvd
+
+#ifdef RSVD_CHOL_PROF
+namespace rsvd {
+void chol_prof_dump(int LP) {
+    long long t[256];
+    (void)hipMemcpyFromSymbol(t, HIP_SYMBOL(g_chol_prof), sizeof(t));
+    const int np = LP / 16;
+    double strip = 0, trail = 0;
+    const double us = 0.01;  // wall_clock64 runs at 100 MHz
+    long long prev = t[0];
+    for (int p = 0; p < np; ++p) {
+        strip += (t[1 + 2 * p] - prev) * us;
+        trail += (t[2 + 2 * p] - t[1 + 2 * p]) * us;
+        prev = t[2 + 2 * p];
+    }
+    printf("  LP=%d factor phases (us): init+diag0 %.1f strip %.1f trailing+diag %.1f\n", LP, (t[0] - t[97]) * us,
+           strip, trail);
+}
+}  // namespace rsvd
+#endif

@@ -118,6 +118,9 @@ static double* spd(int LP, int l) {  // G = X^T X + I with X random l x l
     return p;
 }
 
+#ifdef RSVD_CHOL_PROF
+namespace rsvd { void chol_prof_dump(int LP); }
+#endif
 static void bench_chol() {
     for (int LP : {64, 128, 256, 512}) {
         double* G = spd(LP, LP);
@@ -149,6 +152,9 @@ static void bench_chol() {
                 ng += hG[(size_t)i * LP + j] * hG[(size_t)i * LP + j];
                 e2 += (s2 - (i == j)) * (s2 - (i == j));
             }
+#ifdef RSVD_CHOL_PROF
+        rsvd::chol_prof_dump(LP);
+#endif
         printf("chol LP=%d: %.1f us   |R^T R - G|/|G| = %.2e  |R Rinv - I| = %.2e\n", LP, t, sqrt(e1 / ng), sqrt(e2));
         CK(hipFree(G)); CK(hipFree(R)); CK(hipFree(Ri)); CK(hipFree(W)); CK(hipFree(R32)); CK(hipFree(cf)); CK(hipFree(fl));
     }
