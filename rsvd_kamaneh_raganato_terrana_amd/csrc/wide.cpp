@@ -61,7 +61,10 @@ struct WideLayout {
         npad = rup(n, 32);
         int64_t pslab = 1;
         if (lowp) {
-            const bool v2 = d->dtype == RSVD_BF16 && a_aligned && d->lda % 8 == 0 && m >= 8;
+            // (m a multiple of the 16-B chunk: a chunk is either inside A's rows or wholly past them,
+            // where the clamped read lands on zero S rows / unstored output rows)
+            const bool v2 = a_aligned && ((d->dtype == RSVD_BF16 && d->lda % 8 == 0 && m % 8 == 0 && m >= 8) ||
+                                          (d->dtype == RSVD_FP8_E4M3 && d->lda % 16 == 0 && m % 16 == 0 && m >= 16));
             wnn = plan_wproj(m, n, LP, v2);
             wtn = plan_wproj(n, m, LP, v2);
             pslab = std::max<int64_t>(wnn.splits > 1 ? wnn.splits * m : 0, wtn.splits > 1 ? wtn.splits * n : 0);

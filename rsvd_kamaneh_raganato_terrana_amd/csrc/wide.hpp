@@ -28,9 +28,10 @@ struct WProjPlan {
     int splits;      // K splits (1 = straight into the output panel)
     int64_t chunk;   // K range per workgroup (multiple of 32)
     int blocks;      // output row blocks
-    bool v2;         // LDS-DMA pipelined kernel (bf16 A, LP >= 128, 16-B aligned columns, m >= 8)
+    bool v2;         // LDS-DMA pipelined kernel (bf16 / e4m3 A, LP >= 128, 16-B aligned columns)
 };
-// v2 requires: bf16 A with lda % 8 == 0 and a 16-B aligned base, m >= 8, and S panels zero-padded
+// v2 requires: a 16-B aligned base, bf16 A with lda and m multiples of 8 or e4m3 A with lda and m
+// multiples of 16, and S panels zero-padded
 // to a multiple of 32 rows (the engine allocates them so).
 WProjPlan plan_wproj(int64_t rows_out, int64_t K, int LP, bool v2 = false);
 // NN: Y (m x LP, fp32) = A (m x n) * S       S = n x LP bf16 panel(s)      src/rSVD.cpp:59,66

@@ -276,21 +276,29 @@ template <> struct W2Cfg<128> { static constexpr int WR = 8, WC = 1, G = 8; };
 template <> struct W2Cfg<256> { static constexpr int WR = 4, WC = 2, G = 8; };
 template <> struct W2Cfg<512> { static constexpr int WR = 2, WC = 4, G = 8; };
 
-template <int LP, bool SPLIT>
+template <int LP, bool SPLIT, bool FP8>
 struct W2Shape {
     static constexpr int WR = W2Cfg<LP>::WR, WC = W2Cfg<LP>::WC, G = W2Cfg<LP>::G;
     static constexpr int WI = WR * 64;            // output rows per workgroup
     static constexpr int NS = SPLIT ? 2 : 1;
     static constexpr int SBYTES = KS * LP * 2;    // one S panel tile
-    static constexpr int ABYTES = KS * WI * 2;    // the A tile
+    static constexpr int ABYTES = KS * WI * (FP8 ? 1 : 2);  // the A tile
     static constexpr int STAGE = NS * SBYTES + ABYTES;
     static constexpr int NST0 = 147456 / STAGE;
     static constexpr int NST = NST0 > 4 ? 4 : (NST0 < 2 ? 2 : NST0);
     static constexpr int SGL = SBYTES / 8192;     // glds per thread per S tile (512 threads x 16 B)
-    static constexpr int AGL = ABYTES / 8192;
-    static constexpr int GL = NS * SGL + AGL;     // glds per thread per stage
+    static constexpr int NAI = ABYTES / 1024;     // wave-level glds instructions per A tile
+    static constexpr int AGL = NAI / 8;           // ... per wave (every wave)
+    static constexpr int AEX = NAI % 8;           // waves 0 .. AEX-1 issue one more
+    static constexpr int GL = NS * SGL + AGL;     // glds per thread per stage (waves >= AEX)
     static constexpr size_t LDS = (size_t)NST * STAGE;
 };
+
+// fp8 A images: 16-B unit swizzles that keep the fragment reads conflict-free.  NN [32 k][WI i]
+// bytes, read by ds_read_b64_tr_b8 (16 lanes = 8 k-rows x 16 bytes; lane r supplies row r >> 1,
+// byte 8 (r & 1), and receives the 8 k of column r); TN [WI j][32 k] bytes read by ds_read_b64.
+template <int WI>
+__device__ __forceinline__ int swz8(int k) { return WI == 128 ? ((k >> 1) & 7) : (k & 15); }
 
 __device__ __forceinline__ int swz(int row) { return 2 * ((row & 3) | (((row >> 3) & 1) << 2)); }
 
@@ -328,6 +336,7 @@ __device__ __forceinline__ void wait_lgkm0(i32x2& a, i32x2& b, i32x2& c, i32x2& 
 __device__ __forceinline__ void wait_lgkm0(i32x2& a, i32x2& b) {
     asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a), "+v"(b)::"memory");
 }
+__device__ __forceinline__ void wait_lgkm0(i32x2& a) { asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a)::"memory"); }
 __device__ __forceinline__ void wait_lgkm0(i32x4& a) { asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a)::"memory"); }
 
 template <int N>
@@ -336,12 +345,30 @@ __device__ __forceinline__ void wait_vm() {  // s_waitcnt vmcnt(N), expcnt / lgk
     __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | (0x7 << 4) | (0xF << 8));
 }
 
-template <bool NN, int LP, bool SPLIT>
-__global__ __launch_bounds__(512) void wproj2_kernel(const bf16_t* __restrict__ A, int64_t lda, int64_t rows_out,
+__device__ __forceinline__ i32x2 tr8_read_a(uint32_t a) {
+    i32x2 v;
+    asm volatile("ds_read_b64_tr_b8 %0, %1" : "=v"(v) : "v"(a));
+    return v;
+}
+__device__ __forceinline__ i32x2 read64_a(uint32_t a) {
+    i32x2 v;
+    asm volatile("ds_read_b64 %0, %1" : "=v"(v) : "v"(a));
+    return v;
+}
+// 8 e4m3 bytes (k order) -> the bf16x8 fragment (exact)
+__device__ __forceinline__ bf16x8_t fp8x8_to_bf16x8(i32x2 v) {
+    const uint2 a = fp8x4_to_bf16x4((uint32_t)v.x), b = fp8x4_to_bf16x4((uint32_t)v.y);
+    return __builtin_bit_cast(bf16x8_t, make_uint4(a.x, a.y, b.x, b.y));
+}
+
+template <bool FP8, bool NN, int LP, bool SPLIT>
+__global__ __launch_bounds__(512) void wproj2_kernel(const void* __restrict__ Av, int64_t lda, int64_t rows_out,
                                                      int64_t K, int64_t arows, const bf16_t* __restrict__ Shi,
                                                      const bf16_t* __restrict__ Slo, float* __restrict__ out,
                                                      int64_t slab_stride, int64_t kchunk, int nrowblk) {
-    typedef W2Shape<LP, SPLIT> SH;
+    typedef W2Shape<LP, SPLIT, FP8> SH;
+    const bf16_t* __restrict__ A = reinterpret_cast<const bf16_t*>(Av);
+    const uint8_t* __restrict__ A8 = reinterpret_cast<const uint8_t*>(Av);
     constexpr int WR = SH::WR, G = SH::G, WI = SH::WI, NS = SH::NS, NST = SH::NST;
     extern __shared__ __attribute__((aligned(1024))) char smem_raw[];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -370,6 +397,34 @@ __global__ __launch_bounds__(512) void wproj2_kernel(const bf16_t* __restrict__ 
             }
         }
         char* at = slot + NS * SH::SBYTES;
+        if constexpr (FP8) {
+#pragma unroll
+            for (int t = 0; t < (SH::NAI + 7) / 8; ++t) {
+                const int gi = t * 8 + w;
+                if (SH::NAI % 8 == 0 || gi < SH::NAI) {
+                    const int u = gi * 64 + lane;
+                    const uint8_t* src;
+                    if (NN) {  // [32 k][WI i] bytes: unit u -> k row, swizzled 16-row chunk
+                        constexpr int CPR = WI / 16;
+                        const int k = u / CPR, cp = u % CPR;
+                        int64_t kk = k0 + k;
+                        kk = kk < K ? kk : K - 1;
+                        int64_t i = row0 + 16 * (cp ^ swz8<WI>(k));
+                        i = (i + 16 <= arows) ? i : arows - 16;
+                        src = A8 + kk * lda + i;
+                    } else {  // [WI j][32 k] bytes: 2 units per column j, swapped on (j >> 3) & 1
+                        const int j = u >> 1, cc = u & 1;
+                        int64_t jc = row0 + j;
+                        jc = jc < rows_out ? jc : rows_out - 1;
+                        int64_t i = k0 + 16 * (cc ^ ((j >> 3) & 1));
+                        i = (i + 16 <= arows) ? i : arows - 16;
+                        src = A8 + jc * lda + i;
+                    }
+                    glds16(src, at + gi * 1024);
+                }
+            }
+            return;
+        }
 #pragma unroll
         for (int t = 0; t < SH::AGL; ++t) {
             const int gi = t * 8 + w;
@@ -406,7 +461,12 @@ __global__ __launch_bounds__(512) void wproj2_kernel(const bf16_t* __restrict__ 
 
     for (int st = 0; st < nsteps; ++st) {
         // stage st has landed once at most the younger stages' glds are outstanding
-        if (st + NST - 2 < nsteps) wait_vm<(NST - 2) * SH::GL>(); else wait_vm<0>();
+        if (st + NST - 2 < nsteps) {
+            if (SH::AEX && w < SH::AEX) wait_vm<(NST - 2) * (SH::GL + 1)>();
+            else wait_vm<(NST - 2) * SH::GL>();
+        } else {
+            wait_vm<0>();
+        }
         __builtin_amdgcn_s_barrier();
         if (st + NST - 1 < nsteps) issue(st + NST - 1);
         const uint32_t slot = lds_addr(smem_raw) + (uint32_t)((st % NST) * SH::STAGE);
@@ -416,7 +476,16 @@ __global__ __launch_bounds__(512) void wproj2_kernel(const bf16_t* __restrict__ 
         i32x4 a4[RT];
 #pragma unroll
         for (int t = 0; t < RT; ++t) {
-            if (NN) {
+            if (FP8) {
+                if (NN) {
+                    const int k = 8 * h + (r >> 1);
+                    const int c = 4 * wr + t;  // 16-row chunk of the tile
+                    a1[t] = tr8_read_a(At + k * WI + 16 * (c ^ swz8<WI>(k)) + 8 * (r & 1));
+                } else {
+                    const int j = wr * 64 + 16 * t + r;
+                    a1[t] = read64_a(At + j * 32 + 8 * (h ^ (2 * ((j >> 3) & 1))));
+                }
+            } else if (NN) {
                 const int col = wr * 64 + 16 * t + 4 * p;  // i within the tile
                 const int k1 = 8 * h + q, k2 = k1 + 4;
                 a1[t] = tr_read_a(At + k1 * (WI * 2) + 16 * ((col >> 3) ^ swz(k1)) + 2 * (col & 7));
@@ -448,9 +517,14 @@ __global__ __launch_bounds__(512) void wproj2_kernel(const bf16_t* __restrict__ 
         wait_b(bb[0]);
 #pragma unroll
         for (int t = 0; t < RT; ++t) {  // (retired by the wait above; these waits are no-ops that pin the order)
-            if (NN) wait_lgkm0(a1[t], a2[t]);
-            else wait_lgkm0(a4[t]);
-            af[t] = NN ? join2(a1[t], a2[t]) : __builtin_bit_cast(bf16x8_t, a4[t]);
+            if (FP8) {
+                wait_lgkm0(a1[t]);
+                af[t] = fp8x8_to_bf16x8(a1[t]);
+            } else {
+                if (NN) wait_lgkm0(a1[t], a2[t]);
+                else wait_lgkm0(a4[t]);
+                af[t] = NN ? join2(a1[t], a2[t]) : __builtin_bit_cast(bf16x8_t, a4[t]);
+            }
         }
 #pragma unroll
         for (int g = 0; g < G; ++g) {
@@ -482,15 +556,15 @@ __global__ __launch_bounds__(512) void wproj2_kernel(const bf16_t* __restrict__ 
         }
 }
 
-template <bool NN, int LP, bool SPLIT>
+template <bool FP8, bool NN, int LP, bool SPLIT>
 hipError_t wproj2_go(const void* A, int64_t lda, int64_t m, int64_t n, const bf16_t* Shi, const bf16_t* Slo,
                      const WProjPlan& p, float* slabs, float* Out, hipStream_t s, hipEvent_t done) {
-    typedef W2Shape<LP, SPLIT> SH;
+    typedef W2Shape<LP, SPLIT, FP8> SH;
     const int64_t rows_out = NN ? m : n, K = NN ? n : m;
     float* o = p.splits == 1 ? Out : slabs;
     const int64_t stride = rows_out * LP;
-    hipLaunchKernelGGL((wproj2_kernel<NN, LP, SPLIT>), dim3(p.blocks * p.splits), dim3(512), SH::LDS, s,
-                       reinterpret_cast<const bf16_t*>(A), lda, rows_out, K, m, Shi, Slo, o, stride, p.chunk, p.blocks);
+    hipLaunchKernelGGL((wproj2_kernel<FP8, NN, LP, SPLIT>), dim3(p.blocks * p.splits), dim3(512), SH::LDS, s, A, lda,
+                       rows_out, K, m, Shi, Slo, o, stride, p.chunk, p.blocks);
     hipError_t e = hipGetLastError();
     if (e == hipSuccess && done) e = hipEventRecord(done, s);
     if (e != hipSuccess || p.splits == 1) return e;
@@ -520,10 +594,16 @@ hipError_t wproj_lp(int nn, int fp8, const void* A, int64_t lda, int64_t m, int6
     const bool split = Slo != nullptr;
     if constexpr (LP >= 128) {
         if (p.v2) {
-            if (nn) return split ? wproj2_go<true, LP, true>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d)
-                                 : wproj2_go<true, LP, false>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d);
-            return split ? wproj2_go<false, LP, true>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d)
-                         : wproj2_go<false, LP, false>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d);
+#define GO2(F)                                                                                   \
+    {                                                                                            \
+        if (nn) return split ? wproj2_go<F, true, LP, true>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d) \
+                             : wproj2_go<F, true, LP, false>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d); \
+        return split ? wproj2_go<F, false, LP, true>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d)        \
+                     : wproj2_go<F, false, LP, false>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d);      \
+    }
+            if (fp8) GO2(true);
+            GO2(false);
+#undef GO2
         }
     }
 #define GO(F, N, SP) return wproj_go<F, N, LP, SP>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d)

@@ -206,7 +206,7 @@ static void bench_proj() {
         bf16_t* Sl = dev_random<bf16_t>((size_t)mx * c.LP);
         float* Out;
         CK(hipMalloc(&Out, (size_t)mx * c.LP * 4));
-        for (int v2 = 0; v2 < (c.fp8 ? 1 : 2); ++v2) {
+        for (int v2 = 0; v2 < 2; ++v2) {
             WProjPlan pnn = plan_wproj(c.m, c.n, c.LP, v2), ptn = plan_wproj(c.n, c.m, c.LP, v2);
             float* slabs;
             CK(hipMalloc(&slabs, (size_t)std::max<int64_t>(pnn.splits * c.m, ptn.splits * c.n) * c.LP * 4));
@@ -272,13 +272,23 @@ static uint16_t f2bf_h(float x) {
     return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
 }
 
-static void check_proj() {  // v2 (LDS-DMA) against v1 on random bf16 data
+static void check_proj() {  // v2 (LDS-DMA) against v1 on random bf16 / e4m3 data
+    for (int fp8 = 0; fp8 < 2; ++fp8)
     for (int LP : {128, 256, 512}) {
-        const int64_t m = 2048 + 64, n = 1024 + 32;
+        const int64_t m = 2048 + 64 + 16 * fp8, n = 1024 + 32 + 3 * fp8;
         std::vector<uint16_t> hA((size_t)m * n), hS((size_t)std::max(m, n) * LP), hL(hS.size());
         std::mt19937 g(7);
         std::normal_distribution<float> d;
-        for (auto& x : hA) x = f2bf_h(d(g));
+        if (fp8) {  // random e4m3 codes, no NaN (0x7f / 0xff)
+            uint8_t* b = reinterpret_cast<uint8_t*>(hA.data());
+            for (size_t i = 0; i < (size_t)m * n; ++i) {
+                uint8_t c = (uint8_t)(g() & 0xff);
+                if ((c & 0x7f) == 0x7f) c ^= 1;
+                b[i] = c;
+            }
+        } else {
+            for (auto& x : hA) x = f2bf_h(d(g));
+        }
         for (size_t i = 0; i < hS.size(); ++i) {
             hS[i] = f2bf_h(d(g));
             hL[i] = f2bf_h(d(g) * 1e-3f);
@@ -304,8 +314,8 @@ static void check_proj() {  // v2 (LDS-DMA) against v1 on random bf16 data
             CK(hipMemcpy(Sl, hL.data(), rows_s * LP * 2, hipMemcpyHostToDevice));
             const int64_t ro = nn ? m : n, K = nn ? n : m;
             WProjPlan p1 = plan_wproj(ro, K, LP, false), p2 = plan_wproj(ro, K, LP, true);
-            CK(launch_wproj(nn, 0, A, m, m, n, Sh, Sl, LP, p1, sl, O1, S));
-            CK(launch_wproj(nn, 0, A, m, m, n, Sh, Sl, LP, p2, sl, O2, S));
+            CK(launch_wproj(nn, fp8, A, m, m, n, Sh, Sl, LP, p1, sl, O1, S));
+            CK(launch_wproj(nn, fp8, A, m, m, n, Sh, Sl, LP, p2, sl, O2, S));
             CK(hipStreamSynchronize(S));
             std::vector<float> a(ro * LP), b(ro * LP);
             CK(hipMemcpy(a.data(), O1, a.size() * 4, hipMemcpyDeviceToHost));
@@ -315,8 +325,8 @@ static void check_proj() {  // v2 (LDS-DMA) against v1 on random bf16 data
                 md = std::max(md, (double)fabs(a[i] - b[i]));
                 mx2 = std::max(mx2, (double)fabs(a[i]));
             }
-            printf("check LP=%d %s: max|v1-v2| = %.3e (max|v1| = %.3e) v2 splits=%d chunk=%ld\n", LP, nn ? "NN" : "TN", md,
-                   mx2, p2.splits, (long)p2.chunk);
+            printf("check fp8=%d LP=%d %s: max|v1-v2| = %.3e (max|v1| = %.3e) v2 splits=%d chunk=%ld\n", fp8, LP,
+                   nn ? "NN" : "TN", md, mx2, p2.splits, (long)p2.chunk);
         }
         CK(hipFree(A)); CK(hipFree(Sh)); CK(hipFree(Sl)); CK(hipFree(O1)); CK(hipFree(O2)); CK(hipFree(sl));
     }
