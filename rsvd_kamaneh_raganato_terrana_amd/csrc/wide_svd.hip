@@ -120,15 +120,33 @@ __device__ __forceinline__ void pair_angle(const double* G, int p, int q, double
 size_t block_jacobi_lds(int LP) { return ((size_t)32 * (LP + 1) + 3 * 32 * GS) * sizeof(double); }
 
 // Stage the 32 columns col(0..31) of a column-major LP x LP matrix into LDS rows of pitch LP + 1.
+constexpr int kBJThreads = 512;  // 8 waves: 2 per SIMD for the MFMA phases
+
+// 32 LP / 2 double2: each thread keeps up to 4 loads in flight.
 template <typename F>
 __device__ __forceinline__ void stage_pair(double* Xs, const double* __restrict__ S, int LP, F col) {
     const int XP = LP + 1;
     const int per = LP / 2;  // double2 per column
-    for (int e = threadIdx.x; e < 32 * per; e += 256) {
-        const int k = e / per, i = 2 * (e % per);
-        const double2 v = *reinterpret_cast<const double2*>(S + (int64_t)col(k) * LP + i);
-        Xs[k * XP + i] = v.x;
-        Xs[k * XP + i + 1] = v.y;
+    const int tot = 32 * per;
+    for (int e0 = threadIdx.x; e0 < tot; e0 += 4 * kBJThreads) {
+        double2 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int e = e0 + kBJThreads * u;
+            if (e < tot) {
+                const int k = e / per, i = 2 * (e % per);
+                v[u] = *reinterpret_cast<const double2*>(S + (int64_t)col(k) * LP + i);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int e = e0 + kBJThreads * u;
+            if (e < tot) {
+                const int k = e / per, i = 2 * (e % per);
+                Xs[k * XP + i] = v[u].x;
+                Xs[k * XP + i + 1] = v[u].y;
+            }
+        }
     }
 }
 
@@ -137,7 +155,7 @@ template <typename F>
 __device__ __forceinline__ void apply_pair(const double* Xs, const double* Jp, double* __restrict__ D, int LP, F col,
                                            int w, int r, int h) {
     const int XP = LP + 1;
-    for (int it = w; it < LP / 16; it += 4) {
+    for (int it = w; it < LP / 16; it += kBJThreads / 64) {
         const int i0 = 16 * it;
         f64x4 acc0 = MD::zero(), acc1 = MD::zero();
 #pragma unroll
@@ -154,9 +172,50 @@ __device__ __forceinline__ void apply_pair(const double* Xs, const double* Jp, d
     }
 }
 
-__global__ __launch_bounds__(256) void block_jacobi_kernel(const double* __restrict__ R, int l, int LP,
+#ifdef RSVD_BJ_PROF
+__device__ long long g_bj_prof[8];
+#define BJ_T(k)                                                \
+    do {                                                       \
+        if (wg == 0 && tid == 0) {                             \
+            const long long now_ = wall_clock64();             \
+            bj_acc[(k)] += now_ - bj_last;                     \
+            bj_last = now_;                                    \
+        }                                                      \
+    } while (0)
+#else
+#define BJ_T(k) \
+    do {        \
+    } while (0)
+#endif
+
+// The same product with the pair's columns read straight from global memory (column-major source:
+// the 16 lanes of an MFMA row read 128 contiguous bytes of one column), all 8 k-steps in flight.
+template <typename F>
+__device__ __forceinline__ void apply_pair_global(const double* __restrict__ Src, const double* Jp,
+                                                  double* __restrict__ D, int LP, F col, int w, int r, int h) {
+    for (int it = w; it < LP / 16; it += kBJThreads / 64) {
+        const int i0 = 16 * it;
+        double a[8];
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) a[kk] = Src[(int64_t)col(4 * kk + h) * LP + i0 + r];
+        f64x4 acc0 = MD::zero(), acc1 = MD::zero();
+#pragma unroll
+        for (int kk = 0; kk < 8; ++kk) {
+            acc0 = MD::mma(a[kk], Jp[(4 * kk + h) * GS + r], acc0);
+            acc1 = MD::mma(a[kk], Jp[(4 * kk + h) * GS + 16 + r], acc1);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            D[(int64_t)col(r) * LP + i0 + MD::row(h, j)] = acc0[j];
+            D[(int64_t)col(16 + r) * LP + i0 + MD::row(h, j)] = acc1[j];
+        }
+    }
+}
+
+__global__ __launch_bounds__(kBJThreads) void block_jacobi_kernel(const double* __restrict__ R, int l, int LP,
                                                            double* __restrict__ Xb, double* __restrict__ Jb,
-                                                           unsigned* __restrict__ sync, int* __restrict__ info) {
+                                                           double* __restrict__ scratch, unsigned* __restrict__ sync,
+                                                           int* __restrict__ info) {
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
     const int XP = LP + 1;
     double* Xs = reinterpret_cast<double*>(smem_raw);  // [32][LP + 1]: the pair's columns
@@ -165,40 +224,50 @@ __global__ __launch_bounds__(256) void block_jacobi_kernel(const double* __restr
     double* Jp = Gb + 32 * GS;                         // [32][GS] accumulated inner rotation
     __shared__ int flags[8];
     __shared__ double fro;
+    __shared__ double Ang[32];  // c, s of the 16 pairs of an inner round
+    __shared__ int Rot[16];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int r = lane & 15, h = lane >> 4;
     const int nwg = gridDim.x, wg = blockIdx.x;
     const int NB = LP / 16;
     const int64_t L2 = (int64_t)LP * LP;
     const double tol = (double)l * kEps, tol2 = tol * tol, quad2 = 1e-16;
+#ifdef RSVD_BJ_PROF
+    long long bj_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    long long bj_last = wall_clock64();
+#endif
 
-    // X (column-major, X[c][i] = W[i][c] = R[c][i]) and J = I into buffer 0: rows of this workgroup
-    for (int64_t e = (int64_t)wg * 256 + tid; e < L2; e += (int64_t)nwg * 256) {
-        const int c = (int)(e / LP), i = (int)(e % LP);
-        Xb[e] = (c < l && i < l) ? R[e] : 0.0;
-        Jb[e] = (c == i && c < l) ? 1.0 : 0.0;
-    }
-    // ||W||_F^2 (every workgroup, same order) -> negligible-column threshold
-    if (tid == 0) fro = 0.0;
-    __syncthreads();
+    // X (column-major, X[c][i] = W[i][c] = R[c][i]) and J = I into buffer 0: columns of this
+    // workgroup; this workgroup's part of ||W||_F^2 to scratch[wg]
     {
         double part = 0.0;
-        for (int64_t e = tid; e < L2; e += 256) {
-            const int c = (int)(e / LP), i = (int)(e % LP);
-            const double v = (c < l && i < l) ? R[e] : 0.0;
-            part += v * v;
+        for (int c = wg; c < LP; c += nwg) {
+            const int64_t o = (int64_t)c * LP;
+            for (int i = tid; i < LP; i += kBJThreads) {
+                const double v = (c < l && i < l) ? R[o + i] : 0.0;
+                Xb[o + i] = v;
+                Jb[o + i] = (c == i && c < l) ? 1.0 : 0.0;
+                part += v * v;
+            }
         }
+        if (tid == 0) fro = 0.0;
+        __syncthreads();
         part = warp_sum(part);
         if (lane == 0) atomicAdd(&fro, part);
+        __syncthreads();
+        if (tid == 0) scratch[wg] = fro;
     }
-    __syncthreads();
-    const double negl = fro * (double)l * l * kEps * kEps;
     unsigned bar = 0;
     if (!grid_barrier(sync, (unsigned)nwg * ++bar)) {
         if (tid == 0) info[2] = 1;
         return;
     }
+    // ||W||_F^2 in a fixed order (every workgroup the same value) -> negligible-column threshold
+    double frot = 0.0;
+    for (int k = 0; k < nwg; ++k) frot += scratch[k];
+    const double negl = frot * (double)l * l * kEps * kEps;
 
+    BJ_T(0);
     int par = 0, sweeps = 0;
     for (int sweep = 0; sweep < kMaxSweeps; ++sweep) {
         for (int round = 0; round < NB - 1; ++round) {
@@ -212,25 +281,35 @@ __global__ __launch_bounds__(256) void block_jacobi_kernel(const double* __restr
             // 1. the pair's columns of X into LDS
             stage_pair(Xs, Xsrc, LP, col);
             if (tid < 8) flags[tid] = 0;
-            for (int e = tid; e < 32 * 32; e += 256) Jp[(e / 32) * GS + e % 32] = (e / 32 == e % 32) ? 1.0 : 0.0;
+            for (int e = tid; e < 32 * 32; e += kBJThreads) Jp[(e / 32) * GS + e % 32] = (e / 32 == e % 32) ? 1.0 : 0.0;
             __syncthreads();
-            // 2. Gp = X_pair^T X_pair: wave w -> tile (w >> 1, w & 1), four independent MFMA chains
+            BJ_T(1);
+            // 2. Gp = X_pair^T X_pair: wave w -> tile ((w >> 1) & 1, w & 1) over row half w >> 2 (four
+            //    independent MFMA chains); the halves meet in Ga (half 0) + Gb (half 1)
             {
-                const int ta = w >> 1, tb = w & 1;
+                const int ta = (w >> 1) & 1, tb = w & 1, half = w >> 2;
                 const double* xa = Xs + (16 * ta + r) * XP + h;
                 const double* xb = Xs + (16 * tb + r) * XP + h;
                 f64x4 acc[4] = {MD::zero(), MD::zero(), MD::zero(), MD::zero()};
-                for (int i0 = 0; i0 < LP; i0 += 16) {
+                const int ibeg = half * (LP / 2), iend = ibeg + LP / 2;
+                for (int i0 = ibeg; i0 < iend; i0 += 16) {
 #pragma unroll
                     for (int u = 0; u < 4; ++u) acc[u] = MD::mma(xa[i0 + 4 * u], xb[i0 + 4 * u], acc[u]);
                 }
+                double* Gd = half ? Gb : Ga;
 #pragma unroll
                 for (int j = 0; j < 4; ++j)
-                    Ga[(16 * ta + MD::row(h, j)) * GS + 16 * tb + r] = (acc[0][j] + acc[1][j]) + (acc[2][j] + acc[3][j]);
+                    Gd[(16 * ta + MD::row(h, j)) * GS + 16 * tb + r] = (acc[0][j] + acc[1][j]) + (acc[2][j] + acc[3][j]);
             }
             __syncthreads();
+            for (int e = tid; e < 32 * 32; e += kBJThreads) {
+                const int i = e / 32, j = e % 32;
+                Ga[i * GS + j] += Gb[i * GS + j];
+            }
+            __syncthreads();
+            BJ_T(2);
             // 3. convergence test on the fresh Gram
-            for (int e = tid; e < 32 * 32; e += 256) {
+            for (int e = tid; e < 32 * 32; e += kBJThreads) {
                 const int i = e / 32, j = e % 32;
                 if (i < j) {
                     const double a = Ga[i * GS + i], b = Ga[j * GS + j], g = Ga[i * GS + j];
@@ -246,38 +325,47 @@ __global__ __launch_bounds__(256) void block_jacobi_kernel(const double* __restr
                     __hip_atomic_store(sync + 4 + sweep, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     if (flags[1]) __hip_atomic_store(sync + 36 + sweep, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
-                // 4. inner cyclic Jacobi on Gp: thread (k, k2) rotates the 2x2 block (pair k rows, pair k2
-                //    columns) from both sides into the other G buffer -- one barrier per inner round
-                const int k = tid >> 4, k2 = tid & 15;
+                // 4. inner cyclic Jacobi on Gp, two phases per inner round: (a) lanes 0..15 compute the
+                //    angles of the 16 disjoint pairs into LDS; (b) thread (k, k2) < 256 rotates the 2x2 block
+                //    (pair k rows, pair k2 columns) from both sides into the other G buffer, while threads
+                //    256.. rotate the columns of Jp (Jp <- Jp J)
+                const int k = (tid >> 4) & 15, k2 = tid & 15;
                 double* cur = Ga;
                 double* nxt = Gb;
                 for (int isw = 0; isw < kInnerSweeps; ++isw) {
                     bool any = false;
                     for (int ir = 0; ir < 31; ++ir) {
-                        int p, q, p2, q2;
-                        rr_pair(ir, k, 32, p, q);
+                        if (tid < 16) {
+                            int p, q;
+                            rr_pair(ir, tid, 32, p, q);
+                            double c, sn;
+                            bool rt;
+                            pair_angle(cur, p, q, tol2, negl, c, sn, rt);
+                            Ang[tid] = c;
+                            Ang[16 + tid] = sn;
+                            Rot[tid] = rt;
+                            if (rt) any = true;
+                        }
+                        __syncthreads();
+                        int p2, q2;
                         rr_pair(ir, k2, 32, p2, q2);
-                        // every lane computes the angle of its column pair k2; the row pair k's angle
-                        // comes from the lane of this wave with k2 == k (lane 16 (k & 3) + k)
-                        double c2, s2;
-                        bool r2;
-                        pair_angle(cur, p2, q2, tol2, negl, c2, s2, r2);
-                        const int src = 16 * (k & 3) + k;
-                        const double c1 = __shfl(c2, src, 64), s1 = __shfl(s2, src, 64);
-                        const bool r1 = __shfl((int)r2, src, 64) != 0;
-                        const double b00 = cur[p * GS + p2], b01 = cur[p * GS + q2];
-                        const double b10 = cur[q * GS + p2], b11 = cur[q * GS + q2];
-                        // left: rows (p, q) <- (c1 row_p - s1 row_q, s1 row_p + c1 row_q)
-                        const double l00 = c1 * b00 - s1 * b10, l01 = c1 * b01 - s1 * b11;
-                        const double l10 = s1 * b00 + c1 * b10, l11 = s1 * b01 + c1 * b11;
-                        // right: cols (p2, q2) <- (c2 col_p2 - s2 col_q2, s2 col_p2 + c2 col_q2)
-                        nxt[p * GS + p2] = c2 * l00 - s2 * l01;
-                        nxt[p * GS + q2] = s2 * l00 + c2 * l01;
-                        nxt[q * GS + p2] = c2 * l10 - s2 * l11;
-                        nxt[q * GS + q2] = s2 * l10 + c2 * l11;
-                        if (k == k2 && r1) any = true;
-                        // Jp <- Jp J: columns (p2, q2) of pair k2, rows k and k + 16 (disjoint per thread)
-                        if (r2) {
+                        const double c2 = Ang[k2], s2 = Ang[16 + k2];
+                        if (tid < 256) {
+                            int p, q;
+                            rr_pair(ir, k, 32, p, q);
+                            const double c1 = Ang[k], s1 = Ang[16 + k];
+                            const double b00 = cur[p * GS + p2], b01 = cur[p * GS + q2];
+                            const double b10 = cur[q * GS + p2], b11 = cur[q * GS + q2];
+                            // left: rows (p, q) <- (c1 row_p - s1 row_q, s1 row_p + c1 row_q)
+                            const double l00 = c1 * b00 - s1 * b10, l01 = c1 * b01 - s1 * b11;
+                            const double l10 = s1 * b00 + c1 * b10, l11 = s1 * b01 + c1 * b11;
+                            // right: cols (p2, q2) <- (c2 col_p2 - s2 col_q2, s2 col_p2 + c2 col_q2)
+                            nxt[p * GS + p2] = c2 * l00 - s2 * l01;
+                            nxt[p * GS + q2] = s2 * l00 + c2 * l01;
+                            nxt[q * GS + p2] = c2 * l10 - s2 * l11;
+                            nxt[q * GS + q2] = s2 * l10 + c2 * l11;
+                        } else if (Rot[k2]) {
+                            // Jp columns (p2, q2) of pair k2, rows k and k + 16 (disjoint per thread)
 #pragma unroll
                             for (int rr = 0; rr < 2; ++rr) {
                                 const int row = k + 16 * rr;
@@ -298,14 +386,14 @@ __global__ __launch_bounds__(256) void block_jacobi_kernel(const double* __restr
                     __syncthreads();
                     if (!more) break;
                 }
+                BJ_T(3);
                 // 5. X_pair Jp and J_pair Jp -> destination buffer
                 apply_pair(Xs, Jp, Xd, LP, col, w, r, h);
-                __syncthreads();
-                stage_pair(Xs, Jsrc, LP, col);
-                __syncthreads();
-                apply_pair(Xs, Jp, Jd, LP, col, w, r, h);
+                BJ_T(4);
+                apply_pair_global(Jsrc, Jp, Jd, LP, col, w, r, h);
+                BJ_T(5);
             } else {
-                for (int e = tid; e < 32 * (LP / 2); e += 256) {
+                for (int e = tid; e < 32 * (LP / 2); e += kBJThreads) {
                     const int kk = e / (LP / 2), i = 2 * (e % (LP / 2));
                     const int64_t o = (int64_t)col(kk) * LP + i;
                     *reinterpret_cast<double2*>(Xd + o) = *reinterpret_cast<const double2*>(Xsrc + o);
@@ -313,10 +401,12 @@ __global__ __launch_bounds__(256) void block_jacobi_kernel(const double* __restr
                 }
             }
             par = 1 - par;
+            BJ_T(7);
             if (!grid_barrier(sync, (unsigned)nwg * ++bar)) {
                 if (tid == 0) info[2] = 1;
                 return;
             }
+            BJ_T(6);
         }
         ++sweeps;
         const unsigned rot = __hip_atomic_load(sync + 4 + sweep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -326,6 +416,9 @@ __global__ __launch_bounds__(256) void block_jacobi_kernel(const double* __restr
     if (wg == 0 && tid == 0) {
         sync[2] = (unsigned)par;
         info[0] = sweeps;
+#ifdef RSVD_BJ_PROF
+        for (int k = 0; k < 8; ++k) g_bj_prof[k] = bj_acc[k];
+#endif
     }
 }
 
@@ -446,8 +539,8 @@ hipError_t launch_block_jacobi(const double* R, int l, int LP, double* X, double
     if (LP % 32 || LP < 64 || LP > 512) return hipErrorInvalidValue;
     hipError_t e = hipMemsetAsync(sync, 0, kSyncWords * sizeof(unsigned), s);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(block_jacobi_kernel, dim3(LP / 32), dim3(256), block_jacobi_lds(LP), s, R, l, LP, X, J, sync,
-                       info);
+    hipLaunchKernelGGL(block_jacobi_kernel, dim3(LP / 32), dim3(kBJThreads), block_jacobi_lds(LP), s, R, l, LP, X, J, Uw,
+                       sync, info);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     const size_t lds = (size_t)LP * 8 * 2 + (size_t)LP * 4 + 64;
@@ -460,4 +553,13 @@ template hipError_t launch_block_jacobi<float>(const double*, int, int, double*,
 template hipError_t launch_block_jacobi<double>(const double*, int, int, double*, double*, double*, double*, double*,
                                                 unsigned*, int*, hipStream_t);
 
+#ifdef RSVD_BJ_PROF
+void bj_prof_dump() {
+    long long t[8];
+    (void)hipMemcpyFromSymbol(t, HIP_SYMBOL(g_bj_prof), sizeof(t));
+    printf("  block_jacobi phases (us, wg 0): init %.1f stage %.1f gram %.1f test %.1f inner %.1f applyX %.1f "
+           "stageJ+applyJ %.1f tail %.1f barrier %.1f\n", t[0] * 0.01, t[1] * 0.01, t[2] * 0.01, 0.0, t[3] * 0.01,
+           t[4] * 0.01, t[5] * 0.01, t[7] * 0.01, t[6] * 0.01);
+}
+#endif
 }  // namespace rsvd

@@ -160,6 +160,9 @@ static void bench_chol() {
     }
 }
 
+#ifdef RSVD_BJ_PROF
+namespace rsvd { void bj_prof_dump(); }
+#endif
 static void bench_jac() {
     for (int LP : {64, 128, 256, 512}) {
         // R: upper triangular with a 0.97^i graded diagonal + noise (like a QR-preconditioned B^T)
@@ -187,6 +190,9 @@ static void bench_jac() {
         CK(hipMemcpy(hinfo, info, 16, hipMemcpyDeviceToHost));
         std::vector<double> hS(LP);
         CK(hipMemcpy(hS.data(), Sd, LP * 8, hipMemcpyDeviceToHost));
+#ifdef RSVD_BJ_PROF
+        rsvd::bj_prof_dump();
+#endif
         printf("block_jacobi LP=%d: %.1f us  sweeps=%d timeout=%d  S[0]=%.6f S[last]=%.3e\n", LP, t, hinfo[0], hinfo[2],
                hS[0], hS[LP - 1]);
         CK(hipFree(R)); CK(hipFree(X)); CK(hipFree(J)); CK(hipFree(Uw)); CK(hipFree(Vw)); CK(hipFree(Sd));
