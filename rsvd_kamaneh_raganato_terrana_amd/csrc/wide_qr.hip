@@ -15,6 +15,7 @@
 // (repair_kernel + one predicated CholeskyQR pass) -- an orthonormal basis completed like the
 // reference's Householder Q.
 #include <algorithm>
+#include <utility>
 
 #include "common.hpp"
 #include "kernels.hpp"
@@ -25,6 +26,8 @@ namespace rsvd {
 namespace {
 
 typedef Mfma<double> MD;
+
+constexpr bool gram_sym_ok(int LP) { return LP == 64 || LP == 128 || LP == 256; }
 
 template <typename T> struct Pair;
 template <> struct Pair<float> { typedef float2 type; };
@@ -101,6 +104,164 @@ __global__ __launch_bounds__(256) void gram_wide_kernel(const T* __restrict__ P,
             }
 }
 
+// ------------------------------------------------------------------------------------------------
+// Symmetric Gram of a tall panel, LP in {64, 128, 256}: ONE 512-thread workgroup per row chunk reads
+// its rows once (16-B loads, register-prefetched one step ahead, staged in LDS 32 rows per step) and
+// computes every upper 16x16 tile pair (ta <= tb) of the chunk on the fp64 MFMA (LP = 256: two workgroups per chunk).  For G = P^T P both
+// MFMA operands are "row k, column c" reads of the panel (A: P^T[c][k], B: P[k][c]), so a tile pair
+// costs two LDS reads per 4 rows.  Pairs are dealt round-robin to the waves (9 per wave at
+// LP = 256).  The old kernel gave each 32x32 block its own wave and chunk walk, re-reading every
+// panel row LP/32 + 1 times from HBM; here each byte is read once and the MFMA issue rate is the
+// bound.  Partial tiles land in the (chunk, 32x32 block) slab layout gram_reduce_kernel sums; the
+// lower 16x16 sub-tile of a diagonal 32x32 block is written as the transpose of the upper one.
+// (ta, tb) of upper tile pair p (row-major over the upper triangle of NT x NT tiles); p >= NP -> (0, 0)
+constexpr int pair_ta(int NT, int p) {
+    if (p >= NT * (NT + 1) / 2) return 0;
+    int a = 0;
+    while (p >= NT - a) { p -= NT - a; ++a; }
+    return a;
+}
+constexpr int pair_tb(int NT, int p) {
+    if (p >= NT * (NT + 1) / 2) return 0;
+    int a = 0;
+    while (p >= NT - a) { p -= NT - a; ++a; }
+    return a + p;
+}
+
+template <int NT, int P> struct PairOf {  // forces compile-time evaluation of the tile indices
+    static constexpr int a = pair_ta(NT, P), b = pair_tb(NT, P);
+};
+
+template <int LP> struct GramSym {
+    static constexpr int NH = LP == 256 ? 2 : 1;  // workgroups per chunk
+    static constexpr int NT = LP / 16, NP = NT * (NT + 1) / 2, NW = 8 * NH, PPW = (NP + NW - 1) / NW;
+    static constexpr int NB = LP / 32, NBLK = NB * (NB + 1) / 2;
+};
+
+// slot I of dealer WG: pair WG + NW I (compile-time tile indices, so v[] stays in registers)
+template <int LP, int WG, int... I>
+__device__ __forceinline__ void gram_sym_mma(const double (&v)[LP / 16], f64x4 (&acc)[GramSym<LP>::PPW],
+                                             std::integer_sequence<int, I...>) {
+    typedef GramSym<LP> G;
+    ((acc[I] = (WG + G::NW * I < G::NP) ? MD::mma(v[PairOf<G::NT, WG + G::NW * I>::a], v[PairOf<G::NT, WG + G::NW * I>::b], acc[I])
+                                        : acc[I]),
+     ...);
+}
+
+// does dealer WG touch tile t?
+template <int LP, int WG>
+constexpr bool gram_sym_needs(int t) {
+    typedef GramSym<LP> G;
+    for (int i = 0; i < G::PPW; ++i)
+        if (WG + G::NW * i < G::NP && (pair_ta(G::NT, WG + G::NW * i) == t || pair_tb(G::NT, WG + G::NW * i) == t))
+            return true;
+    return false;
+}
+
+template <int LP, int WG, int t> struct NeedOf {  // compile-time gram_sym_needs
+    static constexpr bool value = gram_sym_needs<LP, WG>(t);
+};
+// the panel values of the tiles dealer WG touches, for the 4 rows of one MFMA step
+template <typename T, int LP, int WG, int... I>
+__device__ __forceinline__ void gram_sym_loadv(const T* rowp, double (&v)[LP / 16], std::integer_sequence<int, I...>) {
+    ((v[I] = NeedOf<LP, WG, I>::value ? (double)rowp[16 * I] : 0.0), ...);
+}
+
+template <typename T, int LP, int WG>
+__device__ __forceinline__ void gram_sym_body(const T* __restrict__ P, int64_t beg, int64_t end, int chunk,
+                                              double* __restrict__ slabs, T* tile) {
+    typedef GramSym<LP> G;
+    constexpr int NT = G::NT, PPW = G::PPW, NTH = 512;
+    constexpr int RS = (sizeof(T) == 8 && LP == 256) ? 16 : 32;  // panel rows per step (LDS <= 64 KB)
+    constexpr int VE = 16 / sizeof(T);                            // elements per 16-B load
+    constexpr int CPR = LP / VE;                                  // 16-B chunks per row
+    constexpr int LPT = RS * CPR / NTH;                           // loads per thread per step
+    static_assert(LPT >= 1 && (RS * CPR) % NTH == 0, "step tiling");
+    constexpr int PITCH = LP + 64 / (int)sizeof(T);  // row pitch: the 4 rows of an MFMA read hit different banks
+    typedef typename Vec16<T>::type V;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int r = lane & 15, h = lane >> 4;
+    f64x4 acc[PPW];
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) acc[i] = MD::zero();
+
+    V reg[LPT];
+    auto load = [&](int64_t r0) {
+#pragma unroll
+        for (int t = 0; t < LPT; ++t) {
+            const int u = tid + NTH * t;
+            const int64_t row = r0 + u / CPR;
+            V v;
+            if constexpr (sizeof(T) == 4) v = make_float4(0.f, 0.f, 0.f, 0.f);
+            else v = make_double2(0.0, 0.0);
+            if (row < end) v = *reinterpret_cast<const V*>(P + row * LP + (u % CPR) * VE);
+            reg[t] = v;
+        }
+    };
+    if (beg < end) load(beg);
+    for (int64_t r0 = beg; r0 < end; r0 += RS) {
+        __syncthreads();  // the previous step's LDS reads are done
+#pragma unroll
+        for (int t = 0; t < LPT; ++t) {
+            const int u = tid + NTH * t;
+            *reinterpret_cast<V*>(tile + (u / CPR) * PITCH + (u % CPR) * VE) = reg[t];
+        }
+        __syncthreads();
+        if (r0 + RS < end) load(r0 + RS);
+#pragma unroll 2
+        for (int g = 0; g < RS / 4; ++g) {
+            const T* rowp = tile + (4 * g + h) * PITCH + r;
+            double v[NT];
+            gram_sym_loadv<T, LP, WG>(rowp, v, std::make_integer_sequence<int, NT>{});
+            gram_sym_mma<LP, WG>(v, acc, std::make_integer_sequence<int, PPW>{});
+        }
+    }
+
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+        const int p = WG + G::NW * i;
+        if (p < G::NP) {
+            const int ta = pair_ta(NT, p), tb = pair_tb(NT, p);
+            const int a = ta >> 1, b = tb >> 1;
+            const int blk = a * G::NB - a * (a - 1) / 2 + (b - a);
+            double* dst = slabs + ((int64_t)chunk * G::NBLK + blk) * 1024;
+            const bool mirror = (a == b) && (ta != tb);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int li = 16 * (ta & 1) + MD::row(h, j), lj = 16 * (tb & 1) + r;
+                dst[li * 32 + lj] = acc[i][j];
+                if (mirror) dst[lj * 32 + li] = acc[i][j];
+            }
+        }
+    }
+}
+
+template <typename T, int LP, int... W>
+__device__ __forceinline__ void gram_sym_dispatch(int wg, const T* P, int64_t beg, int64_t end, int chunk, double* slabs,
+                                                  T* tile, std::integer_sequence<int, W...>) {
+    ((wg == W ? gram_sym_body<T, LP, W>(P, beg, end, chunk, slabs, tile) : void()), ...);
+}
+
+template <typename T, int LP>
+__global__ __launch_bounds__(512) void gram_sym_kernel(const T* __restrict__ P, int64_t rows, int64_t rpc, int nchunk,
+                                                       double* __restrict__ slabs, const int* __restrict__ pred) {
+    if (pred && *pred == 0) return;
+    typedef GramSym<LP> G;
+    // NH workgroups share a chunk (LP = 256: 2, each owning every other pair), dealt to one XCD (block ids
+    // b and b + 8) so the second read of the rows is an L2 hit.
+    constexpr int RS = (sizeof(T) == 8 && LP == 256) ? 16 : 32;
+    constexpr int PITCH = LP + 64 / (int)sizeof(T);
+    __shared__ __attribute__((aligned(16))) T tile[RS * PITCH];
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: scalar branch to the dealer body
+    const int hb = G::NH == 1 ? 0 : (blockIdx.x >> 3) & 1;
+    const int chunk = G::NH == 1 ? blockIdx.x : ((blockIdx.x & 7) | ((blockIdx.x >> 4) << 3));
+    if (chunk >= nchunk) return;
+    const int64_t beg = (int64_t)chunk * rpc;
+    const int64_t end = (beg + rpc < rows) ? beg + rpc : rows;
+    // dealer index: pairs WG, WG + NW, ... belong to wave w of half hb
+    gram_sym_dispatch<T, LP>(w * G::NH + hb, P, beg, end, chunk, slabs, tile, std::make_integer_sequence<int, G::NW>{});
+}
+
 __global__ void gram_reduce_kernel(const double* __restrict__ slabs, int nblk, int nchunk, int LP, int cross,
                                    double* __restrict__ G, const int* __restrict__ pred) {
     if (pred && *pred == 0) return;
@@ -123,8 +284,19 @@ __global__ void gram_reduce_kernel(const double* __restrict__ slabs, int nblk, i
     }
     const int ra = 32 * a + loc / 32, cb = 32 * b + loc % 32;
     if (ra >= LP || cb >= LP) return;
-    double s = 0.0;
-    for (int c = 0; c < nchunk; ++c) s += slabs[((int64_t)c * nblk + blk) * 1024 + loc];
+    // four interleaved partial sums (loads in flight), combined in a fixed order: deterministic
+    const int64_t cs = (int64_t)nblk * 1024;
+    const double* src = slabs + (int64_t)blk * 1024 + loc;
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+    int c = 0;
+    for (; c + 4 <= nchunk; c += 4) {
+        s0 += src[(c + 0) * cs];
+        s1 += src[(c + 1) * cs];
+        s2 += src[(c + 2) * cs];
+        s3 += src[(c + 3) * cs];
+    }
+    for (; c < nchunk; ++c) s0 += src[c * cs];
+    const double s = (s0 + s1) + (s2 + s3);
     G[(int64_t)ra * LP + cb] = s;
     if (!cross && a != b) G[(int64_t)cb * LP + ra] = s;
 }
@@ -757,6 +929,17 @@ GramPlan plan_gram_wide(int64_t rows, int LP, int cross) {
     GramPlan g;
     const int nb = (LP + 31) / 32;
     g.blocks = cross ? nb * nb : nb * (nb + 1) / 2;
+    if (!cross && gram_sym_ok(LP)) {  // gram_sym_kernel: one workgroup per chunk, >= 64 rows each, <= 256 chunks
+        int64_t chunks = (rows + 63) / 64;
+        if (chunks > 256) chunks = 256;
+        if (chunks < 1) chunks = 1;
+        int64_t rpc = (rows + chunks - 1) / chunks;
+        rpc = (rpc + 31) / 32 * 32;  // a multiple of every RS
+        g.rows_per_chunk = rpc;
+        g.chunks = (int)((rows + rpc - 1) / rpc);
+        if (g.chunks < 1) g.chunks = 1;
+        return g;
+    }
     int64_t chunks = (4096 + g.blocks - 1) / g.blocks;
     const int64_t max_by_rows = (rows + 255) / 256;
     if (chunks > max_by_rows) chunks = max_by_rows;
@@ -778,7 +961,17 @@ hipError_t launch_gram_wide(const T* P, const T* P2, int64_t rows, int LP, const
     if (P2)
         hipLaunchKernelGGL((gram_wide_kernel<T, true>), dim3(wgs), dim3(256), 0, s, P, P2, rows, LP, gp.blocks,
                            gp.chunks, gp.rows_per_chunk, slabs, pred);
-    else
+    else if (gram_sym_ok(LP)) {
+        if (LP == 64)
+            hipLaunchKernelGGL((gram_sym_kernel<T, 64>), dim3(gp.chunks), dim3(512), 0, s, P, rows, gp.rows_per_chunk, gp.chunks,
+                               slabs, pred);
+        else if (LP == 128)
+            hipLaunchKernelGGL((gram_sym_kernel<T, 128>), dim3(gp.chunks), dim3(512), 0, s, P, rows,
+                               gp.rows_per_chunk, gp.chunks, slabs, pred);
+        else
+            hipLaunchKernelGGL((gram_sym_kernel<T, 256>), dim3((gp.chunks + 7) / 8 * 16), dim3(512), 0, s, P,
+                               rows, gp.rows_per_chunk, gp.chunks, slabs, pred);
+    } else
         hipLaunchKernelGGL((gram_wide_kernel<T, false>), dim3(wgs), dim3(256), 0, s, P, P, rows, LP, gp.blocks,
                            gp.chunks, gp.rows_per_chunk, slabs, pred);
     hipError_t e = hipGetLastError();

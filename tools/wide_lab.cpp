@@ -97,6 +97,21 @@ static void bench_gram() {
         const double fl = 2.0 * rows * LP * LP * gp.blocks / ((LP / 32.0) * (LP / 32.0));
         printf("gram rows=%ld LP=%d blocks=%d chunks=%d: %.1f us  (%.1f TF/s fp64, %.0f GB/s)\n", (long)rows, LP, gp.blocks,
                gp.chunks, t, fl / t / 1e6, rows * LP * 4.0 / t / 1e3);
+        {  // symmetric path vs the cross (all-blocks) path on the same panel
+            GramPlan gx = plan_gram_wide(rows, LP, 1);
+            double *sx, *Gx;
+            CK(hipMalloc(&sx, (size_t)gx.blocks * gx.chunks * 1024 * 8));
+            CK(hipMalloc(&Gx, (size_t)LP * LP * 8));
+            CK(launch_gram_wide<float>(P, P, rows, LP, gx, sx, Gx, nullptr, S));
+            CK(hipStreamSynchronize(S));
+            std::vector<double> a((size_t)LP * LP), b((size_t)LP * LP);
+            CK(hipMemcpy(a.data(), G, a.size() * 8, hipMemcpyDeviceToHost));
+            CK(hipMemcpy(b.data(), Gx, b.size() * 8, hipMemcpyDeviceToHost));
+            double md = 0, mx = 0;
+            for (size_t i = 0; i < a.size(); ++i) { md = std::max(md, std::fabs(a[i] - b[i])); mx = std::max(mx, std::fabs(b[i])); }
+            printf("  sym vs cross: max |diff| %.3e (max |G| %.3e) %s\n", md, mx, md <= 1e-12 * mx ? "OK" : "MISMATCH");
+            CK(hipFree(sx)); CK(hipFree(Gx));
+        }
         CK(hipFree(P)); CK(hipFree(slabs)); CK(hipFree(G));
     }
 }
