@@ -27,7 +27,7 @@ namespace {
 
 typedef Mfma<double> MD;
 
-constexpr bool gram_sym_ok(int LP) { return LP == 64 || LP == 128 || LP == 256; }
+constexpr bool gram_sym_ok(int LP) { return LP == 64 || LP == 128 || LP == 256 || LP == 512; }
 
 template <typename T> struct Pair;
 template <> struct Pair<float> { typedef float2 type; };
@@ -133,7 +133,10 @@ template <int NT, int P> struct PairOf {  // forces compile-time evaluation of t
 };
 
 template <int LP> struct GramSym {
-    static constexpr int NH = LP == 256 ? 2 : 1;  // workgroups per chunk
+    static constexpr int NH = LP == 512 ? 8 : (LP == 256 ? 2 : 1);  // workgroups per chunk
+    static constexpr int LNH = LP == 512 ? 3 : (LP == 256 ? 1 : 0);
+    // panel rows per LDS step (static LDS <= 64 KB)
+    template <typename T> static constexpr int rs() { return LP == 512 ? (sizeof(T) == 8 ? 8 : 16) : ((sizeof(T) == 8 && LP == 256) ? 16 : 32); }
     static constexpr int NT = LP / 16, NP = NT * (NT + 1) / 2, NW = 8 * NH, PPW = (NP + NW - 1) / NW;
     static constexpr int NB = LP / 32, NBLK = NB * (NB + 1) / 2;
 };
@@ -172,7 +175,7 @@ __device__ __forceinline__ void gram_sym_body(const T* __restrict__ P, int64_t b
                                               double* __restrict__ slabs, T* tile) {
     typedef GramSym<LP> G;
     constexpr int NT = G::NT, PPW = G::PPW, NTH = 512;
-    constexpr int RS = (sizeof(T) == 8 && LP == 256) ? 16 : 32;  // panel rows per step (LDS <= 64 KB)
+    constexpr int RS = G::template rs<T>();  // panel rows per step
     constexpr int VE = 16 / sizeof(T);                            // elements per 16-B load
     constexpr int CPR = LP / VE;                                  // 16-B chunks per row
     constexpr int LPT = RS * CPR / NTH;                           // loads per thread per step
@@ -247,14 +250,14 @@ __global__ __launch_bounds__(512) void gram_sym_kernel(const T* __restrict__ P, 
                                                        double* __restrict__ slabs, const int* __restrict__ pred) {
     if (pred && *pred == 0) return;
     typedef GramSym<LP> G;
-    // NH workgroups share a chunk (LP = 256: 2, each owning every other pair), dealt to one XCD (block ids
-    // b and b + 8) so the second read of the rows is an L2 hit.
-    constexpr int RS = (sizeof(T) == 8 && LP == 256) ? 16 : 32;
+    // NH workgroups share a chunk (LP = 256: 2, LP = 512: 8, dealing the pairs between them), all on one
+    // XCD (block ids b, b + 8, ...) so the repeated reads of the rows are L2 hits.
+    constexpr int RS = G::template rs<T>();
     constexpr int PITCH = LP + 64 / (int)sizeof(T);
     __shared__ __attribute__((aligned(16))) T tile[RS * PITCH];
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform: scalar branch to the dealer body
-    const int hb = G::NH == 1 ? 0 : (blockIdx.x >> 3) & 1;
-    const int chunk = G::NH == 1 ? blockIdx.x : ((blockIdx.x & 7) | ((blockIdx.x >> 4) << 3));
+    const int hb = G::NH == 1 ? 0 : (blockIdx.x >> 3) & (G::NH - 1);
+    const int chunk = G::NH == 1 ? blockIdx.x : ((blockIdx.x & 7) | ((blockIdx.x >> (3 + G::LNH)) << 3));
     if (chunk >= nchunk) return;
     const int64_t beg = (int64_t)chunk * rpc;
     const int64_t end = (beg + rpc < rows) ? beg + rpc : rows;
@@ -931,7 +934,8 @@ GramPlan plan_gram_wide(int64_t rows, int LP, int cross) {
     g.blocks = cross ? nb * nb : nb * (nb + 1) / 2;
     if (!cross && gram_sym_ok(LP)) {  // gram_sym_kernel: one workgroup per chunk, >= 64 rows each, <= 256 chunks
         int64_t chunks = (rows + 63) / 64;
-        if (chunks > 256) chunks = 256;
+        const int64_t cap = LP == 512 ? 128 : 256;  // LP = 512: 8 workgroups per chunk, 1 MB of slab per chunk
+        if (chunks > cap) chunks = cap;
         if (chunks < 1) chunks = 1;
         int64_t rpc = (rows + chunks - 1) / chunks;
         rpc = (rpc + 31) / 32 * 32;  // a multiple of every RS
@@ -968,8 +972,11 @@ hipError_t launch_gram_wide(const T* P, const T* P2, int64_t rows, int LP, const
         else if (LP == 128)
             hipLaunchKernelGGL((gram_sym_kernel<T, 128>), dim3(gp.chunks), dim3(512), 0, s, P, rows,
                                gp.rows_per_chunk, gp.chunks, slabs, pred);
-        else
+        else if (LP == 256)
             hipLaunchKernelGGL((gram_sym_kernel<T, 256>), dim3((gp.chunks + 7) / 8 * 16), dim3(512), 0, s, P,
+                               rows, gp.rows_per_chunk, gp.chunks, slabs, pred);
+        else
+            hipLaunchKernelGGL((gram_sym_kernel<T, 512>), dim3((gp.chunks + 7) / 8 * 64), dim3(512), 0, s, P,
                                rows, gp.rows_per_chunk, gp.chunks, slabs, pred);
     } else
         hipLaunchKernelGGL((gram_wide_kernel<T, false>), dim3(wgs), dim3(256), 0, s, P, P, rows, LP, gp.blocks,
