@@ -87,6 +87,14 @@ def make_A(torch, m_local, n, row0, dtype, rank_cols=128, seed=0x5EED0002):
     return Acm, 1.0
 
 
+def lp_pad(l):
+    """Panel width of the wide engine's LDS-DMA kernels (wide.cpp WideLayout: a power of two >= 128)."""
+    lp = 128
+    while lp < l:
+        lp *= 2
+    return lp
+
+
 def pmc_traffic(key, kernel_prefix):
     """HBM bytes per launch of the kernel from the committed rocprofv3 PMC summary for this
     workload (profiles/*_traffic.json, written by tools/profile.sh + tools/traffic.py; FETCH_SIZE
@@ -231,7 +239,11 @@ def main():
         bound, achieved, peak, unit = "mfma", flop_launch / t_s / 1e12, PEAK_TFLOPS[dt], "TFLOP/s"
     key = f"{args.config}_{dt}_{m_local}x{n}_l{l}_q{q}"
     lowp = dt in ("bf16", "fp8")
-    kpref = "wproj_kernel" if lowp else ("proj_tn_kernel" if kname.startswith("proj_tn") else "proj_nn_kernel")
+    if lowp:  # the LDS-DMA kernel wproj2_kernel<FP8, NN, LP, SPLIT> (hi/lo split skinny operand)
+        nn_k = "true" if kname.startswith("proj_nn") else "false"
+        kpref = f"wproj2_kernel<{'true' if dt == 'fp8' else 'false'}, {nn_k}, {lp_pad(l)}, true>"
+    else:
+        kpref = "proj_tn_kernel" if kname.startswith("proj_tn") else "proj_nn_kernel"
     tr = pmc_traffic(key, kpref)
     roof = {
         "bound": bound,
