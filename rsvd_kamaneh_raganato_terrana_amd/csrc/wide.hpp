@@ -29,11 +29,12 @@ struct WProjPlan {
     int64_t chunk;   // K range per workgroup (multiple of 32)
     int blocks;      // output row blocks
     bool v2;         // LDS-DMA pipelined kernel (bf16 / e4m3 A, LP >= 128, 16-B aligned columns)
+    bool ds = false; // v2 TN at LP = 128 with two k-steps per stage (128-B A runs; K a multiple of 64)
 };
 // v2 requires: a 16-B aligned base, bf16 A with lda and m multiples of 8 or e4m3 A with lda and m
 // multiples of 16, and S panels zero-padded
 // to a multiple of 32 rows (the engine allocates them so).
-WProjPlan plan_wproj(int64_t rows_out, int64_t K, int LP, bool v2 = false);
+WProjPlan plan_wproj(int64_t rows_out, int64_t K, int LP, bool v2 = false, bool nn = true, bool fp8 = false);
 // NN: Y (m x LP, fp32) = A (m x n) * S       S = n x LP bf16 panel(s)      src/rSVD.cpp:59,66
 // TN: Z (n x LP, fp32) = A^T * S             S = m x LP bf16 panel(s)      src/rSVD.cpp:63,89
 // A is column-major (lda) bf16 (a_fp8 = 0) or e4m3 (a_fp8 = 1).  Slo == nullptr: single pass.

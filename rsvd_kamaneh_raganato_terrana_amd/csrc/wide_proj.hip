@@ -271,18 +271,26 @@ __global__ __launch_bounds__(256) void wproj_kernel(const void* __restrict__ Av,
 // image (ds_read_b128 conflict-free; tools/ check in DESIGN.md §3.6).  The S panels must be
 // zero-padded to a multiple of 32 rows; A indices are clamped in bounds (the zero S rows cancel
 // whatever the clamped A values are).
-template <int LP> struct W2Cfg;
-template <> struct W2Cfg<128> { static constexpr int WR = 8, WC = 1, G = 8; };
-template <> struct W2Cfg<256> { static constexpr int WR = 4, WC = 2, G = 8; };
-template <> struct W2Cfg<512> { static constexpr int WR = 2, WC = 4, G = 8; };
+//
+// DS ("double step", bf16 TN at LP = 128): a stage holds TWO 32-deep k-steps, so every A column
+// contributes one 128-B run per stage -- a full-line fabric request instead of two 64-B ones (the
+// TN A image is [WI j][64 i], unit c of row j holding rows 32 (c >> 2) + 8 ((c & 3) ^ ((j >> 1) & 3))
+// .. +7, ds_read_b128 conflict-free per 8 lanes).  To fit two stages in LDS the workgroup takes 256
+// output rows (4 x 2 waves, 64 S columns each).  Needs K and the K chunks multiples of 64.
+template <int LP, bool DS> struct W2Cfg;
+template <> struct W2Cfg<128, false> { static constexpr int WR = 8, WC = 1, G = 8; };
+template <> struct W2Cfg<128, true> { static constexpr int WR = 4, WC = 2, G = 4; };
+template <> struct W2Cfg<256, false> { static constexpr int WR = 4, WC = 2, G = 8; };
+template <> struct W2Cfg<512, false> { static constexpr int WR = 2, WC = 4, G = 8; };
 
-template <int LP, bool SPLIT, bool FP8>
+template <int LP, bool SPLIT, bool FP8, bool DS = false>
 struct W2Shape {
-    static constexpr int WR = W2Cfg<LP>::WR, WC = W2Cfg<LP>::WC, G = W2Cfg<LP>::G;
+    static constexpr int WR = W2Cfg<LP, DS>::WR, WC = W2Cfg<LP, DS>::WC, G = W2Cfg<LP, DS>::G;
     static constexpr int WI = WR * 64;            // output rows per workgroup
     static constexpr int NS = SPLIT ? 2 : 1;
-    static constexpr int SBYTES = KS * LP * 2;    // one S panel tile
-    static constexpr int ABYTES = KS * WI * (FP8 ? 1 : 2);  // the A tile
+    static constexpr int KSS = DS ? 2 * KS : KS;  // k rows per stage
+    static constexpr int SBYTES = KSS * LP * 2;   // one S panel tile
+    static constexpr int ABYTES = KSS * WI * (FP8 ? 1 : 2);  // the A tile
     static constexpr int STAGE = NS * SBYTES + ABYTES;
     static constexpr int NST0 = 147456 / STAGE;
     static constexpr int NST = NST0 > 4 ? 4 : (NST0 < 2 ? 2 : NST0);
@@ -361,12 +369,14 @@ __device__ __forceinline__ bf16x8_t fp8x8_to_bf16x8(i32x2 v) {
     return __builtin_bit_cast(bf16x8_t, make_uint4(a.x, a.y, b.x, b.y));
 }
 
-template <bool FP8, bool NN, int LP, bool SPLIT>
+template <bool FP8, bool NN, int LP, bool SPLIT, bool DS = false>
 __global__ __launch_bounds__(512) void wproj2_kernel(const void* __restrict__ Av, int64_t lda, int64_t rows_out,
                                                      int64_t K, int64_t arows, const bf16_t* __restrict__ Shi,
                                                      const bf16_t* __restrict__ Slo, float* __restrict__ out,
                                                      int64_t slab_stride, int64_t kchunk, int nrowblk) {
-    typedef W2Shape<LP, SPLIT, FP8> SH;
+    typedef W2Shape<LP, SPLIT, FP8, DS> SH;
+    static_assert(!DS || (!NN && !FP8), "double-step stages: bf16 TN only");
+    constexpr int KSS = SH::KSS;
     const bf16_t* __restrict__ A = reinterpret_cast<const bf16_t*>(Av);
     const uint8_t* __restrict__ A8 = reinterpret_cast<const uint8_t*>(Av);
     constexpr int WR = SH::WR, G = SH::G, WI = SH::WI, NS = SH::NS, NST = SH::NST;
@@ -379,12 +389,12 @@ __global__ __launch_bounds__(512) void wproj2_kernel(const void* __restrict__ Av
     const int64_t row0 = (int64_t)rb * WI;
     const int64_t kbeg = (int64_t)sp * kchunk;
     const int64_t kend = (kbeg + kchunk < K) ? kbeg + kchunk : K;
-    const int nsteps = (int)((kend - kbeg + KS - 1) / KS);
+    const int nsteps = (int)((kend - kbeg + KSS - 1) / KSS);
 
     // issue the glds of step `st` into ring slot st % NST
     auto issue = [&](int st) {
         char* slot = smem_raw + (size_t)(st % NST) * SH::STAGE;
-        const int64_t k0 = kbeg + (int64_t)st * KS;
+        const int64_t k0 = kbeg + (int64_t)st * KSS;
 #pragma unroll
         for (int a = 0; a < NS; ++a) {
             const bf16_t* S = a ? Slo : Shi;
@@ -437,6 +447,13 @@ __global__ __launch_bounds__(512) void wproj2_kernel(const void* __restrict__ Av
                 int64_t i = row0 + 8 * (cc ^ swz(j));
                 i = (i + 8 <= arows) ? i : arows - 8;
                 src = A + jj * lda + i;
+            } else if (DS) {  // [WI j][64 i]: 8 units of 8 rows i, swizzled within each 32-row half
+                const int j = u >> 3, c8 = u & 7;
+                int64_t jc = row0 + j;
+                jc = jc < rows_out ? jc : rows_out - 1;
+                int64_t i = k0 + 32 * (c8 >> 2) + 8 * ((c8 & 3) ^ ((j >> 1) & 3));
+                i = (i + 8 <= arows) ? i : arows - 8;
+                src = A + jc * lda + i;
             } else {  // [WI j][32 i]: row = A column row0 + j, 4 chunks of 8 rows i
                 const int j = u >> 2, cc = u & 3;
                 int64_t jc = row0 + j;
@@ -471,75 +488,78 @@ __global__ __launch_bounds__(512) void wproj2_kernel(const void* __restrict__ Av
         if (st + NST - 1 < nsteps) issue(st + NST - 1);
         const uint32_t slot = lds_addr(smem_raw) + (uint32_t)((st % NST) * SH::STAGE);
         const uint32_t At = slot + NS * SH::SBYTES;
-        bf16x8_t af[RT];
-        i32x2 a1[RT], a2[RT];
-        i32x4 a4[RT];
 #pragma unroll
-        for (int t = 0; t < RT; ++t) {
-            if (FP8) {
-                if (NN) {
-                    const int k = 8 * h + (r >> 1);
-                    const int c = 4 * wr + t;  // 16-row chunk of the tile
-                    a1[t] = tr8_read_a(At + k * WI + 16 * (c ^ swz8<WI>(k)) + 8 * (r & 1));
+        for (int ss = 0; ss < KSS / KS; ++ss) {  // the k-steps of the stage
+            bf16x8_t af[RT];
+            i32x2 a1[RT], a2[RT];
+            i32x4 a4[RT];
+#pragma unroll
+            for (int t = 0; t < RT; ++t) {
+                if (FP8) {
+                    if (NN) {
+                        const int k = 8 * h + (r >> 1);
+                        const int c = 4 * wr + t;  // 16-row chunk of the tile
+                        a1[t] = tr8_read_a(At + k * WI + 16 * (c ^ swz8<WI>(k)) + 8 * (r & 1));
+                    } else {
+                        const int j = wr * 64 + 16 * t + r;
+                        a1[t] = read64_a(At + j * 32 + 8 * (h ^ (2 * ((j >> 3) & 1))));
+                    }
+                } else if (NN) {
+                    const int col = wr * 64 + 16 * t + 4 * p;  // i within the tile
+                    const int k1 = 8 * h + q, k2 = k1 + 4;
+                    a1[t] = tr_read_a(At + k1 * (WI * 2) + 16 * ((col >> 3) ^ swz(k1)) + 2 * (col & 7));
+                    a2[t] = tr_read_a(At + k2 * (WI * 2) + 16 * ((col >> 3) ^ swz(k2)) + 2 * (col & 7));
                 } else {
                     const int j = wr * 64 + 16 * t + r;
-                    a1[t] = read64_a(At + j * 32 + 8 * (h ^ (2 * ((j >> 3) & 1))));
+                    a4[t] = read128_a(At + j * (KSS * 2) + 16 * (4 * ss + (h ^ ((j >> 1) & 3))));
                 }
-            } else if (NN) {
-                const int col = wr * 64 + 16 * t + 4 * p;  // i within the tile
-                const int k1 = 8 * h + q, k2 = k1 + 4;
-                a1[t] = tr_read_a(At + k1 * (WI * 2) + 16 * ((col >> 3) ^ swz(k1)) + 2 * (col & 7));
-                a2[t] = tr_read_a(At + k2 * (WI * 2) + 16 * ((col >> 3) ^ swz(k2)) + 2 * (col & 7));
-            } else {
-                const int j = wr * 64 + 16 * t + r;
-                a4[t] = read128_a(At + j * 64 + 16 * (h ^ ((j >> 1) & 3)));
             }
-        }
-        // B fragments of column tile g: hi (and lo) halves of the transposed S rows 8h+q, 8h+q+4
-        auto bread = [&](int g, i32x2* b) {
-            const int col = wc * G * 16 + 16 * g + 4 * p;
-            const int k1 = 8 * h + q, k2 = k1 + 4;
-            const uint32_t o1 = 2 * (k1 * LP + 8 * ((col >> 3) ^ swz(k1)) + (col & 7));
-            const uint32_t o2 = 2 * (k2 * LP + 8 * ((col >> 3) ^ swz(k2)) + (col & 7));
-            b[0] = tr_read_a(slot + o1);
-            b[1] = tr_read_a(slot + o2);
-            if (SPLIT) {
-                b[2] = tr_read_a(slot + SH::SBYTES + o1);
-                b[3] = tr_read_a(slot + SH::SBYTES + o2);
+            // B fragments of column tile g: hi (and lo) halves of the transposed S rows 8h+q, 8h+q+4
+            auto bread = [&](int g, i32x2* b) {
+                const int col = wc * G * 16 + 16 * g + 4 * p;
+                const int k1 = 8 * h + q + 32 * ss, k2 = k1 + 4;
+                const uint32_t o1 = 2 * (k1 * LP + 8 * ((col >> 3) ^ swz(k1)) + (col & 7));
+                const uint32_t o2 = 2 * (k2 * LP + 8 * ((col >> 3) ^ swz(k2)) + (col & 7));
+                b[0] = tr_read_a(slot + o1);
+                b[1] = tr_read_a(slot + o2);
+                if (SPLIT) {
+                    b[2] = tr_read_a(slot + SH::SBYTES + o1);
+                    b[3] = tr_read_a(slot + SH::SBYTES + o2);
+                }
+            };
+            i32x2 bb[2][4];
+            bread(0, bb[0]);
+            auto wait_b = [&](i32x2* b) {
+                if (SPLIT) wait_lgkm0(b[0], b[1], b[2], b[3]);
+                else wait_lgkm0(b[0], b[1]);
+            };
+            wait_b(bb[0]);
+#pragma unroll
+            for (int t = 0; t < RT; ++t) {  // (retired by the wait above; these waits are no-ops that pin the order)
+                if (FP8) {
+                    wait_lgkm0(a1[t]);
+                    af[t] = fp8x8_to_bf16x8(a1[t]);
+                } else {
+                    if (NN) wait_lgkm0(a1[t], a2[t]);
+                    else wait_lgkm0(a4[t]);
+                    af[t] = NN ? join2(a1[t], a2[t]) : __builtin_bit_cast(bf16x8_t, a4[t]);
+                }
             }
-        };
-        i32x2 bb[2][4];
-        bread(0, bb[0]);
-        auto wait_b = [&](i32x2* b) {
-            if (SPLIT) wait_lgkm0(b[0], b[1], b[2], b[3]);
-            else wait_lgkm0(b[0], b[1]);
-        };
-        wait_b(bb[0]);
 #pragma unroll
-        for (int t = 0; t < RT; ++t) {  // (retired by the wait above; these waits are no-ops that pin the order)
-            if (FP8) {
-                wait_lgkm0(a1[t]);
-                af[t] = fp8x8_to_bf16x8(a1[t]);
-            } else {
-                if (NN) wait_lgkm0(a1[t], a2[t]);
-                else wait_lgkm0(a4[t]);
-                af[t] = NN ? join2(a1[t], a2[t]) : __builtin_bit_cast(bf16x8_t, a4[t]);
+            for (int g = 0; g < G; ++g) {
+                if (g + 1 < G) bread(g + 1, bb[(g + 1) & 1]);  // next tile's fragments in flight
+                const i32x2* b = bb[g & 1];
+                const bf16x8_t bh = join2(b[0], b[1]);
+#pragma unroll
+                for (int t = 0; t < RT; ++t) acc[t][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[t], bh, acc[t][g], 0, 0, 0);
+                if (SPLIT) {
+                    const bf16x8_t bl = join2(b[2], b[3]);
+#pragma unroll
+                    for (int t = 0; t < RT; ++t)
+                        acc[t][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[t], bl, acc[t][g], 0, 0, 0);
+                }
+                if (g + 1 < G) wait_b(bb[(g + 1) & 1]);
             }
-        }
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-            if (g + 1 < G) bread(g + 1, bb[(g + 1) & 1]);  // next tile's fragments in flight
-            const i32x2* b = bb[g & 1];
-            const bf16x8_t bh = join2(b[0], b[1]);
-#pragma unroll
-            for (int t = 0; t < RT; ++t) acc[t][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[t], bh, acc[t][g], 0, 0, 0);
-            if (SPLIT) {
-                const bf16x8_t bl = join2(b[2], b[3]);
-#pragma unroll
-                for (int t = 0; t < RT; ++t)
-                    acc[t][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[t], bl, acc[t][g], 0, 0, 0);
-            }
-            if (g + 1 < G) wait_b(bb[(g + 1) & 1]);
         }
     }
 
@@ -556,14 +576,14 @@ __global__ __launch_bounds__(512) void wproj2_kernel(const void* __restrict__ Av
         }
 }
 
-template <bool FP8, bool NN, int LP, bool SPLIT>
+template <bool FP8, bool NN, int LP, bool SPLIT, bool DS = false>
 hipError_t wproj2_go(const void* A, int64_t lda, int64_t m, int64_t n, const bf16_t* Shi, const bf16_t* Slo,
                      const WProjPlan& p, float* slabs, float* Out, hipStream_t s, hipEvent_t done) {
-    typedef W2Shape<LP, SPLIT, FP8> SH;
+    typedef W2Shape<LP, SPLIT, FP8, DS> SH;
     const int64_t rows_out = NN ? m : n, K = NN ? n : m;
     float* o = p.splits == 1 ? Out : slabs;
     const int64_t stride = rows_out * LP;
-    hipLaunchKernelGGL((wproj2_kernel<FP8, NN, LP, SPLIT>), dim3(p.blocks * p.splits), dim3(512), SH::LDS, s, A, lda,
+    hipLaunchKernelGGL((wproj2_kernel<FP8, NN, LP, SPLIT, DS>), dim3(p.blocks * p.splits), dim3(512), SH::LDS, s, A, lda,
                        rows_out, K, m, Shi, Slo, o, stride, p.chunk, p.blocks);
     hipError_t e = hipGetLastError();
     if (e == hipSuccess && done) e = hipEventRecord(done, s);
@@ -592,6 +612,11 @@ template <int LP>
 hipError_t wproj_lp(int nn, int fp8, const void* A, int64_t lda, int64_t m, int64_t n, const bf16_t* Shi,
                     const bf16_t* Slo, const WProjPlan& p, float* slabs, float* Out, hipStream_t s, hipEvent_t d) {
     const bool split = Slo != nullptr;
+    if constexpr (LP == 128) {
+        if (p.v2 && p.ds && !nn && !fp8)
+            return split ? wproj2_go<false, false, 128, true, true>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d)
+                         : wproj2_go<false, false, 128, false, true>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d);
+    }
     if constexpr (LP >= 128) {
         if (p.v2) {
 #define GO2(F)                                                                                   \
@@ -626,10 +651,11 @@ bool wproj_supported_lp(int LP) {
 
 int wproj_rows_per_block(int LP) { return LP <= 128 ? 256 : (LP == 256 ? 128 : 64); }
 
-WProjPlan plan_wproj(int64_t rows_out, int64_t K, int LP, bool v2) {
+WProjPlan plan_wproj(int64_t rows_out, int64_t K, int LP, bool v2, bool nn, bool fp8) {
     WProjPlan p;
     p.v2 = v2 && LP >= 128;
-    const int WI = p.v2 ? (LP == 128 ? 512 : (LP == 256 ? 256 : 128)) : wproj_rows_per_block(LP);
+    p.ds = p.v2 && LP == 128 && !nn && !fp8 && K % 64 == 0;  // double-step TN stages (whole 64-row K chunks)
+    const int WI = p.v2 ? (LP == 128 ? (p.ds ? 256 : 512) : (LP == 256 ? 256 : 128)) : wproj_rows_per_block(LP);
     p.blocks = (int)((rows_out + WI - 1) / WI);
     const int target = (p.v2 || LP >= 512) ? 256 : 512;  // one workgroup per CU (LDS ring / registers)
     int64_t splits = (target + p.blocks - 1) / p.blocks;
@@ -638,7 +664,8 @@ WProjPlan plan_wproj(int64_t rows_out, int64_t K, int LP, bool v2) {
     if (splits > 128) splits = 128;
     if (splits < 1) splits = 1;
     int64_t chunk = (K + splits - 1) / splits;
-    chunk = (chunk + KS - 1) / KS * KS;
+    const int kq = p.ds ? 2 * KS : KS;
+    chunk = (chunk + kq - 1) / kq * kq;
     p.chunk = chunk;
     p.splits = (int)((K + chunk - 1) / chunk);
     return p;

@@ -228,7 +228,7 @@ static void bench_proj() {
         float* Out;
         CK(hipMalloc(&Out, (size_t)mx * c.LP * 4));
         for (int v2 = 0; v2 < 2; ++v2) {
-            WProjPlan pnn = plan_wproj(c.m, c.n, c.LP, v2), ptn = plan_wproj(c.n, c.m, c.LP, v2);
+            WProjPlan pnn = plan_wproj(c.m, c.n, c.LP, v2), ptn = plan_wproj(c.n, c.m, c.LP, v2, false, c.fp8);
             float* slabs;
             CK(hipMalloc(&slabs, (size_t)std::max<int64_t>(pnn.splits * c.m, ptn.splits * c.n) * c.LP * 4));
             const double bytes = (double)c.m * c.n * esz, fl = 2.0 * c.m * c.n * c.LP;
@@ -334,7 +334,7 @@ static void check_proj() {  // v2 (LDS-DMA) against v1 on random bf16 / e4m3 dat
             CK(hipMemcpy(Sh, hS.data(), rows_s * LP * 2, hipMemcpyHostToDevice));
             CK(hipMemcpy(Sl, hL.data(), rows_s * LP * 2, hipMemcpyHostToDevice));
             const int64_t ro = nn ? m : n, K = nn ? n : m;
-            WProjPlan p1 = plan_wproj(ro, K, LP, false), p2 = plan_wproj(ro, K, LP, true);
+            WProjPlan p1 = plan_wproj(ro, K, LP, false, nn, fp8), p2 = plan_wproj(ro, K, LP, true, nn, fp8);
             CK(launch_wproj(nn, fp8, A, m, m, n, Sh, Sl, LP, p1, sl, O1, S));
             CK(launch_wproj(nn, fp8, A, m, m, n, Sh, Sl, LP, p2, sl, O2, S));
             CK(hipStreamSynchronize(S));
