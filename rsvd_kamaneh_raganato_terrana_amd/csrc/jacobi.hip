@@ -106,7 +106,7 @@ __device__ __forceinline__ void rr_pair(int round, int k, int N, int& p, int& q)
 // contiguous rows sub * CH .. (vector LDS accesses); columns are CS apart.
 template <typename C, int LP>
 struct JacobiShape {
-    static constexpr int TPP = (LP <= 32 || sizeof(C) == 8) ? 16 : 8;  // threads per column pair
+    static constexpr int TPP = 16;  // threads per column pair (the round is issue-bound: more threads, shorter chains)
     static constexpr int CH = LP / TPP;                                // rows per thread (even)
     static constexpr int CS = LP + 16 / (int)sizeof(C);                // column stride: 16-B aligned, staggered banks
     static constexpr int NTHR = (LP / 2) * TPP;                        // one pair per TPP threads
