@@ -102,7 +102,12 @@ def pmc_traffic(key, kernel_prefix):
     import glob
 
     best = None
-    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_traffic.json"))):
+    import re
+
+    def natural(f):  # r01_v7 < r01_v11: the newest pass for a workload wins
+        return [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", os.path.basename(f))]
+
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_traffic.json")), key=natural):
         try:
             d = json.load(open(f))
         except (OSError, ValueError):
