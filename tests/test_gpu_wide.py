@@ -74,8 +74,10 @@ def test_wide_f32_device(engine):
     _check(U, S, V, Uo, So, Vo, A.astype(np.float64), 1e-4, 1e-4)
 
 
+# (4096, 1024, 128, 1) and (2048, 900, 100, 2) run the two-k-step TN stages (LP = 128, m % 64 == 0);
+# (1000, 700, 128, 1) the single-step fallback (m % 64 != 0)
 @pytest.mark.parametrize("m,n,l,q", [(4096, 1024, 128, 1), (2048, 3000, 256, 2), (1024, 1536, 64, 2),
-                                     (700, 500, 16, 0)])
+                                     (700, 500, 16, 0), (1000, 700, 128, 1), (2048, 900, 100, 2)])
 def test_bf16_matches_oracle(engine, m, n, l, q):
     torch = _torch()
     A32 = gapped_matrix(m, n, 2 * l, decay=0.95, seed=l + q).astype(np.float32) * 10
