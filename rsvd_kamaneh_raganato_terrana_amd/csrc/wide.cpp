@@ -315,7 +315,8 @@ struct WideEngine {
         if (L.LP <= 64) {
             RSVD_CK(launch_small_svd<double>(R1, L.l, L.LP, Uw, Vw, Sd, h->dflags + 1, s));
         } else {
-            RSVD_CK(launch_block_jacobi<double>(R1, L.l, L.LP, JX, JJ, Uw, Vw, Sd, sync, h->dflags + 1, s));
+            RSVD_CK(launch_block_jacobi<double>(R1, L.l, L.LP, JX, JJ, Uw, Vw, Sd, sync, h->dflags + 1, s,
+                                                sizeof(T) == 4 ? 1e-8 : 1e-16));  // fp32 results: one sweep fewer
         }
         const double sc = (d->a_scale != 0.0) ? d->a_scale : 1.0;
         RSVD_CK(launch_convert_scale<T>(Sd, S, L.l, sc, s));

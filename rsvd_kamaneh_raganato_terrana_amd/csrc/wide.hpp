@@ -96,8 +96,10 @@ hipError_t launch_omega_lowp_from(const float* om, int64_t ld, int64_t n, int l,
 // double buffers), sync (72 words, zeroed here).  LP in {64, 96, ..., 512}.  info[0] = sweeps;
 // info[2] = 1 on a barrier timeout.
 template <typename T>
+// quad2: a sweep whose rotations all have (g^2 / ab) <= quad2 ends the iteration (the next sweep would
+// only square them): 1e-16 for fp64 results, 1e-8 for results delivered in fp32 (as jacobi.hip's fp32 path).
 hipError_t launch_block_jacobi(const double* R, int l, int LP, double* X, double* J, double* Uw, double* Vw, T* S,
-                               unsigned* sync, int* info, hipStream_t s);
+                               unsigned* sync, int* info, hipStream_t s, double quad2 = 1e-16);
 
 // ---- wide.cpp: the host pipeline ------------------------------------------------------------------
 // True when `d` runs on the wide engine (bf16 / fp8 A, or l > 64).

@@ -215,7 +215,7 @@ __device__ __forceinline__ void apply_pair_global(const double* __restrict__ Src
 __global__ __launch_bounds__(kBJThreads) void block_jacobi_kernel(const double* __restrict__ R, int l, int LP,
                                                            double* __restrict__ Xb, double* __restrict__ Jb,
                                                            double* __restrict__ scratch, unsigned* __restrict__ sync,
-                                                           int* __restrict__ info) {
+                                                           int* __restrict__ info, double quad2) {
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
     const int XP = LP + 1;
     double* Xs = reinterpret_cast<double*>(smem_raw);  // [32][LP + 1]: the pair's columns
@@ -231,7 +231,7 @@ __global__ __launch_bounds__(kBJThreads) void block_jacobi_kernel(const double* 
     const int nwg = gridDim.x, wg = blockIdx.x;
     const int NB = LP / 16;
     const int64_t L2 = (int64_t)LP * LP;
-    const double tol = (double)l * kEps, tol2 = tol * tol, quad2 = 1e-16;
+    const double tol = (double)l * kEps, tol2 = tol * tol;
 #ifdef RSVD_BJ_PROF
     long long bj_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     long long bj_last = wall_clock64();
@@ -535,12 +535,12 @@ __global__ __launch_bounds__(1024) void block_jacobi_finish_kernel(const double*
 
 template <typename T>
 hipError_t launch_block_jacobi(const double* R, int l, int LP, double* X, double* J, double* Uw, double* Vw, T* S,
-                               unsigned* sync, int* info, hipStream_t s) {
+                               unsigned* sync, int* info, hipStream_t s, double quad2) {
     if (LP % 32 || LP < 64 || LP > 512) return hipErrorInvalidValue;
     hipError_t e = hipMemsetAsync(sync, 0, kSyncWords * sizeof(unsigned), s);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(block_jacobi_kernel, dim3(LP / 32), dim3(kBJThreads), block_jacobi_lds(LP), s, R, l, LP, X, J, Uw,
-                       sync, info);
+                       sync, info, quad2);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     const size_t lds = (size_t)LP * 8 * 2 + (size_t)LP * 4 + 64;
@@ -549,9 +549,9 @@ hipError_t launch_block_jacobi(const double* R, int l, int LP, double* X, double
 }
 
 template hipError_t launch_block_jacobi<float>(const double*, int, int, double*, double*, double*, double*, float*,
-                                               unsigned*, int*, hipStream_t);
+                                               unsigned*, int*, hipStream_t, double);
 template hipError_t launch_block_jacobi<double>(const double*, int, int, double*, double*, double*, double*, double*,
-                                                unsigned*, int*, hipStream_t);
+                                                unsigned*, int*, hipStream_t, double);
 
 #ifdef RSVD_BJ_PROF
 void bj_prof_dump() {
