@@ -933,7 +933,9 @@ GramPlan plan_gram_wide(int64_t rows, int LP, int cross) {
     const int nb = (LP + 31) / 32;
     g.blocks = cross ? nb * nb : nb * (nb + 1) / 2;
     if (!cross && gram_sym_ok(LP)) {  // gram_sym_kernel: one workgroup per chunk, >= 64 rows each, <= 256 chunks
-        int64_t chunks = (rows + 63) / 64;
+        // >= max(64, LP) rows per chunk: a chunk's slab (LP^2 / 2 doubles) must not outweigh its rows
+        const int64_t rmin = LP > 64 ? LP : 64;
+        int64_t chunks = (rows + rmin - 1) / rmin;
         const int64_t cap = LP == 512 ? 128 : 256;  // LP = 512: 8 workgroups per chunk, 1 MB of slab per chunk
         if (chunks > cap) chunks = cap;
         if (chunks < 1) chunks = 1;
