@@ -120,6 +120,26 @@ def pmc_traffic(key, kernel_prefix):
     return best
 
 
+def pmc_mfma_busy(key, kernel_prefix):
+    """Fraction of SIMD cycles the dominant kernel kept the MFMA pipe busy, from a committed
+    rocprofv3 SQ_VALU_MFMA_BUSY_CYCLES / GRBM_GUI_ACTIVE pass (profiles/*_mfma_busy.json; counts
+    the issued hi/lo MFMAs, not just the algorithmic ones).  None when no pass for this workload."""
+    import glob
+
+    best = None
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_mfma_busy.json"))):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if d.get("workload") != key:
+            continue
+        for k, v in d.get("kernels", {}).items():
+            if k.startswith(kernel_prefix) and v.get("mfma_busy_frac") is not None:
+                best = (v["mfma_busy_frac"], os.path.relpath(f, REPO))
+    return best
+
+
 def cpu_baseline(A_host, l, q, budget_s, threads, note):
     import oracle
 
@@ -246,10 +266,11 @@ def main():
     lowp = dt in ("bf16", "fp8")
     if lowp:  # the LDS-DMA kernel wproj2_kernel<FP8, NN, LP, SPLIT> (hi/lo split skinny operand)
         nn_k = "true" if kname.startswith("proj_nn") else "false"
-        kpref = f"wproj2_kernel<{'true' if dt == 'fp8' else 'false'}, {nn_k}, {lp_pad(l)}, true>"
+        kpref = f"wproj2_kernel<{'true' if dt == 'fp8' else 'false'}, {nn_k}, {lp_pad(l)}, true"  # [, DS]>
     else:
         kpref = "proj_tn_kernel" if kname.startswith("proj_tn") else "proj_nn_kernel"
     tr = pmc_traffic(key, kpref)
+    mb = pmc_mfma_busy(key, kpref)
     roof = {
         "bound": bound,
         "kernel": kname,
@@ -260,6 +281,8 @@ def main():
         "traffic": tr[0] if tr else None,
         "traffic_unit": "bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)",
         "traffic_source": tr[1] if tr else None,
+        "mfma_busy_frac_pmc": mb[0] if mb else None,
+        "mfma_busy_source": mb[1] if mb else None,
         "avg_launch_us": avg_ms * 1e3,
         "algorithmic_flop_per_launch": flop_launch,
         "algorithmic_bytes_per_launch": a_bytes,

@@ -30,14 +30,16 @@ def main():
     fetch, nf = per_kernel(os.path.join(root, "fetch", "run_counter_collection.csv"))
     write, _ = per_kernel(os.path.join(root, "write", "run_counter_collection.csv"))
     out = {"workload": key, "source": root,
-           "correction": "FETCH_SIZE x2 (gfx950: 128-B requests tallied at 64 B), except the TN wproj2 kernels "
-                         "(x1: their A reads are 64-B (bf16) / 32-B (e4m3) runs per column and k-step, one "
+           "correction": "FETCH_SIZE x2 (gfx950: 128-B requests tallied at 64 B), except the single-step TN wproj2 "
+                         "kernels (x1: their A reads are 64-B (bf16) / 32-B (e4m3) runs per column and k-step, one "
                          "request each -- uncalibrated width, taken as tallied); WRITE_SIZE x1",
            "kernels": {}}
     for k in fetch:
         if not (k.startswith("rsvd::") or "proj" in k or "gram" in k or "svd" in k or "panel" in k):
             continue
-        tn_short_runs = k.startswith("wproj2_kernel<") and k.split(",")[1].strip() == "false"
+        args = [a.strip(" >") for a in k[len("wproj2_kernel<"):].split(",")] if k.startswith("wproj2_kernel<") else []
+        # TN (NN = false) single-step stages read 64-B / 32-B runs; two-step stages (DS = true) 128-B runs
+        tn_short_runs = len(args) >= 4 and args[1] == "false" and not (len(args) >= 5 and args[4] == "true")
         f = (1 if tn_short_runs else 2) * fetch[k] * 1024
         w = write.get(k, 0.0) * 1024
         out["kernels"][k] = {"dispatches": nf[k], "fetch_bytes": f, "write_bytes": w, "hbm_bytes": f + w}
