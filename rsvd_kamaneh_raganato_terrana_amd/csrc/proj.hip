@@ -330,12 +330,14 @@ __global__ __launch_bounds__(kWave* kWaves) void proj_tn_kernel(
 
 int64_t round_up(int64_t x, int64_t q) { return (x + q - 1) / q * q; }
 
-// Pick the K split so the grid has ~2 workgroups per CU (256 CUs) while every wave keeps
-// at least ~8 MFMA groups of work and the slab traffic stays bounded.
+// Pick the K split so the grid has ~1 workgroup per CU (256 CUs) while every wave keeps at least
+// ~8 MFMA groups of work and the slab traffic stays bounded.  Measured on C2 (tools/kernel_lab,
+// grid target 128 / 192 / 256 / 320 / 512 / 1024 workgroups): 256 is best -- NN 29.7 us (splits 4),
+// TN 27.0 us (splits 2) against 33.4 / 31.6 us at 512; odd split counts lose more.
 ProjPlan make_plan(int64_t K, int blocks, int64_t kstep_wg) {
     ProjPlan p;
     p.blocks = blocks;
-    int64_t splits = (512 + blocks - 1) / blocks;
+    int64_t splits = (256 + blocks - 1) / blocks;
     const int64_t max_by_work = K / (kstep_wg * 8);
     if (splits > max_by_work) splits = max_by_work;
     if (splits > 32) splits = 32;
