@@ -126,8 +126,13 @@ def pmc_mfma_busy(key, kernel_prefix):
     the issued hi/lo MFMAs, not just the algorithmic ones).  None when no pass for this workload."""
     import glob
 
+    import re
+
+    def natural(f):
+        return [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", os.path.basename(f))]
+
     best = None
-    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_mfma_busy.json"))):
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_mfma_busy.json")), key=natural):
         try:
             d = json.load(open(f))
         except (OSError, ValueError):
