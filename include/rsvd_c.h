@@ -74,7 +74,8 @@ typedef struct {
     int32_t qr_mode;           /* rsvd_qr_mode_t                                               */
     int32_t reserved;
     uint64_t seed;             /* Philox key for Omega when no Omega is supplied               */
-    double a_scale;            /* A = a_scale * (stored A); 0 means 1 (used for FP8_E4M3)      */
+    double a_scale;            /* A = a_scale * (stored A); 0 means 1 (any dtype; S scales by
+                                  |a_scale|, V flips sign when a_scale < 0)                        */
 } rsvd_desc_t;
 
 /* Diagnostics of the last run on a handle. */
@@ -99,6 +100,14 @@ int rsvd_create(int device, rsvd_handle_t *out);
 int rsvd_destroy(rsvd_handle_t h);
 int rsvd_set_stream(rsvd_handle_t h, void *hip_stream);
 const char *rsvd_last_error(rsvd_handle_t h);
+/* Synchronise the handle's stream and report what the queued runs could not report at enqueue
+ * time: RSVD_ERR_HIP for an in-kernel hand-off or grid barrier that timed out,
+ * RSVD_ERR_NUMERICAL for a rank-deficient panel the repair pass could not complete or for
+ * non-finite singular values.  These conditions are sticky on the handle until reported (by this
+ * call or rsvd_get_info), so one rsvd_sync after several asynchronous rsvd_run calls checks them
+ * all.  The *_host_* entry points end with it. */
+int rsvd_sync(rsvd_handle_t h);
+/* rsvd_sync, then the diagnostics of the last run. */
 int rsvd_get_info(rsvd_handle_t h, rsvd_info_t *info);
 /* Row-sharded runs: this handle owns rows [offset, offset + m_local) of a global m x n A; the
  * hook sums the n x l partial products A_g^T Q_g and the l x l Grams across ranks. */

@@ -33,7 +33,7 @@ QR_AUTO, QR_GS2, QR_CHOLQR2 = 0, 1, 2
 # Every symbol include/rsvd_c.h declares (checked by tests/test_capi_exports.py).
 EXPORTS = (
     "rsvd_status_string", "rsvd_abi_version", "rsvd_create", "rsvd_destroy", "rsvd_set_stream",
-    "rsvd_last_error", "rsvd_get_info", "rsvd_set_comm", "rsvd_row_partition",
+    "rsvd_last_error", "rsvd_sync", "rsvd_get_info", "rsvd_set_comm", "rsvd_row_partition",
     "rsvd_workspace_bytes", "rsvd_set_workspace", "rsvd_set_timing", "rsvd_get_timing", "rsvd_run", "rsvd_range_finder",
     "rsvd_generate_omega", "rsvd_run_host_f64", "rsvd_range_finder_host_f64",
     "rsvd_generate_omega_host_f64", "rsvd_qr", "rsvd_svd", "rsvd_qr_workspace_bytes",
@@ -68,23 +68,46 @@ ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, c
                                 ctypes.c_void_p, ctypes.c_void_p)
 
 
-def _up_to_date() -> bool:
-    if not os.path.exists(LIB_PATH):
-        return False
-    t = os.path.getmtime(LIB_PATH)
-    srcs = [os.path.join(CSRC, f) for f in os.listdir(CSRC)]
-    srcs.append(os.path.join(REPO, "include", "rsvd_c.h"))
-    return all(os.path.getmtime(p) <= t for p in srcs if os.path.isfile(p))
+def _sources():
+    """The files librsvd_hip.so is built from, in the order the Makefile hashes them."""
+    hip = "util.hip proj.hip qr.hip jacobi.hip wide_proj.hip wide_qr.hip wide_svd.hip dense.hip".split()
+    cpp = "driver.cpp wide.cpp dense_api.cpp".split()
+    hdr = "common.hpp kernels.hpp wide.hpp dense.hpp handle.hpp".split()
+    return ([os.path.join(CSRC, f) for f in hip + cpp + hdr] + [os.path.join(REPO, "include", "rsvd_c.h")]
+            + [os.path.join(CSRC, "Makefile")])
 
 
-def build(jobs: int = 8, force: bool = False) -> str:
-    """Compile librsvd_hip.so for gfx950 with hipcc (cross-compiles without a GPU)."""
-    if not force and _up_to_date():
+def source_hash() -> str:
+    """sha256 of the library's sources (the Makefile writes the same digest next to the .so)."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for p in _sources():
+        with open(p, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()
+
+
+def built_hash():
+    try:
+        with open(LIB_PATH + ".sha256") as f:
+            return f.read().split()[0]
+    except (OSError, IndexError):
+        return None
+
+
+def build(jobs: int = 8, force: bool = True) -> str:
+    """Compile librsvd_hip.so for gfx950 with hipcc (cross-compiles without a GPU).
+
+    force=True (what __graft_entry__.build() uses) recompiles every object from scratch; otherwise
+    the library is rebuilt unless its recorded source digest matches the current sources."""
+    if not force and os.path.exists(LIB_PATH) and built_hash() == source_hash():
         return LIB_PATH
-    cmd = ["make", "-C", CSRC, f"-j{jobs}"]
     if force:
         subprocess.run(["make", "-C", CSRC, "clean"], check=True, capture_output=True)
-    subprocess.run(cmd, check=True)
+    subprocess.run(["make", "-C", CSRC, f"-j{jobs}"], check=True)
+    if built_hash() != source_hash():
+        raise RuntimeError("librsvd_hip.so was built but its source digest does not match the sources")
     return LIB_PATH
 
 
@@ -98,6 +121,8 @@ def lib():
         return _LIB
     if not os.path.exists(LIB_PATH):
         raise RuntimeError(f"{LIB_PATH} is missing: run rsvd_kamaneh_raganato_terrana_amd.build()")
+    if built_hash() != source_hash():
+        raise RuntimeError(f"{LIB_PATH} is stale (its recorded source digest differs from csrc/): rebuild it")
     L = ctypes.CDLL(LIB_PATH)
     vp, i32, i64, u64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64
     dp = ctypes.POINTER(ctypes.c_double)
@@ -108,6 +133,7 @@ def lib():
     L.rsvd_create.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
     L.rsvd_destroy.argtypes = [vp]
     L.rsvd_set_stream.argtypes = [vp, vp]
+    L.rsvd_sync.argtypes = [vp]
     L.rsvd_get_info.argtypes = [vp, ctypes.POINTER(Info)]
     L.rsvd_set_comm.argtypes = [vp, ctypes.c_int, ctypes.c_int, ALLREDUCE_FN, vp]
     L.rsvd_row_partition.restype = i64

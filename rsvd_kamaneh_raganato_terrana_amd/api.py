@@ -153,6 +153,11 @@ class Engine:
         check(lib().rsvd_get_timing(self.h, ctypes.byref(t)), self.h)
         return {k: getattr(t, k) for k, _ in Timing._fields_}
 
+    def sync(self):
+        """rsvd_sync: wait for the queued runs and raise what they could not report at enqueue time
+        (a timed-out in-kernel hand-off, an unrepairable rank deficiency, non-finite S)."""
+        check(lib().rsvd_sync(self.h), self.h)
+
     def info(self) -> dict:
         inf = Info()
         check(lib().rsvd_get_info(self.h, ctypes.byref(inf)), self.h)
@@ -184,8 +189,11 @@ class Engine:
                     method=int(method), qr_mode=int(qr_mode), reserved=0, seed=seed, a_scale=a_scale)
 
     def rsvd(self, A, l: int, q: int = 2, method: int = SVDMethod.Jacobi, omega=None, seed: int = 0,
-             qr_mode: int = QRMode.Auto, out=None, a_scale: float = 1.0):
-        """Device rSVD: A (m x n, CUDA, column-major f64/f32/bf16/e4m3) -> U (m x l), S (l), V (n x l)."""
+             qr_mode: int = QRMode.Auto, out=None, a_scale: float = 1.0, check_errors: bool = True):
+        """Device rSVD: A (m x n, CUDA, column-major f64/f32/bf16/e4m3) -> U (m x l), S (l), V (n x l).
+
+        check_errors=True synchronises and raises on the run's device-side failures (rsvd_sync);
+        False leaves the run queued (asynchronous) -- call sync() later to check."""
         torch = _torch()
         A, _ = colmajor(A)
         d = self.desc(A, l, q, method, seed, qr_mode, a_scale)
@@ -208,6 +216,8 @@ class Engine:
                              ctypes.c_void_p(U.data_ptr()), U.stride(1),
                              ctypes.c_void_p(S.data_ptr()),
                              ctypes.c_void_p(V.data_ptr()), V.stride(1)), self.h)
+        if check_errors:
+            self.sync()
         return U, S, V
 
     def range_finder(self, A, omega, q: int = 2, qr_mode: int = QRMode.Auto):
@@ -222,6 +232,7 @@ class Engine:
         check(lib().rsvd_range_finder(self.h, ctypes.byref(d), ctypes.c_void_p(A.data_ptr()),
                                       ctypes.c_void_p(om.data_ptr()), ldo, ctypes.c_void_p(Q.data_ptr()),
                                       Q.stride(1)), self.h)
+        self.sync()
         return Q
 
     def generate_omega(self, n: int, l: int, seed: int = 0, dtype=None):
@@ -293,6 +304,7 @@ class Engine:
         check(lib().rsvd_qr(self.h, m, n, ctypes.c_void_p(A.data_ptr()), lda, dt, int(full),
                             ctypes.c_void_p(Q.data_ptr()), Q.stride(1), ctypes.c_void_p(R.data_ptr()),
                             max(1, R.stride(1))), self.h)
+        self.sync()
         return Q, R
 
     def svd(self, A, method: int = SVDMethod.Jacobi, r: int = 0, seed: int = 0):
@@ -311,6 +323,7 @@ class Engine:
         check(lib().rsvd_svd(self.h, m, n, ctypes.c_void_p(A.data_ptr()), lda, dt, int(method), r, seed,
                              ctypes.c_void_p(U.data_ptr()), U.stride(1), ctypes.c_void_p(S.data_ptr()),
                              ctypes.c_void_p(V.data_ptr()), V.stride(1), ctypes.byref(kept)), self.h)
+        self.sync()
         kk = kept.value
         return U[:, :kk], S[:kk], V[:, :kk]
 

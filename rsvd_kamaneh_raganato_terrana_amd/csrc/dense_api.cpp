@@ -137,7 +137,7 @@ struct DenseEngine {
         RSVD_TRY(pass(In, k, T1, true, nullptr));
         RSVD_TRY(pass(T1, k, T2, false, nullptr));
         RSVD_TRY(pass(T2, k, Q, false, nullptr));
-        RSVD_CK(launch_repair_panel<T>(Q, L.rows, k, L.LP, colflag, flag, seed, 0, L.rows, T1, s));
+        RSVD_CK(launch_repair_panel<T>(Q, L.rows, k, L.LP, colflag, flag, seed, 0, L.rows, L.rows, T1, s));
         RSVD_TRY(pass(T1, k, Q, false, flag));
         return RSVD_OK;
     }
@@ -148,7 +148,7 @@ bool ok_dtype(int dt) { return dt == RSVD_F64 || dt == RSVD_F32; }
 int prepare(rsvd_handle_t h, size_t bytes) {
     RSVD_CK(hipSetDevice(h->device));
     RSVD_TRY(ensure_ws(h, bytes));
-    RSVD_CK(hipMemsetAsync(h->dflags, 0, kFlagWords * sizeof(int), h->stream));
+    RSVD_CK(reset_run_flags(h->dflags, h->stream));
     return RSVD_OK;
 }
 
@@ -359,8 +359,7 @@ int rsvd_qr_host_f64(rsvd_handle_t h, int64_t m, int64_t n, const double* A, int
     RSVD_TRY(rsvd_qr(h, m, n, dA.p, m, RSVD_F64, full, dQ.p, m, dR.p, kq));
     RSVD_CK(hipMemcpyAsync(Q, dQ.p, sizeof(double) * m * kq, hipMemcpyDeviceToHost, h->stream));
     RSVD_CK(hipMemcpyAsync(R, dR.p, sizeof(double) * kq * n, hipMemcpyDeviceToHost, h->stream));
-    RSVD_CK(hipStreamSynchronize(h->stream));
-    return RSVD_OK;
+    return rsvd_sync(h);
 }
 
 int rsvd_svd_host_f64(rsvd_handle_t h, int64_t m, int64_t n, const double* A, int64_t lda, int32_t method, int32_t r,
@@ -380,8 +379,7 @@ int rsvd_svd_host_f64(rsvd_handle_t h, int64_t m, int64_t n, const double* A, in
     RSVD_CK(hipMemcpyAsync(U, dU.p, sizeof(double) * m * kk, hipMemcpyDeviceToHost, h->stream));
     RSVD_CK(hipMemcpyAsync(S, dS.p, sizeof(double) * kk, hipMemcpyDeviceToHost, h->stream));
     RSVD_CK(hipMemcpyAsync(V, dV.p, sizeof(double) * n * kk, hipMemcpyDeviceToHost, h->stream));
-    RSVD_CK(hipStreamSynchronize(h->stream));
-    return RSVD_OK;
+    return rsvd_sync(h);
 }
 
 }  // extern "C"

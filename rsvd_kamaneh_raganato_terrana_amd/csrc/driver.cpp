@@ -11,14 +11,13 @@
 //   W = R^T = U_w S V_w^T (jacobi.hip)                  SVD<Jacobi>          SVD_class.hpp:126-178
 //   U = Q U_w ; V = Q_B V_w (panel_small)               U = Q * Utilde       src/rSVD.cpp:128
 //
-// Row sharding (world > 1): the handle holds rows [off, off + m_local) of A (src/rSVD.cpp:20-23
-// split).  The m-side panels stay sharded (their l x l Grams are summed through the all-reduce
-// hook), the n-side panels A^T Q = sum_g A_g^T Q_g are summed through the hook and then
-// orthonormalised redundantly on every rank, so every rank ends with the same Q_B, S, V and
-// its own rows of U.
+// Row-sharded runs (world > 1) go to the wide engine (wide.cpp), which owns the distributed
+// orthonormalisation (Gram all-reduce, rank-deficiency repair with disjoint Philox draws per rank)
+// for every l and dtype; this narrow engine is the single-GPU fast path for fp32 / fp64, l <= 64.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -64,6 +63,9 @@ struct Layout {
     }
 };
 
+// A = a_scale * (stored A); 0 means 1 (rsvd_c.h)
+double a_scale_of(const rsvd_desc_t* d) { return d->a_scale != 0.0 ? d->a_scale : 1.0; }
+
 int check_desc_msg(const rsvd_desc_t* d, const char** err) {
     if (!d) { *err = "null descriptor"; return RSVD_ERR_INVALID_ARG; }
     if (d->m <= 0 || d->n <= 0 || d->l <= 0 || d->q < 0 || d->lda < d->m) {
@@ -78,6 +80,7 @@ int check_desc_msg(const rsvd_desc_t* d, const char** err) {
     }
     if (d->l > 512) { *err = "l > 512 not supported"; return RSVD_ERR_UNSUPPORTED; }
     if (d->l > d->n || d->l > d->m) { *err = "l > min(m, n) not supported"; return RSVD_ERR_UNSUPPORTED; }
+    if (!std::isfinite(d->a_scale)) { *err = "a_scale is not finite"; return RSVD_ERR_INVALID_ARG; }
     return RSVD_OK;
 }
 
@@ -118,27 +121,16 @@ struct Engine {
         ctr = reinterpret_cast<unsigned*>(b + L.off_ctr);
     }
 
-    int allreduce(void* buf, int64_t count, int32_t dtype) {
-        if (h->world <= 1 || !h->allreduce) return RSVD_OK;
-        if (h->allreduce(buf, count, dtype, (void*)s, h->ar_user) != 0) {
-            h->err = "all-reduce hook failed";
-            return RSVD_ERR_COMM;
-        }
-        return RSVD_OK;
-    }
-
     // Per-orth breakdown flags live at dflags[4 + k] (k = orth index within the run, < 12).
     int orth_index = 0;
     int* cur_flag = nullptr;
 
-    // One CholeskyQR pass: R = chol(P^T P) (Gram summed over ranks when `sharded`), Out = P R^-1
-    // (Out may alias P: panel_small stages its rows before writing).  f32: factor in fp32 (the
-    // subspace-only intermediates of the fp32 path, see qr.hip) or fp64.  pred: a predicated pass
-    // (skipped unless *pred != 0) on counters of its own.  refine: receives the need for a second
-    // pass (cond_F(R) too large for one, or a breakdown).
+    // One CholeskyQR pass: R = chol(P^T P), Out = P R^-1 (Out may alias P: panel_small stages its
+    // rows before writing).  f32: factor in fp32 (the subspace-only intermediates of the fp32 path,
+    // see qr.hip) or fp64.  pred: a predicated pass (skipped unless *pred != 0) on counters of its
+    // own.  refine: receives the need for a second pass (cond_F(R) too large for one, or a breakdown).
     int npred = 0, nref = 0;
-    int cholqr_pass(const T* P, int64_t rows, T* Out, bool sharded, int f32, const int* pred = nullptr,
-                    int* refine = nullptr) {
+    int cholqr_pass(const T* P, int64_t rows, T* Out, int f32, const int* pred = nullptr, int* refine = nullptr) {
         const int nb = plan_gram_blocks(rows);
         double* tiles = gram + 32 * (size_t)L.LP * L.LP;
         unsigned* c = ctr;
@@ -153,15 +145,8 @@ struct Engine {
             t0 = tgt0;
             t1 = tgt1;
         }
-        if (sharded && h->world > 1) {
-            RSVD_CK(launch_gram_chol<T>(P, rows, L.LP, nb, gram, tiles, c, t0, t1, 0, f32, Gsum, L.l, nullptr,
-                                        nullptr, cur_flag, s, pred));
-            RSVD_TRY(allreduce(Gsum, (int64_t)L.LP * L.LP, RSVD_F64));
-            RSVD_CK(launch_chol(Gsum, L.l, L.LP, f32, R1, Rinv, cur_flag, s));
-        } else {
-            RSVD_CK(launch_gram_chol<T>(P, rows, L.LP, nb, gram, tiles, c, t0, t1, 1, f32, nullptr, L.l, R1, Rinv,
-                                        cur_flag, s, pred, refine));
-        }
+        RSVD_CK(launch_gram_chol<T>(P, rows, L.LP, nb, gram, tiles, c, t0, t1, 1, f32, nullptr, L.l, R1, Rinv,
+                                    cur_flag, h->dflags + kFlagGramTimeout, s, pred, refine));
         RSVD_CK(launch_panel_small<T>(P, rows, L.LP, Rinv, Out, 0, 0, 0, s, pred));
         return RSVD_OK;
     }
@@ -171,11 +156,10 @@ struct Engine {
     // the first one's R is too ill-conditioned for one pass (device-side predicate); fp64 panels
     // and qr_mode CHOLQR2 always run two.  Output panels keep the predicated fallback that
     // rebuilds Q from P (CGS2 + random completion, util.hip) if any pass flagged a bad pivot.
-    int orth(const T* P, int64_t rows, T* Q, bool sharded, int passes) {
+    int orth(const T* P, int64_t rows, T* Q, int passes) {
         cur_flag = h->dflags + 4 + (orth_index < 12 ? orth_index : 11);
         ++orth_index;
-        const bool dist = sharded && h->world > 1;
-        if (qr_mode == RSVD_QR_GS2 && !dist) {  // always the Gram-Schmidt path
+        if (qr_mode == RSVD_QR_GS2) {  // always the Gram-Schmidt path
             RSVD_CK(hipMemsetAsync(cur_flag, 0xFF, sizeof(int), s));
             RSVD_CK(launch_robust_orth<T>(P, rows, L.l, L.LP, Q, cur_flag, 0x5EEDull + orth_index, s));
             return RSVD_OK;
@@ -184,18 +168,16 @@ struct Engine {
         const bool output = passes >= 2;
         const int f32 = sizeof(T) == 4;
         if (!output) {
-            RSVD_TRY(cholqr_pass(P, rows, Q, sharded, f32));
-        } else if (f32 && qr_mode == RSVD_QR_AUTO && !dist) {
+            RSVD_TRY(cholqr_pass(P, rows, Q, f32));
+        } else if (f32 && qr_mode == RSVD_QR_AUTO) {
             int* refine = reinterpret_cast<int*>(ctr + 62 + (nref++ & 1));
-            RSVD_TRY(cholqr_pass(P, rows, Q, sharded, 0, nullptr, refine));
-            RSVD_TRY(cholqr_pass(Q, rows, Q, sharded, 0, refine, nullptr));
+            RSVD_TRY(cholqr_pass(P, rows, Q, 0, nullptr, refine));
+            RSVD_TRY(cholqr_pass(Q, rows, Q, 0, refine, nullptr));
         } else {
-            RSVD_TRY(cholqr_pass(P, rows, T1, sharded, f32));
-            RSVD_TRY(cholqr_pass(T1, rows, Q, sharded, f32));
+            RSVD_TRY(cholqr_pass(P, rows, T1, f32));
+            RSVD_TRY(cholqr_pass(T1, rows, Q, f32));
         }
-        if (output && !dist) {  // the sharded fallback is not implemented: the flag reports it
-            RSVD_CK(launch_robust_orth<T>(P, rows, L.l, L.LP, Q, cur_flag, 0x5EEDull + orth_index, s));
-        }
+        if (output) RSVD_CK(launch_robust_orth<T>(P, rows, L.l, L.LP, Q, cur_flag, 0x5EEDull + orth_index, s));
         return RSVD_OK;
     }
 
@@ -205,7 +187,8 @@ struct Engine {
         double* tiles = gram + 32 * (size_t)L.LP * L.LP;
         tgt0 += nb;
         tgt1 += gram_tiles(L.LP, 1);
-        RSVD_CK(launch_cross_gram<T>(P, P2, rows, L.LP, nb, gram, tiles, ctr, tgt0, tgt1, Gout, L.l, h->dflags, s));
+        RSVD_CK(launch_cross_gram<T>(P, P2, rows, L.LP, nb, gram, tiles, ctr, tgt0, tgt1, Gout, L.l,
+                                     h->dflags + kFlagGramTimeout, s));
         return RSVD_OK;
     }
 
@@ -239,8 +222,7 @@ struct Engine {
         int ev;
         RSVD_TRY(ev_begin(1, ev));
         RSVD_CK(launch_proj_tn<T>(A, lda, L.m, L.n, Q, L.LP, L.ptn, slab, Z, s, ev >= 0 ? h->ev_pool[ev + 1] : nullptr));
-        // Z = sum_g A_g^T Q_g over the row shards
-        return allreduce(Z, L.n * L.LP, sizeof(T) == 8 ? RSVD_F64 : RSVD_F32);
+        return RSVD_OK;
     }
 
     int load_omega(const void* omega, int64_t ldo, uint64_t seed) {
@@ -255,12 +237,12 @@ struct Engine {
     // intermediate_step (src/rSVD.cpp:57-70): leaves Q (m x LP panel) in Qm.
     int range_finder(const T* A, int64_t lda, int q) {
         RSVD_TRY(proj_nn(A, lda, Xn, Ym));
-        RSVD_TRY(orth(Ym, L.m, Qm, true, q == 0 ? 2 : inter_passes));
+        RSVD_TRY(orth(Ym, L.m, Qm, q == 0 ? 2 : inter_passes));
         for (int i = 0; i < q; ++i) {
             RSVD_TRY(proj_tn(A, lda, Qm, Zn));
-            RSVD_TRY(orth(Zn, L.n, Xn, false, inter_passes));
+            RSVD_TRY(orth(Zn, L.n, Xn, inter_passes));
             RSVD_TRY(proj_nn(A, lda, Xn, Ym));
-            RSVD_TRY(orth(Ym, L.m, Qm, true, i == q - 1 ? 2 : inter_passes));
+            RSVD_TRY(orth(Ym, L.m, Qm, i == q - 1 ? 2 : inter_passes));
         }
         return RSVD_OK;
     }
@@ -277,9 +259,17 @@ struct Engine {
         RSVD_CK(launch_power_prep(R1, Y0, L.l, L.LP, Pp, X0s, Bpm, s));
         RSVD_CK(launch_power_svd(Pp, L.l, L.l, L.LP, Bpm, L.l, 0, power_iterations(L.n), Up, Vc, Sd, h->dflags + 16,
                                  s, X0s, 1));
-        RSVD_CK(launch_convert_scale<T>(Sd, S, L.l, 1.0, s));
+        RSVD_CK(launch_convert_scale<T>(Sd, S, L.l, std::fabs(a_scale_of(d)), s));
         RSVD_CK(launch_panel_small<T>(Qm, L.m, L.LP, Up, reinterpret_cast<T*>(U), 1, L.l, ldu, s));
         RSVD_CK(launch_panel_small<T>(Xn, L.n, L.LP, Vc, reinterpret_cast<T*>(V), 1, L.l, ldv, s));
+        return finish(d, S, V, ldv);
+    }
+
+    // A = a_scale * (stored A) = U (|a_scale| S) (sign(a_scale) V)^T; then the finite check of S.
+    int finish(const rsvd_desc_t* d, T* S, void* V, int64_t ldv) {
+        const double sc = a_scale_of(d);
+        if (sc < 0.0) RSVD_CK(launch_scale_cols<T>(reinterpret_cast<T*>(V), L.n, L.l, ldv, -1.0, s));
+        RSVD_CK(launch_check_finite<T>(S, L.l, h->dflags + kFlagNonFinite, s));
         return RSVD_OK;
     }
 
@@ -287,14 +277,16 @@ struct Engine {
         RSVD_TRY(range_finder(A, d->lda, d->q));
         // Stage B: B^T = A^T Q, QR-preconditioned as in SVD_class.hpp:116-123.
         RSVD_TRY(proj_tn(A, d->lda, Qm, Zn));
-        RSVD_TRY(orth(Zn, L.n, Xn, false, 2));  // Xn = Q_B
+        RSVD_TRY(orth(Zn, L.n, Xn, 2));  // Xn = Q_B
         RSVD_TRY(cross_gram(Xn, Zn, L.n, R1));    // R = Q_B^T B^T exactly (fp64), W = R^T
         if (d->method == RSVD_SVD_POWER) return power_stage(d, U, ldu, S, V, ldv);
         RSVD_CK(launch_small_svd<T>(R1, L.l, L.LP, Uw, Vw, S, h->dflags + 1, s));
+        const double sc = std::fabs(a_scale_of(d));
+        if (sc != 1.0) RSVD_CK(launch_scale_cols<T>(S, L.l, 1, L.l, sc, s));
         const int dcols = L.l;  // d = min(l, n) = l (l <= n enforced)
         RSVD_CK(launch_panel_small<T>(Qm, L.m, L.LP, Uw, reinterpret_cast<T*>(U), 1, dcols, ldu, s));
         RSVD_CK(launch_panel_small<T>(Xn, L.n, L.LP, Vw, reinterpret_cast<T*>(V), 1, dcols, ldv, s));
-        return RSVD_OK;
+        return finish(d, S, V, ldv);
     }
 };
 
@@ -303,7 +295,7 @@ int run_typed(rsvd_handle_t h, const rsvd_desc_t* d, const void* A, const void* 
               int64_t ldu, void* S, void* V, int64_t ldv, void* Qout, int64_t ldq) {
     Layout<T> L(d->m, d->n, d->l);
     RSVD_TRY(ensure_ws(h, L.total));
-    RSVD_CK(hipMemsetAsync(h->dflags, 0, kFlagWords * sizeof(int), h->stream));
+    RSVD_CK(reset_run_flags(h->dflags, h->stream));
     RSVD_CK(hipMemsetAsync(h->ws + L.off_ctr, 0, 64 * sizeof(unsigned), h->stream));
     h->info.splits_nn = L.pnn.splits;
     h->info.splits_tn = L.ptn.splits;
@@ -400,20 +392,45 @@ int rsvd_set_stream(rsvd_handle_t h, void* stream) {
 
 const char* rsvd_last_error(rsvd_handle_t h) { return h ? h->err.c_str() : "null handle"; }
 
-int rsvd_get_info(rsvd_handle_t h, rsvd_info_t* info) {
-    if (!h || !info) return RSVD_ERR_INVALID_ARG;
+// Synchronise the handle's stream and turn the sticky device error words into a status
+// (clearing them): a timed-out in-kernel hand-off, a rank-deficiency repair that broke down again,
+// or non-finite singular values.  `flags` receives the whole flag block.
+static int sync_flags(rsvd_handle_t h, int* flags) {
     RSVD_TRY(set_device(h));
-    int flags[kFlagWords] = {0};
     RSVD_CK(hipMemcpyAsync(flags, h->dflags, kFlagWords * sizeof(int), hipMemcpyDeviceToHost, h->stream));
     RSVD_CK(hipStreamSynchronize(h->stream));
-    if (flags[2]) {
+    const int sticky[4] = {kFlagGramTimeout, kFlagJacobiTimeout, kFlagUnrepaired, kFlagNonFinite};
+    bool any = false;
+    for (int w : sticky) any = any || flags[w] != 0;
+    if (!any) return RSVD_OK;
+    for (int w : sticky) RSVD_CK(hipMemsetAsync(h->dflags + w, 0, sizeof(int), h->stream));
+    RSVD_CK(hipStreamSynchronize(h->stream));
+    if (flags[kFlagGramTimeout]) {
         h->err = "a Gram reduction timed out waiting for its producers";
         return RSVD_ERR_HIP;
     }
-    if (flags[3]) {
+    if (flags[kFlagJacobiTimeout]) {
         h->err = "the block Jacobi grid barrier timed out";
         return RSVD_ERR_HIP;
     }
+    if (flags[kFlagUnrepaired]) {
+        h->err = "a rank-deficient panel could not be re-orthonormalised";
+        return RSVD_ERR_NUMERICAL;
+    }
+    h->err = "non-finite singular values (A holds Inf / NaN, or the factorisation overflowed)";
+    return RSVD_ERR_NUMERICAL;
+}
+
+int rsvd_sync(rsvd_handle_t h) {
+    if (!h) return RSVD_ERR_INVALID_ARG;
+    int flags[kFlagWords] = {0};
+    return sync_flags(h, flags);
+}
+
+int rsvd_get_info(rsvd_handle_t h, rsvd_info_t* info) {
+    if (!h || !info) return RSVD_ERR_INVALID_ARG;
+    int flags[kFlagWords] = {0};
+    RSVD_TRY(sync_flags(h, flags));
     int fallbacks = 0;
     for (int k = 4; k < 16; ++k) fallbacks += flags[k] != 0;
     h->info.cholqr_fallbacks = fallbacks;
@@ -479,11 +496,12 @@ int rsvd_workspace_bytes(const rsvd_desc_t* d, size_t* bytes) {
     if (!d || !bytes) return RSVD_ERR_INVALID_ARG;
     const char* err = "";
     RSVD_TRY(check_desc_msg(d, &err));
-    if (wide_path(d)) return wide_workspace_bytes(d, bytes);
-    if (d->dtype == RSVD_F64)
-        *bytes = Layout<double>(d->m, d->n, d->l).total;
-    else
-        *bytes = Layout<float>(d->m, d->n, d->l).total;
+    RSVD_TRY(wide_workspace_bytes(d, bytes));
+    if (wide_path(d)) return RSVD_OK;
+    // narrow single-GPU layout, or the wide engine's when the handle is row-sharded: the larger
+    const size_t narrow = d->dtype == RSVD_F64 ? Layout<double>(d->m, d->n, d->l).total
+                                               : Layout<float>(d->m, d->n, d->l).total;
+    *bytes = std::max(*bytes, narrow);
     return RSVD_OK;
 }
 
@@ -496,7 +514,7 @@ int rsvd_run(rsvd_handle_t h, const rsvd_desc_t* d, const void* A, const void* o
         return RSVD_ERR_INVALID_ARG;
     }
     RSVD_TRY(set_device(h));
-    if (wide_path(d)) return wide_run(h, d, A, omega, ldo, U, ldu, S, V, ldv, nullptr, 0);
+    if (wide_path(d) || h->world > 1) return wide_run(h, d, A, omega, ldo, U, ldu, S, V, ldv, nullptr, 0);
     if (d->dtype == RSVD_F64) return run_typed<double>(h, d, A, omega, ldo, U, ldu, S, V, ldv, nullptr, 0);
     return run_typed<float>(h, d, A, omega, ldo, U, ldu, S, V, ldv, nullptr, 0);
 }
@@ -510,7 +528,7 @@ int rsvd_range_finder(rsvd_handle_t h, const rsvd_desc_t* d, const void* A, cons
         return RSVD_ERR_INVALID_ARG;
     }
     RSVD_TRY(set_device(h));
-    if (wide_path(d)) return wide_run(h, d, A, omega, ldo, nullptr, 0, nullptr, nullptr, 0, Q, ldq);
+    if (wide_path(d) || h->world > 1) return wide_run(h, d, A, omega, ldo, nullptr, 0, nullptr, nullptr, 0, Q, ldq);
     if (d->dtype == RSVD_F64) return run_typed<double>(h, d, A, omega, ldo, nullptr, 0, nullptr, nullptr, 0, Q, ldq);
     return run_typed<float>(h, d, A, omega, ldo, nullptr, 0, nullptr, nullptr, 0, Q, ldq);
 }
@@ -577,8 +595,7 @@ int rsvd_run_host_f64(rsvd_handle_t h, int64_t m, int64_t n, const double* A, in
     RSVD_CK(hipMemcpyAsync(U, dU.p, sizeof(double) * m * dd, hipMemcpyDeviceToHost, h->stream));
     RSVD_CK(hipMemcpyAsync(S, dS.p, sizeof(double) * dd, hipMemcpyDeviceToHost, h->stream));
     RSVD_CK(hipMemcpyAsync(V, dV.p, sizeof(double) * n * dd, hipMemcpyDeviceToHost, h->stream));
-    RSVD_CK(hipStreamSynchronize(h->stream));
-    return RSVD_OK;
+    return rsvd_sync(h);
 }
 
 int rsvd_range_finder_host_f64(rsvd_handle_t h, int64_t m, int64_t n, const double* A, int64_t lda,
@@ -598,8 +615,7 @@ int rsvd_range_finder_host_f64(rsvd_handle_t h, int64_t m, int64_t n, const doub
     RSVD_CK(hipMemcpyAsync(dO.p, omega, sizeof(double) * n * l, hipMemcpyHostToDevice, h->stream));
     RSVD_TRY(rsvd_range_finder(h, &d, dA.p, dO.p, n, dQ.p, m));
     RSVD_CK(hipMemcpyAsync(Q, dQ.p, sizeof(double) * m * l, hipMemcpyDeviceToHost, h->stream));
-    RSVD_CK(hipStreamSynchronize(h->stream));
-    return RSVD_OK;
+    return rsvd_sync(h);
 }
 
 int rsvd_generate_omega_host_f64(rsvd_handle_t h, int64_t n, int32_t l, uint64_t seed, double* omega) {

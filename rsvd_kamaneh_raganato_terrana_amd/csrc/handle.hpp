@@ -18,8 +18,11 @@ struct rsvd_handle_s {
     char* ws = nullptr;
     size_t ws_bytes = 0;
     bool ws_external = false;  // workspace supplied by the caller (rsvd_set_workspace)
-    // device flags: [1] jacobi sweeps, [2] Gram hand-off timeout, [3] block-Jacobi barrier timeout,
-    // [4..15] per-orthonormalisation breakdown flags, [16] power-method triplets kept
+    // device flags: [1] jacobi sweeps, [4..15] per-orthonormalisation breakdown flags, [16]
+    // power-method triplets kept -- reset at the start of every run; and the STICKY error words
+    // (kept across queued runs, cleared when rsvd_sync / rsvd_get_info report them):
+    // [2] Gram hand-off timeout, [3] block-Jacobi barrier timeout, [20] a rank-deficiency repair
+    // pass that broke down again, [21] non-finite singular values.
     int* dflags = nullptr;
     rsvd_info_t info{};
     int rank = 0, world = 1;
@@ -50,6 +53,14 @@ struct rsvd_handle_s {
     } while (0)
 
 constexpr int kFlagWords = 32;
+constexpr int kFlagGramTimeout = 2, kFlagJacobiTimeout = 3, kFlagUnrepaired = 20, kFlagNonFinite = 21;
+
+// Per-run reset of the non-sticky flag words ([0..1] and [4..19]; the sticky words stay).
+inline hipError_t reset_run_flags(int* dflags, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(dflags, 0, 2 * sizeof(int), s);
+    if (e != hipSuccess) return e;
+    return hipMemsetAsync(dflags + 4, 0, 16 * sizeof(int), s);
+}
 
 inline int lp_of(int l) { return (l + 15) / 16 * 16; }
 inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }

@@ -23,6 +23,13 @@ hipError_t launch_sum_slabs(const T* slabs, int64_t slab_stride, int nslab, int6
 template <typename T>
 hipError_t launch_panel_to_colmajor(const T* in, int64_t m, int cols, int LP, T* out, int64_t ld, hipStream_t s);
 
+// X (col-major rows x cols, ld) *= f
+template <typename T>
+hipError_t launch_scale_cols(T* X, int64_t rows, int cols, int64_t ld, double f, hipStream_t s);
+// *flag |= 1 when any of x[0..n) is not finite (one workgroup)
+template <typename T>
+hipError_t launch_check_finite(const T* x, int n, int* flag, hipStream_t s);
+
 // Fallback re-orthonormalisation of P into Q (CGS2 + deterministic random completion) when
 // *flag != 0; returns immediately otherwise.  One workgroup.
 template <typename T>
@@ -59,16 +66,17 @@ int gram_tiles(int LP, int cross);
 // bad pivot.  ctr[0..1] are run-cumulative arrival counters (zeroed per run): t0 = ctr[0] after
 // this launch's nb arrivals, t1 = ctr[1] after its tile reducers (gram_tiles(LP, 0)).
 // pred (nullable): the whole launch is skipped unless *pred != 0 (give such a launch counters of its
-// own).  refine (nullable, mode 1): set to 1 when cond_F(R) > 2e4 or a pivot broke down -- the
+// own).  tmo: the sticky timeout word (a bounded hand-off spin that expired sets it).  refine (nullable, mode 1): set to 1 when cond_F(R) > 2e4 or a pivot broke down -- the
 // predicate of an optional second CholeskyQR pass.
 template <typename T>
 hipError_t launch_gram_chol(const T* P, int64_t rows, int LP, int nb, double* slabs, double* tiles, unsigned* ctr,
                             unsigned t0, unsigned t1, int mode, int compute_f32, double* Gsum, int l, double* R,
-                            double* Rinv, int* flag, hipStream_t s, const int* pred = nullptr, int* refine = nullptr);
+                            double* Rinv, int* flag, int* tmo, hipStream_t s, const int* pred = nullptr,
+                            int* refine = nullptr);
 // Cross-Gram Gout = P^T P2 (LP x LP fp64, zero outside l x l); t1 advances by gram_tiles(LP, 1).
 template <typename T>
 hipError_t launch_cross_gram(const T* P, const T* P2, int64_t rows, int LP, int nb, double* slabs, double* tiles,
-                             unsigned* ctr, unsigned t0, unsigned t1, double* Gout, int l, int* flag, hipStream_t s);
+                             unsigned* ctr, unsigned t0, unsigned t1, double* Gout, int l, int* tmo, hipStream_t s);
 // Factor an already-summed Gram G (LP x LP) -- same outputs as mode 1 above.
 hipError_t launch_chol(const double* G, int l, int LP, int compute_f32, double* R, double* Rinv, int* flag,
                        hipStream_t s);

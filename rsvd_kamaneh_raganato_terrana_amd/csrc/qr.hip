@@ -229,12 +229,12 @@ __device__ __forceinline__ void write_factor(const double* Rs, const double* RIs
     }
 }
 
-__device__ __forceinline__ bool spin_until(unsigned* ctr, unsigned target, int* flag) {
+__device__ __forceinline__ bool spin_until(unsigned* ctr, unsigned target, int* tmo) {
     unsigned spins = 0;
     while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
         __builtin_amdgcn_s_sleep(1);
-        if (++spins > (1u << 26)) {  // ~seconds: never expected; report instead of hanging
-            atomicOr(flag + 2, 1);
+        if (++spins > (1u << 26)) {  // ~seconds: never expected; report (sticky word) instead of hanging
+            atomicOr(tmo, 1);
             return false;
         }
     }
@@ -257,7 +257,8 @@ __global__ __launch_bounds__(kWave* kGramWaves) void gram_kernel(
     const T* __restrict__ P, const T* __restrict__ P2, int64_t rows, int64_t chunk, int nb,
     double* __restrict__ slabs, double* __restrict__ tiles, unsigned* __restrict__ ctr, unsigned target0,
     unsigned target1, int mode, double* __restrict__ Gsum, int l, double* __restrict__ Rout,
-    double* __restrict__ Rinv, int* __restrict__ flag, const int* __restrict__ pred, int* __restrict__ refine) {
+    double* __restrict__ Rinv, int* __restrict__ flag, int* __restrict__ tmo, const int* __restrict__ pred,
+    int* __restrict__ refine) {
     constexpr int G = Tiles<LP, CROSS>::G, NT = Tiles<LP, CROSS>::NT;
     if (pred && *pred == 0) return;  // predicated pass (private counters: skipping disturbs no other launch)
     typedef Mfma<double> M;
@@ -324,7 +325,7 @@ __global__ __launch_bounds__(kWave* kGramWaves) void gram_kernel(
     if (b >= NT) return;
     // ---- phase 2: tile reducer ----
     if (threadIdx.x == 0) {
-        *ticket = spin_until(ctr, target0, flag) ? 1 : 0;
+        *ticket = spin_until(ctr, target0, tmo) ? 1 : 0;
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -498,12 +499,12 @@ size_t gram_lds_bytes() {
 template <typename T, typename C, int LP, bool CROSS>
 hipError_t gram_launch(const T* P, const T* P2, int64_t rows, int nb, double* slabs, double* tiles, unsigned* ctr,
                        unsigned t0, unsigned t1, int mode, double* Gsum, int l, double* R, double* Rinv, int* flag,
-                       hipStream_t s, const int* pred = nullptr, int* refine = nullptr) {
+                       int* tmo, hipStream_t s, const int* pred = nullptr, int* refine = nullptr) {
     const int64_t chunk = (rows + nb - 1) / nb;
     const int NT = Tiles<LP, CROSS>::NT;
     const int grid = nb > NT ? nb : NT;
     hipLaunchKernelGGL((gram_kernel<T, C, LP, CROSS>), dim3(grid), dim3(kWave * kGramWaves), (gram_lds_bytes<LP, CROSS>()),
-                       s, P, P2, rows, chunk, nb, slabs, tiles, ctr, t0, t1, mode, Gsum, l, R, Rinv, flag, pred, refine);
+                       s, P, P2, rows, chunk, nb, slabs, tiles, ctr, t0, t1, mode, Gsum, l, R, Rinv, flag, tmo, pred, refine);
     return hipGetLastError();
 }
 
@@ -524,14 +525,14 @@ int gram_tiles(int LP, int cross) {
 template <typename T>
 hipError_t launch_gram_chol(const T* P, int64_t rows, int LP, int nb, double* slabs, double* tiles, unsigned* ctr,
                             unsigned t0, unsigned t1, int mode, int compute_f32, double* Gsum, int l, double* R,
-                            double* Rinv, int* flag, hipStream_t s, const int* pred, int* refine) {
+                            double* Rinv, int* flag, int* tmo, hipStream_t s, const int* pred, int* refine) {
     switch (LP) {
 #define CASE(L)                                                                                                   \
     case L:                                                                                                       \
         return compute_f32 ? gram_launch<T, float, L, false>(P, nullptr, rows, nb, slabs, tiles, ctr, t0, t1, mode, \
-                                                              Gsum, l, R, Rinv, flag, s, pred, refine)             \
+                                                              Gsum, l, R, Rinv, flag, tmo, s, pred, refine)        \
                            : gram_launch<T, double, L, false>(P, nullptr, rows, nb, slabs, tiles, ctr, t0, t1, mode, \
-                                                               Gsum, l, R, Rinv, flag, s, pred, refine);
+                                                               Gsum, l, R, Rinv, flag, tmo, s, pred, refine);
         CASE(16) CASE(32) CASE(48) CASE(64)
 #undef CASE
         default: return hipErrorInvalidValue;
@@ -540,12 +541,12 @@ hipError_t launch_gram_chol(const T* P, int64_t rows, int LP, int nb, double* sl
 
 template <typename T>
 hipError_t launch_cross_gram(const T* P, const T* P2, int64_t rows, int LP, int nb, double* slabs, double* tiles,
-                             unsigned* ctr, unsigned t0, unsigned t1, double* Gout, int l, int* flag, hipStream_t s) {
+                             unsigned* ctr, unsigned t0, unsigned t1, double* Gout, int l, int* tmo, hipStream_t s) {
     switch (LP) {
 #define CASE(L)                                                                                                 \
     case L:                                                                                                     \
         return gram_launch<T, double, L, true>(P, P2, rows, nb, slabs, tiles, ctr, t0, t1, 0, Gout, l, nullptr, \
-                                               nullptr, flag, s);
+                                               nullptr, nullptr, tmo, s);
         CASE(16) CASE(32) CASE(48) CASE(64)
 #undef CASE
         default: return hipErrorInvalidValue;
@@ -590,7 +591,7 @@ hipError_t launch_panel_small(const T* In, int64_t rows, int LP, const double* M
 
 #define RSVD_INST(T)                                                                                             \
     template hipError_t launch_gram_chol<T>(const T*, int64_t, int, int, double*, double*, unsigned*, unsigned,    \
-                                            unsigned, int, int, double*, int, double*, double*, int*, hipStream_t, \
+                                            unsigned, int, int, double*, int, double*, double*, int*, int*, hipStream_t, \
                                             const int*, int*);                                                    \
     template hipError_t launch_cross_gram<T>(const T*, const T*, int64_t, int, int, double*, double*, unsigned*,   \
                                              unsigned, unsigned, double*, int, int*, hipStream_t);               \

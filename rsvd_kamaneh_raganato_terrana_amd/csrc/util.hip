@@ -67,6 +67,23 @@ __global__ void sum_slabs_kernel(const T* __restrict__ slabs, int64_t stride, in
     }
 }
 
+template <typename T>
+__global__ void scale_cols_kernel(T* __restrict__ X, int64_t rows, int cols, int64_t ld, double f) {
+    const int64_t total = rows * cols;
+    for (int64_t idx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; idx < total;
+         idx += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t j = idx / rows, i = idx - j * rows;
+        X[i + j * ld] = (T)((double)X[i + j * ld] * f);
+    }
+}
+
+template <typename T>
+__global__ void check_finite_kernel(const T* __restrict__ x, int n, int* __restrict__ flag) {
+    bool bad = false;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) bad = bad || !isfinite((double)x[i]);
+    if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
+}
+
 inline int grid_for(int64_t work, int block) {
     int64_t g = (work + block - 1) / block;
     if (g > 4096) g = 4096;
@@ -106,7 +123,21 @@ hipError_t launch_sum_slabs(const T* slabs, int64_t slab_stride, int nslab, int6
     return hipGetLastError();
 }
 
+template <typename T>
+hipError_t launch_scale_cols(T* X, int64_t rows, int cols, int64_t ld, double f, hipStream_t s) {
+    hipLaunchKernelGGL((scale_cols_kernel<T>), dim3(grid_for(rows * cols, 256)), dim3(256), 0, s, X, rows, cols, ld, f);
+    return hipGetLastError();
+}
+
+template <typename T>
+hipError_t launch_check_finite(const T* x, int n, int* flag, hipStream_t s) {
+    hipLaunchKernelGGL((check_finite_kernel<T>), dim3(1), dim3(256), 0, s, x, n, flag);
+    return hipGetLastError();
+}
+
 #define RSVD_INST(T)                                                                                    \
+    template hipError_t launch_scale_cols<T>(T*, int64_t, int, int64_t, double, hipStream_t);           \
+    template hipError_t launch_check_finite<T>(const T*, int, int*, hipStream_t);                       \
     template hipError_t launch_philox_omega<T>(T*, int64_t, int, int, uint64_t, hipStream_t);           \
     template hipError_t launch_colmajor_to_panel<T>(const T*, int64_t, int64_t, int, int, T*, hipStream_t); \
     template hipError_t launch_panel_to_colmajor<T>(const T*, int64_t, int, int, T*, int64_t, hipStream_t); \

@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <string>
 
 #include "handle.hpp"
@@ -129,7 +130,10 @@ struct WideEngine {
     int inter_passes = 1;  // power-iteration intermediates only carry a subspace (driver.cpp)
     int qr_mode = RSVD_QR_AUTO;
     int orth_index = 0;
-    int64_t row_off = 0, m_total = 0;  // this rank's rows of the m side
+    // Repair draws of the m side: rank g's rows are stream rows [g 2^40, g 2^40 + m_g) of a
+    // world x 2^40-row stream (disjoint for any shard sizes, src/rSVD.cpp:20-23 remainders included),
+    // normalised by the global row count estimate world * m_g.
+    int64_t row_off = 0, m_total = 0, m_norm = 0;
     uint64_t seed = 0;
 
     WideEngine(rsvd_handle_t h_, const WideLayout<T>& L_, int dtype_) : h(h_), L(L_), s(h_->stream), dtype(dtype_) {
@@ -245,10 +249,11 @@ struct WideEngine {
             RSVD_TRY(cholqr_pass(T1, rows, gp, Q, sharded, hi, lo, flag, nullptr));
         }
         if (repair) {
-            const int64_t off = mside ? row_off : 0, tot = mside ? m_total : L.n;
+            const int64_t off = mside ? row_off : 0, tot = mside ? m_total : L.n, nrm = mside ? m_norm : L.n;
             RSVD_CK(launch_repair_panel<T>(Q, rows, L.l, L.LP, colflag, flag, seed ^ (0x5EEDull + orth_index), off,
-                                           tot, T1, s));
-            RSVD_TRY(cholqr_pass(T1, rows, gp, Q, sharded, hi, lo, flag, flag));
+                                           tot, nrm, T1, s));
+            // a breakdown in the repaired pass is reported (sticky) by rsvd_sync as RSVD_ERR_NUMERICAL
+            RSVD_TRY(cholqr_pass(T1, rows, gp, Q, sharded, hi, lo, h->dflags + kFlagUnrepaired, flag));
         }
         return RSVD_OK;
     }
@@ -290,8 +295,7 @@ struct WideEngine {
         RSVD_CK(launch_power_prep(R1, Y0, L.l, L.LP, Pp, X0s, Bpm, s));
         RSVD_CK(launch_power_svd(Pp, L.l, L.l, L.LP, Bpm, L.l, 0, power_iterations(L.n), Up, Vc, Sd, h->dflags + 16,
                                  s, X0s, 1));
-        const double sc = (d->a_scale != 0.0) ? d->a_scale : 1.0;
-        RSVD_CK(launch_convert_scale<T>(Sd, S, L.l, sc, s));
+        RSVD_CK(launch_convert_scale<T>(Sd, S, L.l, std::fabs(a_scale(d)), s));
         if (sizeof(T) == 4) {
             const int L2 = L.LP * L.LP;
             RSVD_CK(launch_convert_scale<float>(Up, Uw32, L2, 1.0, s));
@@ -301,6 +305,14 @@ struct WideEngine {
                                      nullptr, nullptr, s));
         RSVD_CK(launch_panel_gemm<T>(Xn, L.n, L.LP, mat(Vc, Vw32), 0, reinterpret_cast<T*>(V), ldv, L.l, nullptr,
                                      nullptr, nullptr, s));
+        return finish(d, S, V, ldv);
+    }
+
+    static double a_scale(const rsvd_desc_t* d) { return d->a_scale != 0.0 ? d->a_scale : 1.0; }
+    // A = a_scale * (stored A) = U (|a_scale| S) (sign(a_scale) V)^T; then the finite check of S.
+    int finish(const rsvd_desc_t* d, T* S, void* V, int64_t ldv) {
+        if (a_scale(d) < 0.0) RSVD_CK(launch_scale_cols<T>(reinterpret_cast<T*>(V), L.n, L.l, ldv, -1.0, s));
+        RSVD_CK(launch_check_finite<T>(S, L.l, h->dflags + kFlagNonFinite, s));
         return RSVD_OK;
     }
 
@@ -318,8 +330,7 @@ struct WideEngine {
             RSVD_CK(launch_block_jacobi<double>(R1, L.l, L.LP, JX, JJ, Uw, Vw, Sd, sync, h->dflags + 1, s,
                                                 sizeof(T) == 4 ? 1e-8 : 1e-16));  // fp32 results: one sweep fewer
         }
-        const double sc = (d->a_scale != 0.0) ? d->a_scale : 1.0;
-        RSVD_CK(launch_convert_scale<T>(Sd, S, L.l, sc, s));
+        RSVD_CK(launch_convert_scale<T>(Sd, S, L.l, std::fabs(a_scale(d)), s));
         if (sizeof(T) == 4) {
             const int L2 = L.LP * L.LP;
             RSVD_CK(launch_convert_scale<float>(Uw, Uw32, L2, 1.0, s));
@@ -329,7 +340,7 @@ struct WideEngine {
                                      nullptr, nullptr, s));
         RSVD_CK(launch_panel_gemm<T>(Xn, L.n, L.LP, mat(Vw, Vw32), 0, reinterpret_cast<T*>(V), ldv, L.l, nullptr,
                                      nullptr, nullptr, s));
-        return RSVD_OK;
+        return finish(d, S, V, ldv);
     }
 };
 
@@ -338,7 +349,7 @@ int wide_typed(rsvd_handle_t h, const rsvd_desc_t* d, const void* A, const void*
                int64_t ldu, void* S, void* V, int64_t ldv, void* Qout, int64_t ldq) {
     WideLayout<T> L(d, (reinterpret_cast<uintptr_t>(A) & 15) == 0);
     RSVD_TRY(ensure_ws(h, L.total));
-    RSVD_CK(hipMemsetAsync(h->dflags, 0, kFlagWords * sizeof(int), h->stream));
+    RSVD_CK(reset_run_flags(h->dflags, h->stream));
     if (L.lowp) {  // the zero padding rows of the bf16 panels (never written by the kernels)
         const size_t bpr = (size_t)2 * L.LP;
         for (size_t off : {L.off_Xh, L.off_Xl})
@@ -351,10 +362,13 @@ int wide_typed(rsvd_handle_t h, const rsvd_desc_t* d, const void* A, const void*
     WideEngine<T> E(h, L, d->dtype);
     E.qr_mode = d->qr_mode;
     E.seed = d->seed;
-    // Repair stream layout of the m side: rank g's rows are stream rows [g m, g m + m) of a
-    // world * m panel (any disjoint layout keeps the repaired global columns Gaussian).
-    E.row_off = (int64_t)h->rank * d->m;
-    E.m_total = (int64_t)h->world * d->m;
+    if (h->world > 1) {
+        E.row_off = (int64_t)h->rank << 40;
+        E.m_total = (int64_t)h->world << 40;
+    } else {
+        E.m_total = d->m;
+    }
+    E.m_norm = (int64_t)h->world * d->m;
     RSVD_TRY(E.load_omega(omega, ldo, d->seed));
     if (Qout) {
         RSVD_TRY(E.range_finder(A, d->lda, d->q));

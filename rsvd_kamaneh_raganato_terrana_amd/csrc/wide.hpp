@@ -72,12 +72,13 @@ hipError_t launch_panel_gemm(const T* In, int64_t rows, int LP, const T* M, int 
 template <typename T>
 hipError_t launch_convert_scale(const double* x, T* y, int n, double sc, hipStream_t s);
 // Rank-deficiency repair of an orthonormalised panel: copies Q into Out, replacing every column
-// k with colflag[k] != 0 by Philox Gaussian values / sqrt(rows_total) (stream element
-// row_off + i + rows_total * k: row shards of one global panel draw one global column).
+// k with colflag[k] != 0 by Philox Gaussian values / sqrt(norm_rows) (stream element
+// row_off + i + rows_total * k: row shards of one global panel draw disjoint parts of one stream).
 // No-op unless *flag != 0.
 template <typename T>
 hipError_t launch_repair_panel(const T* Q, int64_t rows, int l, int LP, const int* colflag, const int* flag,
-                               uint64_t seed, int64_t row_off, int64_t rows_total, T* Out, hipStream_t s);
+                               uint64_t seed, int64_t row_off, int64_t rows_total, int64_t norm_rows, T* Out,
+                               hipStream_t s);
 // fp32 / fp64 panel -> bf16 hi (+ lo) panels (rows x LP).
 template <typename T>
 hipError_t launch_split_bf16(const T* P, int64_t rows, int LP, bf16_t* hi, bf16_t* lo, hipStream_t s);

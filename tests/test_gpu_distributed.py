@@ -27,6 +27,17 @@ def _free_port():
         return s.getsockname()[1]
 
 
+def _matrix(case):
+    """The global A of a case: the gapped family, or the reference's own rank-2 input
+    input/sparse_matrix.mtx (tests/golden/inputs.npz)."""
+    m, n, l = case[:3]
+    if len(case) > 5 and case[5] == "sparse_matrix":
+        return np.load(os.path.join(REPO, "tests", "golden", "inputs.npz"))["sparse_matrix"].astype(np.float64)
+    from conftest import gapped_matrix
+
+    return gapped_matrix(m, n, 2 * l, decay=0.93, seed=5).astype(np.float64)
+
+
 def _worker(rank, port, case, q):
     try:
         sys.path.insert(0, REPO)
@@ -41,8 +52,8 @@ def _worker(rank, port, case, q):
         os.environ["MASTER_PORT"] = str(port)
         dist.init_process_group("gloo", rank=rank, world_size=WORLD)
         torch.cuda.set_device(0)
-        m, n, l, qq, dt = case
-        A = gapped_matrix(m, n, 2 * l, decay=0.93, seed=5).astype(np.float64)
+        m, n, l, qq, dt = case[:5]
+        A = _matrix(case)
         rows, off = R.row_partition(m, WORLD, rank)
         tdt = {"f64": torch.float64, "f32": torch.float32, "bf16": torch.bfloat16}[dt]
         Ag = torch.from_numpy(np.ascontiguousarray(A[off:off + rows].T)).cuda().to(tdt).t()
@@ -60,14 +71,9 @@ def _worker(rank, port, case, q):
         q.put((rank, None, traceback.format_exc(), None, None, None))
 
 
-@pytest.mark.parametrize("case", [(600, 300, 32, 2, "f64"), (1024, 512, 64, 2, "f32"), (2048, 1024, 128, 1, "bf16")])
-def test_row_sharded_world2_matches_oracle(case):
+def _run_world2(case):
     import torch.multiprocessing as mp
 
-    import oracle
-    from conftest import rel_fro, sign_align
-
-    m, n, l, qq, dt = case
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -80,6 +86,35 @@ def test_row_sharded_world2_matches_oracle(case):
     for r in res:
         assert r[1] is not None, r[2]
     res.sort(key=lambda t: t[1])
+    return res
+
+
+@pytest.mark.parametrize("dt", ["f64", "f32"])
+def test_row_sharded_rank_deficient_is_orthonormal(dt):
+    """The reference's rank-2 input/sparse_matrix.mtx (A[i,j] = 100 i + j + 1) split over 2 ranks,
+    l = 16: the breakdown columns of every output panel are completed (repair pass with disjoint
+    Philox rows per rank), so U and V are orthonormal -- as the reference's Householder Q always is
+    (src/rSVD.cpp:60-61) -- and sigma_1, sigma_2 are the known answers."""
+    res = _run_world2((100, 100, 16, 2, dt, "sparse_matrix"))
+    U = np.vstack([r[2] for r in res])
+    S, V = res[0][3], res[0][4]
+    tol = 1e-10 if dt == "f64" else 1e-5
+    assert np.linalg.norm(U.T @ U - np.eye(16)) < tol
+    assert np.linalg.norm(V.T @ V - np.eye(16)) < tol
+    rtol = 1e-12 if dt == "f64" else 1e-6
+    assert abs(S[0] - 577391.767) < 1e-9 * 577391.767 + rtol * S[0]
+    assert abs(S[1] - 1443.12761) < 1e-7 * 1443.12761 + rtol * S[0]
+    assert np.all(S[2:] < (1e-9 if dt == "f64" else 1e-5) * S[0])
+
+
+@pytest.mark.parametrize("case", [(600, 300, 32, 2, "f64"), (1024, 512, 64, 2, "f32"), (2048, 1024, 128, 1, "bf16"),
+                                  (4096, 2048, 256, 2, "bf16")])
+def test_row_sharded_world2_matches_oracle(case):
+    import oracle
+    from conftest import rel_fro, sign_align
+
+    m, n, l, qq, dt = case
+    res = _run_world2(case)
     U = np.vstack([r[2] for r in res])
     A = np.vstack([r[5] for r in res])  # the values the GPU saw (bf16 / fp32 rounded)
     S0, V0 = res[0][3], res[0][4]
