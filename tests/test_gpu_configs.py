@@ -53,7 +53,7 @@ def test_c2_full_size_f32(engine):
     Uo, So, Vo = oracle.rsvd(A.astype(np.float64), l, q=2, Omega=Om)
     U, S, V = engine.rsvd(_dev_colmajor(A, torch.float32), l, q=2, omega=torch.from_numpy(Om.astype(np.float32)))
     U, S, V = (x.cpu().double().numpy() for x in (U, S, V))
-    _check(U, S, V, Uo, So, Vo, A.astype(np.float64), 1e-4, 1e-4)
+    _check(U, S, V, Uo, So, Vo, A.astype(np.float64), 1e-4, 1e-3)
 
 
 @pytest.mark.parametrize("m,n,l", [(4096, 2048, 256), (4096, 2048, 512)])
