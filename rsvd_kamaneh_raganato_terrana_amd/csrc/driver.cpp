@@ -279,6 +279,8 @@ struct Engine {
         RSVD_TRY(proj_tn(A, d->lda, Qm, Zn));
         RSVD_TRY(orth(Zn, L.n, Xn, 2));  // Xn = Q_B
         RSVD_TRY(cross_gram(Xn, Zn, L.n, R1));    // R = Q_B^T B^T exactly (fp64), W = R^T
+        // Inf / NaN in A reach R through B^T = A^T Q whatever the orthonormalisations did with them
+        RSVD_CK(launch_check_finite<double>(R1, L.LP * L.LP, h->dflags + kFlagNonFinite, s));
         if (d->method == RSVD_SVD_POWER) return power_stage(d, U, ldu, S, V, ldv);
         RSVD_CK(launch_small_svd<T>(R1, L.l, L.LP, Uw, Vw, S, h->dflags + 1, s));
         const double sc = std::fabs(a_scale_of(d));
@@ -358,7 +360,8 @@ int rsvd_create(int device, rsvd_handle_t* out) {
     rsvd_handle_t h = new rsvd_handle_s();
     h->device = device;
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipMalloc(&h->dflags, kFlagWords * sizeof(int)) != hipSuccess) {
+        hipMalloc(&h->dflags, kFlagWords * sizeof(int)) != hipSuccess ||
+        hipMemset(h->dflags, 0, kFlagWords * sizeof(int)) != hipSuccess) {
         delete h;
         return RSVD_ERR_HIP;
     }

@@ -26,7 +26,7 @@ hipError_t launch_panel_to_colmajor(const T* in, int64_t m, int cols, int LP, T*
 // X (col-major rows x cols, ld) *= f
 template <typename T>
 hipError_t launch_scale_cols(T* X, int64_t rows, int cols, int64_t ld, double f, hipStream_t s);
-// *flag |= 1 when any of x[0..n) is not finite (one workgroup)
+// *flag |= 1 when any of x[0..n) is not finite
 template <typename T>
 hipError_t launch_check_finite(const T* x, int n, int* flag, hipStream_t s);
 

@@ -5,6 +5,8 @@
 // regenerates the identical matrix from a counter-based Philox4x32-10 stream keyed by the
 // seed, so Omega needs no communication and the CPU oracle (oracle/rsvd_oracle.c,
 // orc_philox_gaussian) can draw the same numbers.  Element (i, j) is stream element i + n*j.
+#include <algorithm>
+
 #include "common.hpp"
 #include "kernels.hpp"
 
@@ -80,7 +82,8 @@ __global__ void scale_cols_kernel(T* __restrict__ X, int64_t rows, int cols, int
 template <typename T>
 __global__ void check_finite_kernel(const T* __restrict__ x, int n, int* __restrict__ flag) {
     bool bad = false;
-    for (int i = threadIdx.x; i < n; i += blockDim.x) bad = bad || !isfinite((double)x[i]);
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+        bad = bad || !isfinite((double)x[i]);
     if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
 }
 
@@ -131,7 +134,7 @@ hipError_t launch_scale_cols(T* X, int64_t rows, int cols, int64_t ld, double f,
 
 template <typename T>
 hipError_t launch_check_finite(const T* x, int n, int* flag, hipStream_t s) {
-    hipLaunchKernelGGL((check_finite_kernel<T>), dim3(1), dim3(256), 0, s, x, n, flag);
+    hipLaunchKernelGGL((check_finite_kernel<T>), dim3(std::min(64, (n + 255) / 256)), dim3(256), 0, s, x, n, flag);
     return hipGetLastError();
 }
 

@@ -321,6 +321,8 @@ struct WideEngine {
         RSVD_TRY(proj_tn(A, d->lda, Qm, Qh, Ql, Zn));               // B^T = A^T Q
         RSVD_TRY(orth(Zn, false, Xn, 2, nullptr, nullptr, true));  // Q_B
         RSVD_CK(launch_gram_wide<T>(Xn, Zn, L.n, L.LP, L.gx, gslab, R1, nullptr, s));  // R = Q_B^T B^T
+        // Inf / NaN in A reach R through B^T = A^T Q whatever the orthonormalisations did with them
+        RSVD_CK(launch_check_finite<double>(R1, L.LP * L.LP, h->dflags + kFlagNonFinite, s));
         if (d->method == RSVD_SVD_POWER) return power_stage(d, U, ldu, S, V, ldv);
         // the small SVD always runs in fp64 (U_w, V_w feed the fp32 panel products of U and V)
         double* Sd = G;  // free scratch by now

@@ -35,7 +35,8 @@ def _matrix(case):
         return np.load(os.path.join(REPO, "tests", "golden", "inputs.npz"))["sparse_matrix"].astype(np.float64)
     from conftest import gapped_matrix
 
-    return gapped_matrix(m, n, 2 * l, decay=0.93, seed=5).astype(np.float64)
+    # the leading half of the spectrum stays above the noise floor (1e-3 N): l = 256 decays slower
+    return gapped_matrix(m, n, 2 * l, decay=0.93 if l < 256 else 0.985, seed=5).astype(np.float64)
 
 
 def _worker(rank, port, case, q):

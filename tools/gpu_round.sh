@@ -7,7 +7,7 @@ tag=${1:-x}; mode=${2:-tests}
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 if [ "$mode" = tests ]; then
-  tools/gpu_tests.sh || exit 1
+  tools/gpu_tests.sh ${TESTS:-tests} || exit 1
 fi
 timeout -k 10 300 python3 bench.py > gpurun_out/bench_${tag}.json 2> gpurun_out/bench_${tag}.err || { tail -20 gpurun_out/bench_${tag}.err; exit 1; }
 cat gpurun_out/bench_${tag}.json
