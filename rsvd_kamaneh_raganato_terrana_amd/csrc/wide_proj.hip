@@ -312,8 +312,9 @@ __device__ __forceinline__ int swz(int row) { return 2 * ((row & 3) | (((row >> 
 
 typedef __attribute__((address_space(3))) void* lds_void_ptr;
 
+template <int AUX = 0>
 __device__ __forceinline__ void glds16(const void* g, char* lds_wave_base) {
-    __builtin_amdgcn_global_load_lds(g, (lds_void_ptr)lds_wave_base, 16, 0, 0);
+    __builtin_amdgcn_global_load_lds(g, (lds_void_ptr)lds_wave_base, 16, 0, AUX);
 }
 
 // LDS reads of the v2 kernel are inline asm: hipcc's waitcnt pass treats a compiler-visible LDS
@@ -369,7 +370,9 @@ __device__ __forceinline__ bf16x8_t fp8x8_to_bf16x8(i32x2 v) {
     return __builtin_bit_cast(bf16x8_t, make_uint4(a.x, a.y, b.x, b.y));
 }
 
-template <bool FP8, bool NN, int LP, bool SPLIT, bool DS = false>
+// KN (tuning knobs): bit 0 -- A (read once per launch) with the non-temporal policy (aux = 2) so
+// the panel S, re-read by every workgroup, keeps the L2; bit 1 -- s_setprio 1 for waves 4-7.
+template <bool FP8, bool NN, int LP, bool SPLIT, bool DS = false, int KN = 0>
 __global__ __launch_bounds__(512) void wproj2_kernel(const void* __restrict__ Av, int64_t lda, int64_t rows_out,
                                                      int64_t K, int64_t arows, const bf16_t* __restrict__ Shi,
                                                      const bf16_t* __restrict__ Slo, float* __restrict__ out,
@@ -430,7 +433,7 @@ __global__ __launch_bounds__(512) void wproj2_kernel(const void* __restrict__ Av
                         i = (i + 16 <= arows) ? i : arows - 16;
                         src = A8 + jc * lda + i;
                     }
-                    glds16(src, at + gi * 1024);
+                    glds16<(KN & 1) ? 2 : 0>(src, at + gi * 1024);
                 }
             }
             return;
@@ -462,7 +465,7 @@ __global__ __launch_bounds__(512) void wproj2_kernel(const void* __restrict__ Av
                 i = (i + 8 <= arows) ? i : arows - 8;
                 src = A + jc * lda + i;
             }
-            glds16(src, at + gi * 1024);
+            glds16<(KN & 1) ? 2 : 0>(src, at + gi * 1024);
         }
     };
 
@@ -472,6 +475,7 @@ __global__ __launch_bounds__(512) void wproj2_kernel(const void* __restrict__ Av
 #pragma unroll
         for (int g = 0; g < G; ++g) acc[t][g] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+    if ((KN & 2) && w >= 4) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int st = 0; st < NST - 1; ++st)
         if (st < nsteps) issue(st);
@@ -583,8 +587,13 @@ hipError_t wproj2_go(const void* A, int64_t lda, int64_t m, int64_t n, const bf1
     const int64_t rows_out = NN ? m : n, K = NN ? n : m;
     float* o = p.splits == 1 ? Out : slabs;
     const int64_t stride = rows_out * LP;
-    hipLaunchKernelGGL((wproj2_kernel<FP8, NN, LP, SPLIT, DS>), dim3(p.blocks * p.splits), dim3(512), SH::LDS, s, A, lda,
-                       rows_out, K, m, Shi, Slo, o, stride, p.chunk, p.blocks);
+    // NN streams A in whole columns: non-temporal A (and the static priority) measured -9..-11 % on
+    // the C3 / C4 / C5 NN launches; TN's short column runs need the L2 to keep the second half of
+    // each line for the next k-step (non-temporal: +4..13 %), so TN keeps the default policy
+    // (profiles/r02_wide_lab_knobs.txt).
+    constexpr int KN = NN ? 3 : 0;
+    hipLaunchKernelGGL((wproj2_kernel<FP8, NN, LP, SPLIT, DS, KN>), dim3(p.blocks * p.splits), dim3(512), SH::LDS, s, A,
+                       lda, rows_out, K, m, Shi, Slo, o, stride, p.chunk, p.blocks);
     hipError_t e = hipGetLastError();
     if (e == hipSuccess && done) e = hipEventRecord(done, s);
     if (e != hipSuccess || p.splits == 1) return e;

@@ -2,8 +2,10 @@
 
 FETCH_SIZE / WRITE_SIZE are in KiB per dispatch.  gfx950 correction (MI355X_MICROARCH.md, HBM):
 FETCH_SIZE reports exactly half of the bytes of a wide (16 B/lane) coalesced streaming read, so
-it is doubled; WRITE_SIZE is exact for 16-B-per-lane stores.  The projection kernels read A with
-16-B vector loads, so the doubled figure applies to them.
+it is doubled; WRITE_SIZE is exact for 16-B-per-lane stores.  profiles/r02_fetch_calibration.json
+(tools/fetch_calib.hip) measured the factor for the projection kernels' own access shapes -- 32-,
+64- and 128-B column runs and contiguous streaming read by global_load_lds_dwordx4 all report
+0.50-0.52 of the bytes -- so the doubled figure applies to every projection kernel.
 
 usage: python tools/traffic.py gpurun_out/prof_<tag> <workload-key> > profiles/traffic_<key>.json
 """
@@ -30,17 +32,13 @@ def main():
     fetch, nf = per_kernel(os.path.join(root, "fetch", "run_counter_collection.csv"))
     write, _ = per_kernel(os.path.join(root, "write", "run_counter_collection.csv"))
     out = {"workload": key, "source": root,
-           "correction": "FETCH_SIZE x2 (gfx950: 128-B requests tallied at 64 B), except the single-step TN wproj2 "
-                         "kernels (x1: their A reads are 64-B (bf16) / 32-B (e4m3) runs per column and k-step, one "
-                         "request each -- uncalibrated width, taken as tallied); WRITE_SIZE x1",
+           "correction": "FETCH_SIZE x2 for every kernel (calibrated for 32/64/128-B column runs and streaming: "
+                         "profiles/r02_fetch_calibration.json); WRITE_SIZE x1",
            "kernels": {}}
     for k in fetch:
         if not (k.startswith("rsvd::") or "proj" in k or "gram" in k or "svd" in k or "panel" in k):
             continue
-        args = [a.strip(" >") for a in k[len("wproj2_kernel<"):].split(",")] if k.startswith("wproj2_kernel<") else []
-        # TN (NN = false) single-step stages read 64-B / 32-B runs; two-step stages (DS = true) 128-B runs
-        tn_short_runs = len(args) >= 4 and args[1] == "false" and not (len(args) >= 5 and args[4] == "true")
-        f = (1 if tn_short_runs else 2) * fetch[k] * 1024
+        f = 2 * fetch[k] * 1024
         w = write.get(k, 0.0) * 1024
         out["kernels"][k] = {"dispatches": nf[k], "fetch_bytes": f, "write_bytes": w, "hbm_bytes": f + w}
     json.dump(out, sys.stdout, indent=1)
