@@ -34,9 +34,11 @@ import time
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-# MI355X dense peaks (MI355X_MICROARCH.md): matrix fp32 157.3, fp64 78.6, bf16 2516.6 TF/s (e4m3 A
-# is widened to bf16 in LDS, so its projections run at the bf16 rate); HBM 8 TB/s.
+# MI355X dense peaks (MI355X_MICROARCH.md): matrix fp32 157.3, fp64 78.6, bf16 2516.6 TF/s, fp8 5033.2
+# (block-scaled f8f6f4 form; the non-scaled fp8 MFMA runs at the bf16 rate).  e4m3 A: the sketch
+# A * Omega runs e4m3 x e4m3 on the fp8 MFMA; the hi/lo products widen A to bf16 (bf16 rate).
 PEAK_TFLOPS = {"f32": 157.3, "f64": 78.6, "bf16": 2516.6, "fp8": 2516.6}
+PEAK_FP8_TFLOPS = 5033.2
 ELEM_BYTES = {"f32": 4, "f64": 8, "bf16": 2, "fp8": 1}
 PEAK_HBM_GBS = 8000.0
 
@@ -270,6 +272,21 @@ def main():
         "launches_timed": kn,
         "proj_share_of_step": (tm["nn_ms"] + tm["tn_ms"]) / (elapsed * 1e3) if elapsed > 0 else None,
     }
+
+    # the sketch Y = A Omega alone (single pass: Omega is exact in the storage type)
+    sk_n = tm.get("sketch_launches", 0)
+    if sk_n:
+        sk_s = tm["sketch_ms"] / sk_n * 1e-3
+        sk_tf = flop_launch / sk_s / 1e12
+        sk_gbs = a_bytes / sk_s / 1e9
+        sk_peak = PEAK_FP8_TFLOPS if dt == "fp8" else PEAK_TFLOPS[dt]
+        if ai * PEAK_HBM_GBS / 1e3 < sk_peak:
+            sk = {"bound": "hbm", "achieved": sk_gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": sk_gbs / PEAK_HBM_GBS}
+        else:
+            sk = {"bound": "mfma", "achieved": sk_tf, "peak": sk_peak, "unit": "TFLOP/s", "frac": sk_tf / sk_peak}
+        sk.update({"kernel": "sketch Y = A Omega" + (" (e4m3 x e4m3, v_mfma_f32_16x16x32_fp8_fp8)" if dt == "fp8" else ""),
+                   "avg_launch_us": sk_s * 1e6, "achieved_TFLOPs": sk_tf, "achieved_GBps": sk_gbs, "launches_timed": sk_n})
+        roof["sketch"] = sk
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_budget > 0:

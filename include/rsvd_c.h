@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define RSVD_ABI_VERSION 3
+#define RSVD_ABI_VERSION 4
 
 typedef enum {
     RSVD_OK = 0,
@@ -125,6 +125,9 @@ int rsvd_workspace_bytes(const rsvd_desc_t *desc, size_t *bytes);
 typedef struct {
     int32_t nn_launches, tn_launches;
     double nn_ms, tn_ms;
+    int32_t sketch_launches, reserved; /* the sketch Y = A Omega alone (also counted in nn_*): e4m3 A runs
+                                          it on the fp8 MFMA, every other product on the bf16 / fp32 one */
+    double sketch_ms;
 } rsvd_timing_t;
 int rsvd_set_timing(rsvd_handle_t h, int enable);
 int rsvd_get_timing(rsvd_handle_t h, rsvd_timing_t *t);

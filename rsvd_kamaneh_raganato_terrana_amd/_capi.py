@@ -61,6 +61,7 @@ class Timing(ctypes.Structure):
     _fields_ = [
         ("nn_launches", ctypes.c_int32), ("tn_launches", ctypes.c_int32),
         ("nn_ms", ctypes.c_double), ("tn_ms", ctypes.c_double),
+        ("sketch_launches", ctypes.c_int32), ("reserved", ctypes.c_int32), ("sketch_ms", ctypes.c_double),
     ]
 
 

@@ -212,9 +212,9 @@ struct Engine {
         return RSVD_OK;
     }
 
-    int proj_nn(const T* A, int64_t lda, const T* X, T* Y) {
+    int proj_nn(const T* A, int64_t lda, const T* X, T* Y, int kind = 0) {
         int ev;
-        RSVD_TRY(ev_begin(0, ev));
+        RSVD_TRY(ev_begin(kind, ev));
         RSVD_CK(launch_proj_nn<T>(A, lda, L.m, L.n, X, L.LP, L.pnn, slab, Y, s, ev >= 0 ? h->ev_pool[ev + 1] : nullptr));
         return RSVD_OK;
     }
@@ -236,7 +236,7 @@ struct Engine {
 
     // intermediate_step (src/rSVD.cpp:57-70): leaves Q (m x LP panel) in Qm.
     int range_finder(const T* A, int64_t lda, int q) {
-        RSVD_TRY(proj_nn(A, lda, Xn, Ym));
+        RSVD_TRY(proj_nn(A, lda, Xn, Ym, 2));  // the sketch
         RSVD_TRY(orth(Ym, L.m, Qm, q == 0 ? 2 : inter_passes));
         for (int i = 0; i < q; ++i) {
             RSVD_TRY(proj_tn(A, lda, Qm, Zn));
@@ -450,8 +450,10 @@ int rsvd_set_timing(rsvd_handle_t h, int enable) {
     h->timing = enable != 0;
     h->ev_used.clear();
     h->ev_next = 0;
-    h->acc_ms[0] = h->acc_ms[1] = 0.0;
-    h->acc_n[0] = h->acc_n[1] = 0;
+    for (int k = 0; k < 3; ++k) {
+        h->acc_ms[k] = 0.0;
+        h->acc_n[k] = 0;
+    }
     return RSVD_OK;
 }
 
@@ -464,6 +466,10 @@ int rsvd_get_timing(rsvd_handle_t h, rsvd_timing_t* t) {
         RSVD_CK(hipEventElapsedTime(&ms, h->ev_pool[u.second], h->ev_pool[u.second + 1]));
         h->acc_ms[u.first] += ms;
         h->acc_n[u.first] += 1;
+        if (u.first == 2) {  // the sketch is also an A*X launch
+            h->acc_ms[0] += ms;
+            h->acc_n[0] += 1;
+        }
     }
     h->ev_used.clear();
     h->ev_next = 0;
@@ -471,6 +477,9 @@ int rsvd_get_timing(rsvd_handle_t h, rsvd_timing_t* t) {
     t->tn_launches = h->acc_n[1];
     t->nn_ms = h->acc_ms[0];
     t->tn_ms = h->acc_ms[1];
+    t->sketch_launches = h->acc_n[2];
+    t->reserved = 0;
+    t->sketch_ms = h->acc_ms[2];
     return RSVD_OK;
 }
 

@@ -28,13 +28,14 @@ struct rsvd_handle_s {
     int rank = 0, world = 1;
     rsvd_allreduce_fn allreduce = nullptr;
     void* ar_user = nullptr;
-    // timing mode: hipEvent pairs around every projection kernel (kind 0 = A*X, 1 = A^T*Q)
+    // timing mode: hipEvent pairs around every projection kernel (kind 0 = A*X, 1 = A^T*Q, 2 = the
+    // sketch A*Omega, which also counts as kind 0)
     bool timing = false;
     std::vector<hipEvent_t> ev_pool;
     std::vector<std::pair<int, int>> ev_used;  // (kind, first event index)
     size_t ev_next = 0;
-    double acc_ms[2] = {0.0, 0.0};
-    int acc_n[2] = {0, 0};
+    double acc_ms[3] = {0.0, 0.0, 0.0};
+    int acc_n[3] = {0, 0, 0};
 };
 
 #define RSVD_CK(expr)                                                                         \

@@ -49,10 +49,11 @@ struct WideLayout {
     WProjPlan wnn, wtn;
     ProjPlan pnn, ptn;
     GramPlan gm, gn, gx;
-    size_t off_Xn, off_Zn, off_Ym, off_Qm, off_T1, off_Xh, off_Xl, off_Qh, off_Ql, off_pslab, off_gslab;
+    size_t off_Xn, off_Zn, off_Ym, off_Qm, off_T1, off_Xh, off_Xl, off_Qh, off_Ql, off_X8, off_pslab, off_gslab;
     size_t off_G, off_R, off_Rinv, off_W, off_R1, off_Uw, off_Vw, off_JX, off_JJ, off_M32, off_colflag, off_sync, total;
 
     int64_t mpad, npad;  // bf16 panel rows, zero-padded to a multiple of 32 (wproj2 reads whole k-steps)
+    bool s8 = false;     // the sketch runs e4m3 x e4m3 on the fp8 MFMA
 
     // a_aligned: A's base is 16-B aligned (the LDS-DMA projection kernel needs 16-B source chunks)
     WideLayout(const rsvd_desc_t* d, bool a_aligned = true)
@@ -97,6 +98,9 @@ struct WideLayout {
         off_Xl = take(bn);
         off_Qh = take(bm);
         off_Ql = take(bm);
+        // e4m3 A: the sketch Omega as an e4m3 panel (the fp8-MFMA sketch product, launch_wproj_s8)
+        s8 = d->dtype == RSVD_FP8_E4M3 && wproj_s8_supported(wnn, LP);
+        off_X8 = take(s8 ? (size_t)npad * LP : 0);
         off_pslab = take(sizeof(T) * std::max<int64_t>(pslab, 1) * LP);
         off_gslab = take(sizeof(double) * gslab);
         off_G = take(sizeof(double) * L2);
@@ -123,6 +127,7 @@ struct WideEngine {
     int dtype;
     T *Xn, *Zn, *Ym, *Qm, *T1, *pslab;
     bf16_t *Xh, *Xl, *Qh, *Ql;
+    fp8_t* X8;
     double *gslab, *G, *R, *Rinv, *W, *R1, *Uw, *Vw, *JX, *JJ;
     float *Rinv32, *Uw32, *Vw32;
     int* colflag;
@@ -148,6 +153,7 @@ struct WideEngine {
         Xl = L.lowp ? reinterpret_cast<bf16_t*>(b + L.off_Xl) : nullptr;
         Qh = L.lowp ? reinterpret_cast<bf16_t*>(b + L.off_Qh) : nullptr;
         Ql = L.lowp ? reinterpret_cast<bf16_t*>(b + L.off_Ql) : nullptr;
+        X8 = L.s8 ? reinterpret_cast<fp8_t*>(b + L.off_X8) : nullptr;
         gslab = reinterpret_cast<double*>(b + L.off_gslab);
         G = reinterpret_cast<double*>(b + L.off_G);
         R = reinterpret_cast<double*>(b + L.off_R);
@@ -190,9 +196,9 @@ struct WideEngine {
     }
 
     // Y = A X (X: bf16 panels for low precision, T panel otherwise)
-    int proj_nn(const void* A, int64_t lda, const T* X, const bf16_t* xh, const bf16_t* xl, T* Y) {
+    int proj_nn(const void* A, int64_t lda, const T* X, const bf16_t* xh, const bf16_t* xl, T* Y, int kind = 0) {
         int ev;
-        RSVD_TRY(ev_begin(0, ev));
+        RSVD_TRY(ev_begin(kind, ev));
         hipEvent_t done = ev >= 0 ? h->ev_pool[ev + 1] : nullptr;
         if (L.lowp) {
             RSVD_CK(launch_wproj(1, dtype == RSVD_FP8_E4M3, A, lda, L.m, L.n, xh, xl, L.LP, L.wnn,
@@ -200,6 +206,15 @@ struct WideEngine {
         } else {
             RSVD_CK(launch_proj_nn<T>(reinterpret_cast<const T*>(A), lda, L.m, L.n, X, L.LP, L.pnn, pslab, Y, s, done));
         }
+        return RSVD_OK;
+    }
+    // Y = A Omega with e4m3 A and the e4m3 sketch in X8: both operands exact e4m3 on the fp8 MFMA
+    int proj_nn_s8(const void* A, int64_t lda, T* Y) {
+        int ev;
+        RSVD_TRY(ev_begin(2, ev));
+        hipEvent_t done = ev >= 0 ? h->ev_pool[ev + 1] : nullptr;
+        RSVD_CK(launch_wproj_s8(A, lda, L.m, L.n, X8, L.LP, L.wnn, reinterpret_cast<float*>(pslab),
+                                reinterpret_cast<float*>(Y), s, done));
         return RSVD_OK;
     }
     // Z = A^T Q, summed over the row shards
@@ -275,7 +290,12 @@ struct WideEngine {
     }
 
     int range_finder(const void* A, int64_t lda, int q) {
-        RSVD_TRY(proj_nn(A, lda, Xn, Xh, nullptr, Ym));  // the sketch: Omega is exactly bf16 (lowp)
+        if (L.s8) {  // the sketch: Omega is exactly e4m3 -- fp8 MFMA
+            RSVD_CK(launch_bf16_to_fp8(Xh, L.npad * L.LP, X8, s));
+            RSVD_TRY(proj_nn_s8(A, lda, Ym));
+        } else {
+            RSVD_TRY(proj_nn(A, lda, Xn, Xh, nullptr, Ym, 2));  // the sketch: Omega is exactly bf16 (lowp)
+        }
         RSVD_TRY(orth(Ym, true, Qm, q == 0 ? 2 : inter_passes, Qh, Ql, q == 0));
         for (int i = 0; i < q; ++i) {
             const bool last = i == q - 1;

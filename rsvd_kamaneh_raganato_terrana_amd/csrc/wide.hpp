@@ -43,6 +43,15 @@ hipError_t launch_wproj(int nn, int a_fp8, const void* A, int64_t lda, int64_t m
                         const bf16_t* Slo, int LP, const WProjPlan& p, float* slabs, float* Out, hipStream_t s,
                         hipEvent_t done = nullptr);
 
+// e4m3 A times an e4m3 panel S8 (n x LP bytes, rows zero-padded to a multiple of 32): the Gaussian
+// sketch Y = A Omega of an e4m3 A on v_mfma_f32_16x16x32_fp8_fp8 (both operands exact e4m3).
+// Needs an NN plan with v2 and LP in {256, 512} (wproj_s8_supported).
+bool wproj_s8_supported(const WProjPlan& p, int LP);
+hipError_t launch_wproj_s8(const void* A, int64_t lda, int64_t m, int64_t n, const fp8_t* S8, int LP, const WProjPlan& p,
+                           float* slabs, float* Out, hipStream_t s, hipEvent_t done = nullptr);
+// bf16 panel holding exactly-e4m3 values -> e4m3 codes (count elements)
+hipError_t launch_bf16_to_fp8(const bf16_t* in, int64_t count, fp8_t* out, hipStream_t s);
+
 // ---- wide_qr.hip -------------------------------------------------------------------------------
 struct GramPlan {
     int blocks;   // 32 x 32 blocks of the Gram (upper triangle, or all for a cross Gram)

@@ -283,13 +283,13 @@ template <> struct W2Cfg<128, true> { static constexpr int WR = 4, WC = 2, G = 4
 template <> struct W2Cfg<256, false> { static constexpr int WR = 4, WC = 2, G = 8; };
 template <> struct W2Cfg<512, false> { static constexpr int WR = 2, WC = 4, G = 8; };
 
-template <int LP, bool SPLIT, bool FP8, bool DS = false>
+template <int LP, bool SPLIT, bool FP8, bool DS = false, bool S8 = false>
 struct W2Shape {
     static constexpr int WR = W2Cfg<LP, DS>::WR, WC = W2Cfg<LP, DS>::WC, G = W2Cfg<LP, DS>::G;
     static constexpr int WI = WR * 64;            // output rows per workgroup
     static constexpr int NS = SPLIT ? 2 : 1;
     static constexpr int KSS = DS ? 2 * KS : KS;  // k rows per stage
-    static constexpr int SBYTES = KSS * LP * 2;   // one S panel tile
+    static constexpr int SBYTES = KSS * LP * (S8 ? 1 : 2);  // one S panel tile (e4m3 S: one byte per element)
     static constexpr int ABYTES = KSS * WI * (FP8 ? 1 : 2);  // the A tile
     static constexpr int STAGE = NS * SBYTES + ABYTES;
     static constexpr int NST0 = 147456 / STAGE;
@@ -372,13 +372,18 @@ __device__ __forceinline__ bf16x8_t fp8x8_to_bf16x8(i32x2 v) {
 
 // KN (tuning knobs): bit 0 -- A (read once per launch) with the non-temporal policy (aux = 2) so
 // the panel S, re-read by every workgroup, keeps the L2; bit 1 -- s_setprio 1 for waves 4-7.
-template <bool FP8, bool NN, int LP, bool SPLIT, bool DS = false, int KN = 0>
+// S8 (e4m3 A, NN, single pass, LP >= 256): S is an e4m3 panel -- the exactly-e4m3 Gaussian sketch
+// Omega -- so both operands stay e4m3 and the product runs on v_mfma_f32_16x16x32_fp8_fp8: no
+// widening of A, half the S bytes through L2 and LDS.  The S image is [32 k][LP] bytes swizzled
+// like the e4m3 A image and read with ds_read_b64_tr_b8.
+template <bool FP8, bool NN, int LP, bool SPLIT, bool DS = false, int KN = 0, bool S8 = false>
 __global__ __launch_bounds__(512) void wproj2_kernel(const void* __restrict__ Av, int64_t lda, int64_t rows_out,
                                                      int64_t K, int64_t arows, const bf16_t* __restrict__ Shi,
                                                      const bf16_t* __restrict__ Slo, float* __restrict__ out,
                                                      int64_t slab_stride, int64_t kchunk, int nrowblk) {
-    typedef W2Shape<LP, SPLIT, FP8, DS> SH;
+    typedef W2Shape<LP, SPLIT, FP8, DS, S8> SH;
     static_assert(!DS || (!NN && !FP8), "double-step stages: bf16 TN only");
+    static_assert(!S8 || (FP8 && NN && !SPLIT && LP >= 256), "e4m3 S: single-pass e4m3 NN at LP >= 256");
     constexpr int KSS = SH::KSS;
     const bf16_t* __restrict__ A = reinterpret_cast<const bf16_t*>(Av);
     const uint8_t* __restrict__ A8 = reinterpret_cast<const uint8_t*>(Av);
@@ -398,6 +403,17 @@ __global__ __launch_bounds__(512) void wproj2_kernel(const void* __restrict__ Av
     auto issue = [&](int st) {
         char* slot = smem_raw + (size_t)(st % NST) * SH::STAGE;
         const int64_t k0 = kbeg + (int64_t)st * KSS;
+        if constexpr (S8) {  // [32 k][LP] bytes: 16-B chunk cp of row k at cp ^ swz8<LP>(k)
+            const uint8_t* S = reinterpret_cast<const uint8_t*>(Shi);
+#pragma unroll
+            for (int t = 0; t < SH::SGL; ++t) {
+                const int gi = t * 8 + w;
+                const int u = gi * 64 + lane;
+                constexpr int CPR = LP / 16;
+                const int k = u / CPR, cp = u % CPR;
+                glds16(S + (k0 + k) * LP + 16 * (cp ^ swz8<LP>(k)), slot + gi * 1024);
+            }
+        } else {
 #pragma unroll
         for (int a = 0; a < NS; ++a) {
             const bf16_t* S = a ? Slo : Shi;
@@ -408,6 +424,7 @@ __global__ __launch_bounds__(512) void wproj2_kernel(const void* __restrict__ Av
                 const int row = u / (LP / 8), cc = u % (LP / 8);
                 glds16(S + (k0 + row) * LP + 8 * (cc ^ swz(row)), slot + a * SH::SBYTES + gi * 1024);
             }
+        }
         }
         char* at = slot + NS * SH::SBYTES;
         if constexpr (FP8) {
@@ -518,6 +535,26 @@ __global__ __launch_bounds__(512) void wproj2_kernel(const void* __restrict__ Av
                     a4[t] = read128_a(At + j * (KSS * 2) + 16 * (4 * ss + (h ^ ((j >> 1) & 3))));
                 }
             }
+            if constexpr (S8) {  // both operands e4m3: fragments are the raw 8 bytes of k 8h .. 8h + 7
+                i32x2 bv[G];
+                const int k = 8 * h + (r >> 1);
+#pragma unroll
+                for (int g = 0; g < G; ++g)  // every B fragment in flight, then one wait
+                    bv[g] = tr8_read_a(slot + k * LP + 16 * ((wc * G + g) ^ swz8<LP>(k)) + 8 * (r & 1));
+#pragma unroll
+                for (int t = 0; t < RT; ++t) wait_lgkm0(a1[t]);
+#pragma unroll
+                for (int g = 0; g < G; ++g) wait_lgkm0(bv[g]);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int g = 0; g < G; ++g)
+#pragma unroll
+                    for (int t = 0; t < RT; ++t)
+                        acc[t][g] = __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(__builtin_bit_cast(long, a1[t]),
+                                                                              __builtin_bit_cast(long, bv[g]), acc[t][g],
+                                                                              0, 0, 0);
+                continue;
+            }
             // B fragments of column tile g: hi (and lo) halves of the transposed S rows 8h+q, 8h+q+4
             auto bread = [&](int g, i32x2* b) {
                 const int col = wc * G * 16 + 16 * g + 4 * p;
@@ -580,10 +617,10 @@ __global__ __launch_bounds__(512) void wproj2_kernel(const void* __restrict__ Av
         }
 }
 
-template <bool FP8, bool NN, int LP, bool SPLIT, bool DS = false>
+template <bool FP8, bool NN, int LP, bool SPLIT, bool DS = false, bool S8 = false>
 hipError_t wproj2_go(const void* A, int64_t lda, int64_t m, int64_t n, const bf16_t* Shi, const bf16_t* Slo,
                      const WProjPlan& p, float* slabs, float* Out, hipStream_t s, hipEvent_t done) {
-    typedef W2Shape<LP, SPLIT, FP8, DS> SH;
+    typedef W2Shape<LP, SPLIT, FP8, DS, S8> SH;
     const int64_t rows_out = NN ? m : n, K = NN ? n : m;
     float* o = p.splits == 1 ? Out : slabs;
     const int64_t stride = rows_out * LP;
@@ -592,8 +629,8 @@ hipError_t wproj2_go(const void* A, int64_t lda, int64_t m, int64_t n, const bf1
     // each line for the next k-step (non-temporal: +4..13 %), so TN keeps the default policy
     // (profiles/r02_wide_lab_knobs.txt).
     constexpr int KN = NN ? 3 : 0;
-    hipLaunchKernelGGL((wproj2_kernel<FP8, NN, LP, SPLIT, DS, KN>), dim3(p.blocks * p.splits), dim3(512), SH::LDS, s, A,
-                       lda, rows_out, K, m, Shi, Slo, o, stride, p.chunk, p.blocks);
+    hipLaunchKernelGGL((wproj2_kernel<FP8, NN, LP, SPLIT, DS, KN, S8>), dim3(p.blocks * p.splits), dim3(512), SH::LDS, s,
+                       A, lda, rows_out, K, m, Shi, Slo, o, stride, p.chunk, p.blocks);
     hipError_t e = hipGetLastError();
     if (e == hipSuccess && done) e = hipEventRecord(done, s);
     if (e != hipSuccess || p.splits == 1) return e;
@@ -678,6 +715,16 @@ WProjPlan plan_wproj(int64_t rows_out, int64_t K, int LP, bool v2, bool nn, bool
     p.chunk = chunk;
     p.splits = (int)((K + chunk - 1) / chunk);
     return p;
+}
+
+bool wproj_s8_supported(const WProjPlan& p, int LP) { return p.v2 && (LP == 256 || LP == 512); }
+
+hipError_t launch_wproj_s8(const void* A, int64_t lda, int64_t m, int64_t n, const fp8_t* S8, int LP, const WProjPlan& p,
+                           float* slabs, float* Out, hipStream_t s, hipEvent_t done) {
+    if (!wproj_s8_supported(p, LP)) return hipErrorInvalidValue;
+    const bf16_t* S = reinterpret_cast<const bf16_t*>(S8);
+    if (LP == 256) return wproj2_go<true, true, 256, false, false, true>(A, lda, m, n, S, nullptr, p, slabs, Out, s, done);
+    return wproj2_go<true, true, 512, false, false, true>(A, lda, m, n, S, nullptr, p, slabs, Out, s, done);
 }
 
 hipError_t launch_wproj(int nn, int a_fp8, const void* A, int64_t lda, int64_t m, int64_t n, const bf16_t* Shi,

@@ -915,6 +915,18 @@ __global__ void omega_lowp_from_kernel(const float* __restrict__ om, int64_t ld,
     }
 }
 
+// bf16 values that are exactly e4m3 -> e4m3 codes, 4 per thread (exact: no rounding happens)
+__global__ void bf16_to_fp8_kernel(const bf16_t* __restrict__ in, int64_t count4, uint32_t* __restrict__ out) {
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < count4; e += (int64_t)gridDim.x * blockDim.x) {
+        const uint2 v = reinterpret_cast<const uint2*>(in)[e];
+        const float f0 = __uint_as_float(v.x << 16), f1 = __uint_as_float(v.x & 0xFFFF0000u);
+        const float f2 = __uint_as_float(v.y << 16), f3 = __uint_as_float(v.y & 0xFFFF0000u);
+        int w = __builtin_amdgcn_cvt_pk_fp8_f32(f0, f1, 0, false);
+        w = __builtin_amdgcn_cvt_pk_fp8_f32(f2, f3, w, true);
+        out[e] = (uint32_t)w;
+    }
+}
+
 template <typename T>
 __global__ void convert_scale_kernel(const double* __restrict__ x, T* __restrict__ y, int n, double sc) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1042,6 +1054,13 @@ hipError_t launch_omega_lowp(bf16_t* panel, int64_t n, int l, int LP, uint64_t s
                              hipStream_t s) {
     hipLaunchKernelGGL(omega_lowp_kernel, dim3(grid_1d(n * LP)), dim3(256), 0, s, panel, n, l, LP, seed, round_fp8,
                        f);
+    return hipGetLastError();
+}
+
+hipError_t launch_bf16_to_fp8(const bf16_t* in, int64_t count, fp8_t* out, hipStream_t s) {
+    if (count % 4) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(bf16_to_fp8_kernel, dim3(grid_1d(count / 4)), dim3(256), 0, s, in, count / 4,
+                       reinterpret_cast<uint32_t*>(out));
     return hipGetLastError();
 }
 

@@ -371,6 +371,102 @@ static void check_proj() {  // v2 (LDS-DMA) against v1 on random bf16 / e4m3 dat
     }
 }
 
+// e4m3 x e4m3 sketch (launch_wproj_s8, fp8 MFMA) against the bf16 path on the same exact values
+static void check_s8() {
+    for (int LP : {256, 512}) {
+        const int64_t m = 4096 + 16 * 3, n = 2048 + 32;
+        const int64_t npad = (n + 31) / 32 * 32;
+        std::vector<uint8_t> hA((size_t)m * n), hS8((size_t)npad * LP, 0);
+        std::vector<uint16_t> hSb((size_t)npad * LP, 0);
+        std::mt19937 g(11);
+        auto code = [&]() {
+            uint8_t c = (uint8_t)(g() & 0xff);
+            if ((c & 0x7f) == 0x7f) c ^= 1;
+            return c;
+        };
+        auto e4m3_to_f = [](uint8_t c) {
+            const int sgn = c >> 7, e = (c >> 3) & 15, mm = c & 7;
+            const float v = e ? std::ldexp(1.0f + mm / 8.0f, e - 7) : std::ldexp(mm / 8.0f, -6);
+            return sgn ? -v : v;
+        };
+        for (auto& x : hA) x = code();
+        for (int64_t i = 0; i < n; ++i)
+            for (int c = 0; c < LP; ++c) {
+                const uint8_t cd = code();
+                hS8[(size_t)i * LP + c] = cd;
+                const float f = e4m3_to_f(cd);
+                uint32_t u;
+                std::memcpy(&u, &f, 4);
+                hSb[(size_t)i * LP + c] = (uint16_t)(u >> 16);  // exact: e4m3 has 4 significant bits
+            }
+        void* A;
+        uint8_t* S8;
+        bf16_t *Sb, *Sb2;
+        float *O1, *O2, *sl;
+        CK(hipMalloc(&A, hA.size()));
+        CK(hipMalloc(&S8, hS8.size()));
+        CK(hipMalloc(&Sb, hSb.size() * 2));
+        CK(hipMalloc(&Sb2, hSb.size() * 2));
+        CK(hipMalloc(&O1, m * LP * 4));
+        CK(hipMalloc(&O2, m * LP * 4));
+        CK(hipMalloc(&sl, (size_t)64 * m * LP * 4));
+        CK(hipMemcpy(A, hA.data(), hA.size(), hipMemcpyHostToDevice));
+        CK(hipMemcpy(S8, hS8.data(), hS8.size(), hipMemcpyHostToDevice));
+        CK(hipMemcpy(Sb, hSb.data(), hSb.size() * 2, hipMemcpyHostToDevice));
+        // the engine's own conversion bf16 -> e4m3 must reproduce the codes
+        CK(launch_bf16_to_fp8(Sb, npad * LP, reinterpret_cast<fp8_t*>(Sb2), S));
+        std::vector<uint8_t> back(hS8.size());
+        CK(hipMemcpy(back.data(), Sb2, back.size(), hipMemcpyDeviceToHost));
+        size_t bad = 0;
+        for (size_t i = 0; i < back.size(); ++i) {
+            const bool z1 = (back[i] & 0x7f) == 0, z2 = (hS8[i] & 0x7f) == 0;  // +-0 may flip sign
+            bad += !(back[i] == hS8[i] || (z1 && z2));
+        }
+        WProjPlan p = plan_wproj(m, n, LP, true, true, true);
+        CK(launch_wproj(1, 1, A, m, m, n, Sb, nullptr, LP, p, sl, O1, S));
+        CK(launch_wproj_s8(A, m, m, n, reinterpret_cast<const fp8_t*>(S8), LP, p, sl, O2, S));
+        CK(hipStreamSynchronize(S));
+        std::vector<float> a(m * LP), b(m * LP);
+        CK(hipMemcpy(a.data(), O1, a.size() * 4, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(b.data(), O2, b.size() * 4, hipMemcpyDeviceToHost));
+        double md = 0, mx = 0;
+        for (size_t i = 0; i < a.size(); ++i) {
+            md = std::max(md, (double)fabs(a[i] - b[i]));
+            mx = std::max(mx, (double)fabs(a[i]));
+        }
+        const double bytes = (double)m * n;
+        double t1 = time_us([&] { CK(launch_wproj(1, 1, A, m, m, n, Sb, nullptr, LP, p, sl, O1, S)); });
+        double t2 = time_us([&] { CK(launch_wproj_s8(A, m, m, n, reinterpret_cast<const fp8_t*>(S8), LP, p, sl, O2, S)); });
+        printf("check_s8 LP=%d m=%ld n=%ld: max|bf16 path - fp8 path| = %.3e (max %.3e); bf16->e4m3 code mismatches %zu;"
+               " bf16 path %.1f us, fp8 path %.1f us (%.0f GB/s)\n", LP, (long)m, (long)n, md, mx, bad, t1, t2,
+               bytes / t2 / 1e3);
+        CK(hipFree(A)); CK(hipFree(S8)); CK(hipFree(Sb)); CK(hipFree(Sb2)); CK(hipFree(O1)); CK(hipFree(O2));
+        CK(hipFree(sl));
+    }
+    // C5 shape timing on random data
+    const int64_t m = 131072, n = 8192;
+    const int LP = 512;
+    void* A;
+    uint8_t* S8;
+    bf16_t* Sb;
+    float *O, *sl;
+    CK(hipMalloc(&A, (size_t)m * n));
+    hipLaunchKernelGGL(fill_random_kernel, dim3(4096), dim3(256), 0, S, (uint16_t*)A, (size_t)m * n / 2, 1);
+    CK(hipMalloc(&S8, (size_t)n * LP));
+    hipLaunchKernelGGL(fill_random_kernel, dim3(4096), dim3(256), 0, S, (uint16_t*)S8, (size_t)n * LP / 2, 1);
+    Sb = dev_random<bf16_t>((size_t)n * LP);
+    CK(hipMalloc(&O, (size_t)m * LP * 4));
+    CK(hipMalloc(&sl, (size_t)m * LP * 4));
+    WProjPlan p = plan_wproj(m, n, LP, true, true, true);
+    double t1 = time_us([&] { CK(launch_wproj(1, 1, A, m, m, n, Sb, nullptr, LP, p, sl, O, S)); });
+    double t2 = time_us([&] { CK(launch_wproj_s8(A, m, m, n, reinterpret_cast<const fp8_t*>(S8), LP, p, sl, O, S)); });
+    const double fl = 2.0 * m * n * LP;
+    printf("C5 sketch 131072x8192 e4m3, LP=512: bf16-MFMA path %.1f us (%.0f TF), fp8-MFMA path %.1f us (%.0f TF = %.3f "
+           "of the 5033 TF fp8 dense peak), splits %d\n", t1, fl / t1 / 1e6, t2, fl / t2 / 1e6, fl / t2 / 1e6 / 5033.2,
+           p.splits);
+    CK(hipFree(A)); CK(hipFree(S8)); CK(hipFree(Sb)); CK(hipFree(O)); CK(hipFree(sl));
+}
+
 int main(int argc, char** argv) {
     const std::string what = argc > 1 ? argv[1] : "all";
     CK(hipStreamCreate(&S));
@@ -381,6 +477,7 @@ int main(int argc, char** argv) {
     if (what == "all" || what == "proj") bench_proj();
     if (what == "all" || what == "check") check_proj();
     if (what == "probe") probe_glds();
+    if (what == "s8") check_s8();
     CK(hipStreamDestroy(S));
     return 0;
 }
