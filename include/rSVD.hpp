@@ -38,7 +38,7 @@ inline Mat_m generateOmega(int n, int l) { return rsvd::generate_omega<Mat_m>(n,
 // int l) -- q = 1 and the power-method small SVD with V = VT^T in columns
 // (image_compression/src/rSVD.cpp:77-118, src/SVD.cpp:31-55).  An overload of the 6-argument form.
 inline void rSVD(Mat_m &A, Mat_m &U, Vec_v &S, Mat_m &V, int l) {
-    rsvd::rsvd_columns(A, U, S, V, l, rsvd::Method::Power, /*q=*/1);
+    rsvd::rsvd_columns(A, U, S, V, l, rsvd::Method::PowerImageCompression, /*q=*/1);
 }
 
 #endif

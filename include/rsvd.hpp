@@ -32,7 +32,12 @@
 
 namespace rsvd {
 
-enum class Method { Jacobi = RSVD_SVD_JACOBI, Power = RSVD_SVD_POWER, ParallelJacobi = RSVD_SVD_PARALLEL_JACOBI };
+enum class Method {
+    Jacobi = RSVD_SVD_JACOBI,
+    Power = RSVD_SVD_POWER,
+    ParallelJacobi = RSVD_SVD_PARALLEL_JACOBI,
+    PowerImageCompression = RSVD_SVD_POWER_IC  // image_compression's power-method SVD (5-argument rSVD)
+};
 
 class Context {
 public:
@@ -81,9 +86,9 @@ inline void check(int status, const char* what) {
 
 // rSVD(A, U, S, V, l, method) with q power iterations (the reference hard-codes q = 2).
 // rSVD with the outputs as the C ABI returns them: U m x d, S d, V n x d with the right singular
-// vectors in COLUMNS for every method (d = min(l, n)).  With Method::Power and q = 1 this is
-// image_compression's 5-argument rSVD(A, U, S, V, l) (image_compression/src/rSVD.cpp:77-118:
-// q = 1, power-method small SVD with V = VT^T, image_compression/src/SVD.cpp:31-55).
+// vectors in COLUMNS for every method (d = min(l, n)).  With Method::PowerImageCompression and
+// q = 1 this is image_compression's 5-argument rSVD(A, U, S, V, l) (image_compression/src/rSVD.cpp:
+// 77-118: q = 1, power-method small SVD with V = VT^T, image_compression/src/SVD.cpp:31-55).
 template <class Mat, class Vec>
 void rsvd_columns(const Mat& A, Mat& U, Vec& S, Mat& V, int l, Method method, int q) {
     const int64_t m = A.rows(), n = A.cols();

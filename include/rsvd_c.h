@@ -54,8 +54,17 @@ typedef enum {
  * fp32 at the ABI. */
 typedef enum { RSVD_F64 = 0, RSVD_F32 = 1, RSVD_BF16 = 2, RSVD_FP8_E4M3 = 3 } rsvd_dtype_t;
 
-/* Mirrors enum class SVDMethod { Jacobi, Power, ParallelJacobi } (include/SVD_class.hpp:28-32). */
-typedef enum { RSVD_SVD_JACOBI = 0, RSVD_SVD_POWER = 1, RSVD_SVD_PARALLEL_JACOBI = 2 } rsvd_svd_method_t;
+/* Mirrors enum class SVDMethod { Jacobi, Power, ParallelJacobi } (include/SVD_class.hpp:28-32).
+ * RSVD_SVD_POWER_IC (rsvd_run / rsvd_range_finder only) is image_compression's power-method small
+ * SVD behind its 5-argument rSVD (image_compression/src/SVD.cpp:30-55, PowerMethod.cpp:3-43): B is
+ * recomputed as A^T A of the deflated matrix after every triplet and there is no sigma < 1e-12 stop
+ * (a triplet with sigma == 0, where the reference divides by zero, ends it); V in columns. */
+typedef enum {
+    RSVD_SVD_JACOBI = 0,
+    RSVD_SVD_POWER = 1,
+    RSVD_SVD_PARALLEL_JACOBI = 2,
+    RSVD_SVD_POWER_IC = 3
+} rsvd_svd_method_t;
 
 /* Orthonormalisation of the tall-skinny panels.  AUTO = CholeskyQR (one pass for fp32 power-
  * iteration intermediates, two otherwise) with a predicated Gram-Schmidt (CGS2) re-

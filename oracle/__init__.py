@@ -68,6 +68,10 @@ def lib(opt: str = "O3"):
     L.orc_rsvd.restype = i32
     L.orc_rsvd_power.argtypes = [i64, i64, dp, i64, i64, i64, dp, i64, u64, dp, dp, dp]
     L.orc_rsvd_power.restype = i64
+    L.orc_ic_power_svd.argtypes = [i64, i64, dp, i64, i64, u64, dp, dp, dp]
+    L.orc_ic_power_svd.restype = i64
+    L.orc_ic_rsvd.argtypes = [i64, i64, dp, i64, i64, dp, i64, u64, dp, dp, dp]
+    L.orc_ic_rsvd.restype = i64
     if opt == "O3":
         _LIB = L
     return L
@@ -211,6 +215,34 @@ def rsvd_power(A, l: int, q: int = 2, Omega=None, seed: int = 0, pm_seed: int = 
         return U, S, V
     if k == 0:
         return np.zeros((m, 1)), np.zeros(1), np.zeros((n, 1))
+    return U[:, :k].copy(order="F"), S[:k].copy(), V[:, :k].copy(order="F")
+
+
+def ic_power_svd(data, dim: int = 0, seed: int = 0):
+    """image_compression's singularValueDecomposition (image_compression/src/SVD.cpp:30-55): U (m x
+    dim), S (dim), V (n x dim, v_i in columns); B = A^T A recomputed after every deflation, no early
+    stop.  Start vectors Philox(seed + i) (the reference draws std::random_device)."""
+    D = _f(data)
+    m, n = D.shape
+    dim = dim or min(m, n)
+    U = np.zeros((m, dim), order="F")
+    S = np.zeros(dim)
+    V = np.zeros((n, dim), order="F")
+    k = lib().orc_ic_power_svd(m, n, _p(D), m, dim, seed, _p(U), _p(S), _p(V))
+    return U[:, :k].copy(order="F"), S[:k].copy(), V[:, :k].copy(order="F")
+
+
+def ic_rsvd(A, l: int, Omega, pm_seed: int = 0):
+    """image_compression's 5-argument rSVD(A, U, S, V, l) (image_compression/src/rSVD.cpp:77-118):
+    q = 1, the power-method SVD above on B = Q^T A.  U (m x d), S (d), V (n x d), d = min(l, n)."""
+    A = _f(A)
+    m, n = A.shape
+    Om = _f(Omega)
+    d = min(l, n)
+    U = np.zeros((m, d), order="F")
+    S = np.zeros(d)
+    V = np.zeros((n, d), order="F")
+    k = lib().orc_ic_rsvd(m, n, _p(A), m, l, _p(Om), n, pm_seed, _p(U), _p(S), _p(V))
     return U[:, :k].copy(order="F"), S[:k].copy(), V[:, :k].copy(order="F")
 
 

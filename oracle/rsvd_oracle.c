@@ -540,3 +540,66 @@ int64_t orc_rsvd_power(int64_t m, int64_t n, const double *A, int64_t lda, int64
     free(Ut); free(B); free(Q);
     return kept;
 }
+
+/* ------------------------------------------------------------------------------------------ */
+/* image_compression's power-method SVD (image_compression/src/SVD.cpp:30-55 with powerMethod,   */
+/* PowerMethod.cpp:3-43) and its 5-argument rSVD (image_compression/src/rSVD.cpp:77-118).        */
+/* Differences from SVD<Power> above: after every triplet A -= sigma u v^T and B = A^T A is       */
+/* RECOMPUTED (SVD.cpp:47-48), and there is no sigma < 1e-12 stop (a sigma of 0 makes the         */
+/* reference divide by zero; the oracle stops there and reports the triplets written).           */
+/* U: m x dim, S: dim, V: n x dim with v_i in column i (V = VT^T, SVD.cpp:54).                   */
+/* ------------------------------------------------------------------------------------------ */
+int64_t orc_ic_power_svd(int64_t m, int64_t n, const double *data_in, int64_t ld, int64_t dim, uint64_t seed,
+                         double *U, double *S, double *V) {
+    double *A = (double *)malloc(sizeof(double) * (size_t)(m * n));
+    for (int64_t j = 0; j < n; ++j) memcpy(A + IDX(0, j, m), data_in + IDX(0, j, ld), sizeof(double) * (size_t)m);
+    double *B = (double *)malloc(sizeof(double) * (size_t)(n * n));
+    double *x0 = (double *)malloc(sizeof(double) * (size_t)n);
+    double *res = (double *)malloc(sizeof(double) * (size_t)n);
+    double *u = (double *)malloc(sizeof(double) * (size_t)m);
+    orc_gemm('T', 'N', n, n, m, A, m, A, m, 0.0, B, n); /* B = A^T A (SVD.cpp:40) */
+    const double eps = 1.e-10, delta = 0.05, lambda = 0.1; /* PowerMethod.cpp:24-27 */
+    const int s = (int)ceil(log(4.0 * log(2.0 * (double)n / delta) / (eps * delta)) / (2.0 * lambda));
+    for (int64_t i = 0; i < m * dim; ++i) U[i] = 0.0;
+    for (int64_t i = 0; i < n * dim; ++i) V[i] = 0.0;
+    for (int64_t i = 0; i < dim; ++i) S[i] = 0.0;
+    int64_t kept = dim;
+    for (int64_t i = 0; i < dim; ++i) {
+        orc_philox_gaussian(seed + (uint64_t)i, 0, n, x0);
+        nrm(x0, n);
+        for (int it = 1; it <= s; ++it) { /* x0 = B x0; x0.normalize() (:29-32) */
+            orc_gemm('N', 'N', n, 1, n, B, n, x0, n, 0.0, res, n);
+            memcpy(x0, res, sizeof(double) * (size_t)n);
+            nrm(x0, n);
+        }
+        nrm(x0, n); /* v = x0.normalized() (:35-36) */
+        orc_gemm('N', 'N', m, 1, n, A, m, x0, n, 0.0, u, m);
+        double sigma = 0.0;
+        for (int64_t t = 0; t < m; ++t) sigma += u[t] * u[t];
+        sigma = sqrt(sigma); /* sigma = (A v).norm() (:39) */
+        if (!(sigma > 0.0)) { kept = i; break; }
+        for (int64_t t = 0; t < m; ++t) u[t] /= sigma; /* u = A v / sigma (:42) */
+        for (int64_t c = 0; c < n; ++c) /* A -= sigma u v^T (SVD.cpp:47) */
+            for (int64_t t = 0; t < m; ++t) A[IDX(t, c, m)] -= sigma * u[t] * x0[c];
+        orc_gemm('T', 'N', n, n, m, A, m, A, m, 0.0, B, n); /* B = A^T A (:48) */
+        for (int64_t t = 0; t < m; ++t) U[IDX(t, i, m)] = u[t];
+        for (int64_t c = 0; c < n; ++c) V[IDX(c, i, n)] = x0[c];
+        S[i] = sigma;
+    }
+    free(u); free(res); free(x0); free(B); free(A);
+    return kept;
+}
+
+int64_t orc_ic_rsvd(int64_t m, int64_t n, const double *A, int64_t lda, int64_t l, const double *Omega, int64_t ldo,
+                    uint64_t pm_seed, double *U, double *S, double *V) {
+    double *Q = (double *)malloc(sizeof(double) * (size_t)(m * l));
+    orc_intermediate_step(m, n, A, lda, Omega, ldo, l, 1, Q, m); /* q = 1 (image_compression/src/rSVD.cpp:103) */
+    double *B = (double *)malloc(sizeof(double) * (size_t)(l * n));
+    orc_gemm('T', 'N', l, n, m, Q, m, A, lda, 0.0, B, l); /* B = Q^T A (:109) */
+    const int64_t d = l < n ? l : n;                      /* min_dim (:112) */
+    double *Ut = (double *)malloc(sizeof(double) * (size_t)(l * d));
+    const int64_t kept = orc_ic_power_svd(l, n, B, l, d, pm_seed, Ut, S, V);
+    orc_gemm('N', 'N', m, d, l, Q, m, Ut, l, 0.0, U, m); /* U = Q * Utilde (:117) */
+    free(Ut); free(B); free(Q);
+    return kept;
+}

@@ -92,4 +92,14 @@ int64_t orc_rsvd_power(int64_t m, int64_t n, const double *A, int64_t lda, int64
 #ifdef __cplusplus
 }
 #endif
+/* image_compression's power-method SVD (image_compression/src/SVD.cpp:30-55, PowerMethod.cpp:3-43):
+ * B recomputed as A^T A after every deflation, no sigma < 1e-12 stop; V (n x dim) in columns; start
+ * vectors orc_philox_gaussian(seed + i).  Returns the triplets written (dim unless a sigma is 0). */
+int64_t orc_ic_power_svd(int64_t m, int64_t n, const double *data, int64_t ld, int64_t dim, uint64_t seed,
+                         double *U, double *S, double *V);
+/* image_compression's 5-argument rSVD (image_compression/src/rSVD.cpp:77-118): q = 1, the power-method
+ * SVD above on B = Q^T A with dim = min(l, n).  U m x d, S d, V n x d (d = min(l, n)). */
+int64_t orc_ic_rsvd(int64_t m, int64_t n, const double *A, int64_t lda, int64_t l, const double *Omega, int64_t ldo,
+                    uint64_t pm_seed, double *U, double *S, double *V);
+
 #endif

@@ -19,10 +19,12 @@ from .api import (  # noqa: F401
     qr_decomposition_full,
     qr_decomposition_reduced,
     rSVD,
+    rSVD_image_compression,
 )
 
 __all__ = [
     "build", "row_partition", "RSVDError", "Engine", "QRMode", "SVDMethod", "colmajor",
     "default_engine", "empty_colmajor", "generateOmega", "intermediate_step", "make_allreduce_hook", "rSVD",
+    "rSVD_image_compression",
     "SVD", "qr_decomposition_full", "qr_decomposition_reduced",
 ]

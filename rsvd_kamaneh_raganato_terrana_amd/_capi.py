@@ -27,7 +27,7 @@ STATUS = {
 }
 
 F64, F32, BF16, FP8_E4M3 = 0, 1, 2, 3
-SVD_JACOBI, SVD_POWER, SVD_PARALLEL_JACOBI = 0, 1, 2
+SVD_JACOBI, SVD_POWER, SVD_PARALLEL_JACOBI, SVD_POWER_IC = 0, 1, 2, 3
 QR_AUTO, QR_GS2, QR_CHOLQR2 = 0, 1, 2
 
 # Every symbol include/rsvd_c.h declares (checked by tests/test_capi_exports.py).

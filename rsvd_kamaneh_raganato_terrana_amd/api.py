@@ -393,6 +393,17 @@ def rSVD(A, l: int, method: SVDMethod = SVDMethod.Jacobi, q: int = 2, omega=None
     return U[:, :kept], S[:kept], Vf[:, :kept]
 
 
+def rSVD_image_compression(A, l: int, omega=None, seed: int = 0):
+    """image_compression's 5-argument rSVD(A, U, S, V, l) (image_compression/src/rSVD.cpp:77-118): q = 1,
+    its own power-method SVD of B (image_compression/src/SVD.cpp:30-55 -- B = A^T A recomputed after
+    every deflation, no sigma < 1e-12 stop) and V = VT^T with the right singular vectors in columns.
+    Returns (U m x d, S d, V n x d), d = min(l, n)."""
+    eng = default_engine()
+    if _is_torch(A):
+        return eng.rsvd(A, l, q=1, method=_capi.SVD_POWER_IC, omega=omega, seed=seed)
+    return eng.rsvd_host(A, l, q=1, method=_capi.SVD_POWER_IC, omega=omega, seed=seed)
+
+
 def intermediate_step(A, Omega, l: int, q: int):
     """intermediate_step (src/rSVD.cpp:57-70): the orthonormal range basis Q (m x l)."""
     eng = default_engine()

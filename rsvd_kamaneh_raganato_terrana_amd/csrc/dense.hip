@@ -320,7 +320,10 @@ __global__ __launch_bounds__(kPowThreads) void power_svd_kernel(const T* __restr
             sq += acc * acc;
         }
         const double sigma = sqrt(block_sum(sq, red));
-        if (sigma < 1e-12) {  // SVD_class.hpp:198-208
+        // SVD_class.hpp:198-208 stops at sigma < 1e-12; image_compression's SVD (rsvd_mode 2,
+        // image_compression/src/SVD.cpp:44-51) has no stop -- it only ends here at sigma == 0, where
+        // the reference would divide by zero (u = A v / sigma, PowerMethod.cpp:42)
+        if (rsvd_mode == 2 ? !(sigma > 0.0) : sigma < 1e-12) {
             k = i;
             break;
         }
@@ -330,10 +333,38 @@ __global__ __launch_bounds__(kPowThreads) void power_svd_kernel(const T* __restr
             Up[r * LP + i] = (T)u;
             sq += u * u;
         }
-        const double f = sigma * sigma * block_sum(sq, red);  // B -= update^T update (:212)
-        for (int e = tid; e < n * n; e += kPowThreads) {
-            const int r = e / n, c = e - r * n;
-            B[(int64_t)r * LP + c] -= f * (x[r] * x[c]);
+        const double f = sigma * sigma * block_sum(sq, red);
+        if (rsvd_mode == 2) {
+            // image_compression recomputes B = A_{i+1}^T A_{i+1} after A_{i+1} = A_i - sigma u v^T
+            // (SVD.cpp:47-48): B' = B - sigma (w v^T + v w^T) + sigma^2 (u.u) v v^T with w = A_i^T u,
+            // A_i = P - sum_j sigma_j u_j v_j^T (the deflations so far)
+            {
+                const int lane = tid & 63, w = tid >> 6;
+                for (int j = w; j < i; j += kPowThreads / 64) {  // coef_j = sigma_j (u_j . u)
+                    double d = 0.0;
+                    for (int64_t r = lane; r < m; r += 64) d += (double)Up[r * LP + j] * (double)Up[r * LP + i];
+#pragma unroll
+                    for (int o = 32; o > 0; o >>= 1) d += __shfl_xor(d, o);
+                    if (lane == 0) coef[j] = S[j] * d;
+                }
+                __syncthreads();
+            }
+            for (int c = tid; c < n; c += kPowThreads) {  // y <- w
+                double acc = 0.0;
+                for (int64_t r = 0; r < m; ++r) acc += (double)P[r * LP + c] * (double)Up[r * LP + i];
+                for (int j = 0; j < i; ++j) acc -= coef[j] * Vr[rsvd_mode ? (int64_t)c * LP + j : (int64_t)j * LP + c];
+                y[c] = acc;
+            }
+            __syncthreads();
+            for (int e = tid; e < n * n; e += kPowThreads) {
+                const int r = e / n, c = e - r * n;
+                B[(int64_t)r * LP + c] += f * (x[r] * x[c]) - sigma * (y[r] * x[c] + x[r] * y[c]);
+            }
+        } else {
+            for (int e = tid; e < n * n; e += kPowThreads) {  // B -= update^T update (:212)
+                const int r = e / n, c = e - r * n;
+                B[(int64_t)r * LP + c] -= f * (x[r] * x[c]);
+            }
         }
         for (int c = tid; c < n; c += kPowThreads)  // V_.row(i) = v (:214); rsvd mode: column i
             Vr[rsvd_mode ? (int64_t)c * LP + i : (int64_t)i * LP + c] = x[c];

@@ -36,7 +36,8 @@ int power_iterations(int64_t n);
 // u_i -> column i of Up (m x LP panel), v_i -> row i of Vr (LP x LP), S[i]; *kept = triplets
 // found (< dim when sigma < 1e-12 stops it).  One workgroup.  n <= LP <= 512.
 // x0 (nullable): start vectors as rows of an LP x LP matrix instead of Philox(seed + i).
-// rsvd_mode: v_i goes to COLUMN i of Vr, and triplets past an early stop are written as zeros.
+// rsvd_mode: v_i goes to COLUMN i of Vr, and triplets past an early stop are written as zeros;
+// rsvd_mode 2: image_compression's deflation (B recomputed as A_i^T A_i, no sigma < 1e-12 stop).
 hipError_t launch_power_svd(const double* P, int64_t m, int n, int LP, double* B, int dim, uint64_t seed, int iters,
                             double* Up, double* Vr, double* S, int* kept, hipStream_t s, const double* x0 = nullptr,
                             int rsvd_mode = 0);

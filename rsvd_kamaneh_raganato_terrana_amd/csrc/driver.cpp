@@ -74,7 +74,8 @@ int check_desc_msg(const rsvd_desc_t* d, const char** err) {
     }
     if (d->dtype < RSVD_F64 || d->dtype > RSVD_FP8_E4M3) { *err = "unsupported dtype"; return RSVD_ERR_UNSUPPORTED; }
     if (d->qr_mode < RSVD_QR_AUTO || d->qr_mode > RSVD_QR_CHOLQR2) { *err = "bad qr_mode"; return RSVD_ERR_INVALID_ARG; }
-    if (d->method != RSVD_SVD_JACOBI && d->method != RSVD_SVD_PARALLEL_JACOBI && d->method != RSVD_SVD_POWER) {
+    if (d->method != RSVD_SVD_JACOBI && d->method != RSVD_SVD_PARALLEL_JACOBI && d->method != RSVD_SVD_POWER &&
+        d->method != RSVD_SVD_POWER_IC) {
         *err = "Unsupported SVD method";  // src/rSVD.cpp:123 wording
         return RSVD_ERR_UNSUPPORTED;
     }
@@ -258,7 +259,7 @@ struct Engine {
         RSVD_TRY(cross_gram(Xn, T1, L.n, Y0));  // Y0 = Q_B^T X0
         RSVD_CK(launch_power_prep(R1, Y0, L.l, L.LP, Pp, X0s, Bpm, s));
         RSVD_CK(launch_power_svd(Pp, L.l, L.l, L.LP, Bpm, L.l, 0, power_iterations(L.n), Up, Vc, Sd, h->dflags + 16,
-                                 s, X0s, 1));
+                                 s, X0s, d->method == RSVD_SVD_POWER_IC ? 2 : 1));
         RSVD_CK(launch_convert_scale<T>(Sd, S, L.l, std::fabs(a_scale_of(d)), s));
         RSVD_CK(launch_panel_small<T>(Qm, L.m, L.LP, Up, reinterpret_cast<T*>(U), 1, L.l, ldu, s));
         RSVD_CK(launch_panel_small<T>(Xn, L.n, L.LP, Vc, reinterpret_cast<T*>(V), 1, L.l, ldv, s));
@@ -281,7 +282,7 @@ struct Engine {
         RSVD_TRY(cross_gram(Xn, Zn, L.n, R1));    // R = Q_B^T B^T exactly (fp64), W = R^T
         // Inf / NaN in A reach R through B^T = A^T Q whatever the orthonormalisations did with them
         RSVD_CK(launch_check_finite<double>(R1, L.LP * L.LP, h->dflags + kFlagNonFinite, s));
-        if (d->method == RSVD_SVD_POWER) return power_stage(d, U, ldu, S, V, ldv);
+        if (d->method == RSVD_SVD_POWER || d->method == RSVD_SVD_POWER_IC) return power_stage(d, U, ldu, S, V, ldv);
         RSVD_CK(launch_small_svd<T>(R1, L.l, L.LP, Uw, Vw, S, h->dflags + 1, s));
         const double sc = std::fabs(a_scale_of(d));
         if (sc != 1.0) RSVD_CK(launch_scale_cols<T>(S, L.l, 1, L.l, sc, s));

@@ -314,7 +314,7 @@ struct WideEngine {
         RSVD_CK(launch_gram_wide<T>(Xn, T1, L.n, L.LP, L.gx, gslab, Y0, nullptr, s));  // Y0 = Q_B^T X0
         RSVD_CK(launch_power_prep(R1, Y0, L.l, L.LP, Pp, X0s, Bpm, s));
         RSVD_CK(launch_power_svd(Pp, L.l, L.l, L.LP, Bpm, L.l, 0, power_iterations(L.n), Up, Vc, Sd, h->dflags + 16,
-                                 s, X0s, 1));
+                                 s, X0s, d->method == RSVD_SVD_POWER_IC ? 2 : 1));
         RSVD_CK(launch_convert_scale<T>(Sd, S, L.l, std::fabs(a_scale(d)), s));
         if (sizeof(T) == 4) {
             const int L2 = L.LP * L.LP;
@@ -343,7 +343,7 @@ struct WideEngine {
         RSVD_CK(launch_gram_wide<T>(Xn, Zn, L.n, L.LP, L.gx, gslab, R1, nullptr, s));  // R = Q_B^T B^T
         // Inf / NaN in A reach R through B^T = A^T Q whatever the orthonormalisations did with them
         RSVD_CK(launch_check_finite<double>(R1, L.LP * L.LP, h->dflags + kFlagNonFinite, s));
-        if (d->method == RSVD_SVD_POWER) return power_stage(d, U, ldu, S, V, ldv);
+        if (d->method == RSVD_SVD_POWER || d->method == RSVD_SVD_POWER_IC) return power_stage(d, U, ldu, S, V, ldv);
         // the small SVD always runs in fp64 (U_w, V_w feed the fp32 panel products of U and V)
         double* Sd = G;  // free scratch by now
         if (L.LP <= 64) {

@@ -67,16 +67,37 @@ def test_rsvd_power_reference_layout_and_early_stop(engine):
 
 
 def test_image_compression_rsvd_q1_power(engine):
-    # image_compression/src/rSVD.cpp:77-118: q = 1, power-method small SVD, V = VT^T (columns)
+    """image_compression's 5-argument rSVD (image_compression/src/rSVD.cpp:77-118): q = 1 and ITS power-
+    method SVD (image_compression/src/SVD.cpp:30-55: B = A^T A recomputed after every deflation, no
+    early stop), V = VT^T in columns -- against the oracle's restatement of exactly that
+    (oracle.ic_rsvd)."""
     import rsvd_kamaneh_raganato_terrana_amd as R
 
     m, n, l = 512, 384, 24
     A = gapped_matrix(m, n, 2 * l, decay=0.8, seed=21)
-    U, S, V = engine.rsvd_host(A, l, q=1, method=R.SVDMethod.Power, seed=99)
+    U, S, V = R.rSVD_image_compression(A, l, seed=99)
     assert U.shape == (m, l) and S.shape == (l,) and V.shape == (n, l)
     Om = engine.generate_omega_host(n, l, seed=99)
-    Uo, So, Vf = oracle.rsvd_power(A, l, q=1, Omega=Om, pm_seed=99 ^ PM_KEY)
+    Uo, So, Vo = oracle.ic_rsvd(A, l, Om, pm_seed=99 ^ PM_KEY)
     k = 12
     assert rel_fro(S[:k], So[:k]) < 1e-10
-    assert rel_fro(sign_align(V[:, :k], Vf[:k, :].T), Vf[:k, :].T) < 1e-8
+    assert rel_fro(sign_align(V[:, :k], Vo[:, :k]), Vo[:, :k]) < 1e-8
     assert rel_fro(sign_align(U[:, :k], Uo[:, :k]), Uo[:, :k]) < 1e-8
+
+
+def test_image_compression_rsvd_has_no_early_stop(engine):
+    """Rank 3, l = 8: SVD<Power> stops after three triplets (sigma < 1e-12, SVD_class.hpp:198-208);
+    image_compression's SVD has no such stop and returns all l triplets (SVD.cpp:44-51)."""
+    import rsvd_kamaneh_raganato_terrana_amd as R
+
+    rng = np.random.default_rng(3)
+    m, n, l = 120, 90, 8
+    A = np.asfortranarray((rng.standard_normal((m, 3)) * [3.0, 2.0, 1.0]) @ rng.standard_normal((3, n)))
+    U, S, V = R.rSVD_image_compression(A, l, seed=8)
+    Om = engine.generate_omega_host(n, l, seed=8)
+    Uo, So, Vo = oracle.ic_rsvd(A, l, Om, pm_seed=8 ^ PM_KEY)
+    assert S.shape == (l,) and So.shape == (l,) and U.shape == (m, l) and V.shape == (n, l)
+    assert rel_fro(S[:3], So[:3]) < 1e-10
+    assert np.all(S[3:] < 1e-10 * S[0])
+    Up, Sp, Vp = R.rSVD(A, l, R.SVDMethod.Power, q=1, seed=8)
+    assert Sp.shape == (3,)

@@ -156,6 +156,45 @@ def test_power_method_svd_matches_lapack():
     assert np.max(np.abs(S[:5] - Sg[:5])) < 1e-6
 
 
+def test_image_compression_power_svd_known_answers():
+    """image_compression's SVD (image_compression/src/SVD.cpp:30-55) on its own test inputs
+    (image_compression/data/input/mat/*.mtx, tests/golden/inputs.npz).  The diagonal matrices have
+    sigma = 100, 99, 98, ...: ratios of 0.99 that the fixed s(n) power iterations
+    (PowerMethod.cpp:24-27) resolve only to ~1e-3 -- the reference's own accuracy on them; the
+    dim triplets are all returned (no early stop) with unit singular vectors."""
+    for name in ("sparse_diagonal_matrix", "block_diagonal_matrix"):
+        A = INPUTS[name].astype(np.float64)
+        U, S, V = oracle.ic_power_svd(A, 10, seed=5)
+        Sg = np.linalg.svd(A, compute_uv=False)
+        assert S.shape == (10,) and U.shape == (100, 10) and V.shape == (100, 10)
+        assert np.max(np.abs(S - Sg[:10])) < 1e-3 * Sg[0]
+        assert np.allclose(np.linalg.norm(U, axis=0), 1.0) and np.allclose(np.linalg.norm(V, axis=0), 1.0)
+    # image_compression/tests/SVD_test2.cpp:30-34 style 4 x 4 known matrix against LAPACK
+    A = np.asfortranarray(np.array([[4.0, 0, 0, 0], [0, 3, 0, 0], [0, 0, 2, 0], [0, 0, 0, 1]]) +
+                          0.1 * np.arange(16).reshape(4, 4))
+    U, S, V = oracle.ic_power_svd(A, 4, seed=2)
+    Sg = np.linalg.svd(A, compute_uv=False)
+    assert np.max(np.abs(S - Sg)) < 1e-9 * Sg[0]
+
+
+def test_image_compression_svd_recomputes_b():
+    """The two power-method SVDs differ only in how B follows the deflation: SVD<Power> updates
+    B -= (sigma u v^T)^T (sigma u v^T) (SVD_class.hpp:212), image_compression recomputes A^T A
+    (SVD.cpp:48) -- the same matrix when v is an exact eigenvector.  Rank 3: SVD<Power> stops at
+    sigma < 1e-12 after three triplets, image_compression's SVD keeps going."""
+    rng = np.random.default_rng(3)
+    A = np.asfortranarray((rng.standard_normal((40, 3)) * [3.0, 2.0, 1.0]) @ rng.standard_normal((3, 30)))
+    U, S, V = oracle.ic_power_svd(A, 6, seed=4)
+    Up, Sp, Vp = oracle.power_svd(A, r=6, seed=4)
+    assert Sp.shape == (3,) and S.shape == (6,)
+    assert np.max(np.abs(S[:3] - Sp)) < 1e-10 * S[0]
+    assert np.all(S[3:] < 1e-10 * S[0])
+    Om = oracle.generate_omega(30, 8, 9)
+    Ui, Si, Vi = oracle.ic_rsvd(A, 8, Om, pm_seed=1)
+    assert Si.shape == (8,) and Ui.shape == (40, 8) and Vi.shape == (30, 8)
+    assert np.max(np.abs(Si[:3] - np.linalg.svd(A, compute_uv=False)[:3])) < 1e-9 * Si[0]
+
+
 def test_unsupported_method_raises():
     with pytest.raises(ValueError):
         oracle.rsvd(np.eye(8), 4, method=7)

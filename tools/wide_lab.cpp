@@ -208,8 +208,24 @@ static void bench_jac() {
 #ifdef RSVD_BJ_PROF
         rsvd::bj_prof_dump();
 #endif
-        printf("block_jacobi LP=%d: %.1f us  sweeps=%d timeout=%d  S[0]=%.6f S[last]=%.3e\n", LP, t, hinfo[0], hinfo[2],
-               hS[0], hS[LP - 1]);
+        std::vector<double> hU((size_t)LP * LP), hV((size_t)LP * LP);
+        CK(hipMemcpy(hU.data(), Uw, hU.size() * 8, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(hV.data(), Vw, hV.size() * 8, hipMemcpyDeviceToHost));
+        double rec = 0, wn = 0, orth = 0;  // W = R^T = Uw diag(S) Vw^T (row-major [row][col]); Vw^T Vw = I
+        for (int i = 0; i < LP; ++i)
+            for (int j = 0; j < LP; ++j) {
+                double a = 0, o = 0;
+                for (int k = 0; k < LP; ++k) {
+                    a += hU[(size_t)i * LP + k] * hS[k] * hV[(size_t)j * LP + k];
+                    o += hV[(size_t)k * LP + i] * hV[(size_t)k * LP + j];
+                }
+                const double w = hR[(size_t)j * LP + i];
+                rec += (a - w) * (a - w);
+                wn += w * w;
+                orth += (o - (i == j)) * (o - (i == j));
+            }
+        printf("block_jacobi LP=%d: %.1f us  sweeps=%d timeout=%d  S[0]=%.6f S[last]=%.3e  |W-USV'|/|W|=%.2e  |V'V-I|=%.2e\n",
+               LP, t, hinfo[0], hinfo[2], hS[0], hS[LP - 1], sqrt(rec / wn), sqrt(orth));
         CK(hipFree(R)); CK(hipFree(X)); CK(hipFree(J)); CK(hipFree(Uw)); CK(hipFree(Vw)); CK(hipFree(Sd));
         CK(hipFree(sync)); CK(hipFree(info));
     }
