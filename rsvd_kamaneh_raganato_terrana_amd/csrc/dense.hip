@@ -471,6 +471,261 @@ hipError_t launch_shift_diag(double* G, int LP, int l, int64_t rows, double u, h
     return hipGetLastError();
 }
 
+// ------------------------------------------------------------------------------------------------
+// SVD<Power> for large n (n > 512: B = A^T A no longer fits the one-workgroup kernel above).
+//
+// gram_cm_kernel: B = A^T A (n x n fp64, symmetric, stored in full) from the column-major A, one
+// 64 x 64 tile of B per 256-thread workgroup (upper tiles only, mirrored), fp64 MFMA 16x16x4 with
+// the k order permuted inside each 16-row step so a lane reads 4 consecutive rows of one column
+// (32 contiguous bytes) per fragment.
+namespace {
+
+constexpr int kPgThreads = 256;
+
+__global__ __launch_bounds__(256) void gram_cm_kernel(const double* __restrict__ A, int64_t lda, int64_t m, int64_t n,
+                                                      double* __restrict__ B) {
+    typedef Mfma<double> MD;
+    const int nt = (int)((n + 63) / 64);
+    // upper-triangular tile index -> (ti, tj), ti <= tj
+    int t = blockIdx.x, ti = 0;
+    while (t >= nt - ti) {
+        t -= nt - ti;
+        ++ti;
+    }
+    const int tj = ti + t;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 15, h = lane >> 4;
+    const int64_t ca = (int64_t)ti * 64 + 16 * w + r;  // this lane's A-operand column
+    f64x4 acc[4] = {MD::zero(), MD::zero(), MD::zero(), MD::zero()};
+    for (int64_t k0 = 0; k0 < m; k0 += 16) {
+        const int64_t kr = k0 + 4 * h;
+        double a[4], b[4][4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) a[j] = (ca < n && kr + j < m) ? A[ca * lda + kr + j] : 0.0;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const int64_t cb = (int64_t)tj * 64 + 16 * g + r;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) b[g][j] = (cb < n && kr + j < m) ? A[cb * lda + kr + j] : 0.0;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) acc[g] = MD::mma(a[j], b[g][j], acc[g]);
+    }
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int64_t row = (int64_t)ti * 64 + 16 * w + MD::row(h, j), col = (int64_t)tj * 64 + 16 * g + r;
+            if (row < n && col < n) {
+                B[row * n + col] = acc[g][j];
+                B[col * n + row] = acc[g][j];
+            }
+        }
+}
+
+// Grid barrier of the power kernel below (counter form, MI355X_MICROARCH.md "Workgroup dispatch
+// ... inter-workgroup visibility": drained stores -> workgroup barrier -> agent release -> relaxed
+// counter add; relaxed poll -> agent acquire).  Bounded: a timeout sets the abort word.
+__device__ bool pg_barrier(unsigned* sync, unsigned target) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    __shared__ int ok;
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_fetch_add(sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int good = 1;
+        long spins = 0;
+        while (__hip_atomic_load(sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            __builtin_amdgcn_s_sleep(1);
+            if ((++spins & 1023) == 0 &&
+                (__hip_atomic_load(sync + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0 || spins > (1l << 27))) {
+                __hip_atomic_store(sync + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                good = 0;
+                break;
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        ok = good;
+    }
+    __syncthreads();
+    return ok != 0;
+}
+
+__device__ __forceinline__ double pg_block_sum(double v, double* red) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    __syncthreads();
+    if (lane == 0) red[w] = v;
+    __syncthreads();
+    double t = 0.0;
+#pragma unroll
+    for (int i = 0; i < kPgThreads / 64; ++i) t += red[i];
+    return t;
+}
+
+// Row range of workgroup g out of G for `rows` rows: the reference's split (src/PM.cpp:31-35).
+__device__ __forceinline__ void pg_rows(int64_t rows, int G, int g, int64_t& r0, int64_t& r1) {
+    const int64_t per = rows / G, rem = rows % G;
+    r0 = g * per + (g < rem ? g : rem);
+    r1 = r0 + per + (g < rem ? 1 : 0);
+}
+
+// The power method with deflation (SVD_class.hpp:183-219, src/PM.cpp:4-81) on a persistent grid:
+// workgroup g owns rows pg_rows(n, G, g) of B for the matvecs x <- B x (the reference's MPI row
+// partition of B, PM.cpp:31-35, with the Gatherv + Bcast of each iterate replaced by one grid
+// barrier: every workgroup reads the whole iterate from the L2) and rows pg_rows(m, G, g) of A for
+// u = A_i v.  The iterate is normalised on the fly: y_{t+1} = B y_t / |y_t|.  A_i = A - sum_j
+// sigma_j u_j v_j^T is applied implicitly (the coefficients sigma_j (v_j . v) are reduced over the
+// grid); B is deflated explicitly, B -= sigma^2 (u.u) v v^T (:212).  Outputs: U (m x dim, ldu),
+// V (n x dim, ldv, v_i in column i), S (dim), *kept.  Work: Y (2 n), part (G (dim + 2)), sync (8).
+__global__ __launch_bounds__(kPgThreads) void power_grid_kernel(const double* __restrict__ A, int64_t lda, int64_t m,
+                                                                int64_t n, double* __restrict__ B, int dim, uint64_t seed,
+                                                                int iters, double* __restrict__ U, int64_t ldu,
+                                                                double* __restrict__ V, int64_t ldv,
+                                                                double* __restrict__ S, double* __restrict__ Y,
+                                                                double* __restrict__ part, unsigned* __restrict__ sync,
+                                                                int* __restrict__ kept, int* __restrict__ tmo) {
+    __shared__ double red[kPgThreads / 64];
+    __shared__ double coef_s[64];
+    const int G = gridDim.x, g = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    int64_t b0, b1, a0, a1;
+    pg_rows(n, G, g, b0, b1);
+    pg_rows(m, G, g, a0, a1);
+    const int P = dim + 2;  // partial slots per workgroup
+    unsigned bar = 0;
+    auto barrier = [&]() -> bool {
+        if (pg_barrier(sync, (unsigned)G * ++bar)) return true;
+        if (g == 0 && tid == 0) atomicOr(tmo, 1);
+        return false;
+    };
+    auto grid_sum = [&](int slot) {  // fixed-order sum of the workgroups' partials in `slot`
+        double t = 0.0;
+        for (int q = 0; q < G; ++q) t += part[(size_t)q * P + slot];
+        return t;
+    };
+    double* y0 = Y;
+    double* y1 = Y + n;
+    int k = dim;
+    for (int i = 0; i < dim; ++i) {
+        // x0 = N(0,1) Philox stream (seed + i) (src/PM.cpp:15-22); |x0| over the grid
+        double sq = 0.0;
+        for (int64_t c = b0 + tid; c < b1; c += kPgThreads) {
+            const double v = gauss_elem((uint64_t)c, seed + (uint64_t)i);
+            y0[c] = v;
+            sq += v * v;
+        }
+        sq = pg_block_sum(sq, red);
+        if (tid == 0) part[(size_t)g * P + dim] = sq;
+        if (!barrier()) return;
+        double nrm = sqrt(grid_sum(dim));
+        // s iterations x <- B x / |B x| (:40-69): y_{t+1} = B (y_t / |y_t|)
+        for (int it = 0; it < iters; ++it) {
+            const double inv = 1.0 / nrm;
+            double sq2 = 0.0;
+            for (int64_t row = b0 + w; row < b1; row += kPgThreads / 64) {
+                const double* br = B + row * n;
+                double acc = 0.0;
+                for (int64_t c = lane; c < n; c += 64) acc += br[c] * y0[c];
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+                acc *= inv;
+                if (lane == 0) y1[row] = acc;
+                sq2 += (lane == 0) ? acc * acc : 0.0;
+            }
+            sq2 = pg_block_sum(sq2, red);
+            if (tid == 0) part[(size_t)g * P + dim + ((it + 1) & 1)] = sq2;
+            if (!barrier()) return;
+            nrm = sqrt(grid_sum(dim + ((it + 1) & 1)));
+            double* t = y0;
+            y0 = y1;
+            y1 = t;
+        }
+        // v = x0.normalized() (:72-73); coef_j = sigma_j (v_j . v) for the implicit deflation of A
+        const double vs = 1.0 / nrm;
+        for (int j0 = 0; j0 < i; j0 += 64) {
+            const int jn = (i - j0) < 64 ? (i - j0) : 64;
+            for (int jj = w; jj < jn; jj += kPgThreads / 64) {
+                const double* vj = V + (size_t)(j0 + jj) * ldv;
+                double d = 0.0;
+                for (int64_t c = b0 + lane; c < b1; c += 64) d += vj[c] * y0[c];
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) d += __shfl_xor(d, o);
+                if (lane == 0) part[(size_t)g * P + j0 + jj] = d * vs;
+            }
+        }
+        if (!barrier()) return;
+        // u = A_i v = A v - sum_j coef_j u_j over this workgroup's rows of A; |u| over the grid
+        double su = 0.0;
+        for (int j0 = 0; j0 <= i; j0 += 64) {  // coefficients in chunks of 64 (LDS)
+            const int jn = (i - j0) < 64 ? (i - j0) : 64;
+            if (jn <= 0 && j0 > 0) break;
+            __syncthreads();
+            if (tid < jn) coef_s[tid] = S[j0 + tid] * grid_sum(j0 + tid);
+            __syncthreads();
+            for (int64_t row = a0 + tid; row < a1; row += kPgThreads) {
+                double acc = 0.0;
+                if (j0 == 0)
+                    for (int64_t c = 0; c < n; ++c) acc += A[row + c * lda] * (y0[c] * vs);
+                else
+                    acc = U[row + (size_t)i * ldu];
+                for (int jj = 0; jj < jn; ++jj) acc -= coef_s[jj] * U[row + (size_t)(j0 + jj) * ldu];
+                U[row + (size_t)i * ldu] = acc;
+            }
+        }
+        for (int64_t row = a0 + tid; row < a1; row += kPgThreads) {
+            const double u = U[row + (size_t)i * ldu];
+            su += u * u;
+        }
+        su = pg_block_sum(su, red);
+        if (tid == 0) part[(size_t)g * P + dim] = su;
+        if (!barrier()) return;
+        const double sigma = sqrt(grid_sum(dim));
+        if (sigma < 1e-12) {  // SVD_class.hpp:198-208
+            k = i;
+            break;
+        }
+        // u /= sigma; B -= sigma^2 (u.u) v v^T (:210-212) with u.u = 1; V(:, i) = v; S[i] = sigma
+        for (int64_t row = a0 + tid; row < a1; row += kPgThreads) U[row + (size_t)i * ldu] /= sigma;
+        const double f = su * vs * vs;  // sigma^2 (u.u) = |A_i v|^2 = su, with v = y0 vs
+        for (int64_t row = b0 + w; row < b1; row += kPgThreads / 64) {
+            const double xr = y0[row];
+            double* br = B + row * n;
+            for (int64_t c = lane; c < n; c += 64) br[c] -= f * xr * y0[c];
+        }
+        for (int64_t c = b0 + tid; c < b1; c += kPgThreads) V[c + (size_t)i * ldv] = y0[c] * vs;
+        if (g == 0 && tid == 0) S[i] = sigma;
+        if (!barrier()) return;
+    }
+    if (g == 0 && tid == 0) *kept = k;
+}
+
+}  // namespace
+
+hipError_t launch_gram_colmajor(const double* A, int64_t lda, int64_t m, int64_t n, double* B, hipStream_t s) {
+    const int64_t nt = (n + 63) / 64;
+    hipLaunchKernelGGL(gram_cm_kernel, dim3((unsigned)(nt * (nt + 1) / 2)), dim3(256), 0, s, A, lda, m, n, B);
+    return hipGetLastError();
+}
+
+int power_grid_size(int64_t n) {
+    int64_t g = (n + 15) / 16;
+    return (int)(g > 256 ? 256 : (g < 1 ? 1 : g));
+}
+
+hipError_t launch_power_grid(const double* A, int64_t lda, int64_t m, int64_t n, double* B, int dim, uint64_t seed,
+                             int iters, double* U, int64_t ldu, double* V, int64_t ldv, double* S, double* Y,
+                             double* part, unsigned* sync, int* kept, int* tmo, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(sync, 0, 8 * sizeof(unsigned), s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(power_grid_kernel, dim3(power_grid_size(n)), dim3(kPgThreads), 0, s, A, lda, m, n, B, dim, seed,
+                       iters, U, ldu, V, ldv, S, Y, part, sync, kept, tmo);
+    return hipGetLastError();
+}
+
 int power_iterations(int64_t n) {
     // s = ceil(log(4 log(2 n / delta) / (eps delta)) / (2 lambda)), src/PM.cpp:25-28
     const double eps = 1.e-10, delta = 0.05, lambda = 0.1;

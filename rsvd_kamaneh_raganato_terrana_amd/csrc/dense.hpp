@@ -30,6 +30,16 @@ hipError_t launch_trsm_rows(const T* In, int64_t rows, int k, int LP, const doub
 // LP fp64 scratch.  One workgroup, LU with partial pivoting.
 template <typename T>
 hipError_t launch_det_sign(T* Qp, int m, int LP, double* W, hipStream_t s);
+// SVD<Power> for any n (dense.hip power_grid_kernel): B = A^T A (n x n fp64, full) from A (m x n
+// column-major), then the power method with deflation on a persistent grid of power_grid_size(n)
+// workgroups (row partition of B as src/PM.cpp:31-35).  U m x dim (ldu), V n x dim (ldv, v_i in
+// column i), S dim, *kept; Y: 2 n, part: grid x (dim + 2) doubles, sync: 8 words; *tmo |= 1 when a
+// grid barrier times out.
+hipError_t launch_gram_colmajor(const double* A, int64_t lda, int64_t m, int64_t n, double* B, hipStream_t s);
+int power_grid_size(int64_t n);
+hipError_t launch_power_grid(const double* A, int64_t lda, int64_t m, int64_t n, double* B, int dim, uint64_t seed,
+                             int iters, double* U, int64_t ldu, double* V, int64_t ldv, double* S, double* Y,
+                             double* part, unsigned* sync, int* kept, int* tmo, hipStream_t s);
 // Iterations per singular value of the reference power method (src/PM.cpp:25-28).
 int power_iterations(int64_t n);
 // SVD<Power> on A (m x LP fp64 panel, n used columns) with B = A^T A (LP x LP, overwritten):

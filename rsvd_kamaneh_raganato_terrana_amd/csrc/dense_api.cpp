@@ -237,6 +237,44 @@ int svd_power(rsvd_handle_t h, int64_t m, int64_t n, const double* A, int64_t ld
     return RSVD_OK;
 }
 
+// SVD<Power> with n > 512: B (n x n), the iterate pair, the grid partials, the barrier words, kept
+struct PowerGridWs {
+    size_t off_B, off_Y, off_part, off_sync, off_kept, total;
+    PowerGridWs(int64_t n, int64_t dim) {
+        size_t o = 0;
+        auto take = [&](size_t bytes) {
+            const size_t at = o;
+            o = align256(o + bytes);
+            return at;
+        };
+        off_B = take(sizeof(double) * (size_t)n * n);
+        off_Y = take(sizeof(double) * 2 * (size_t)n);
+        off_part = take(sizeof(double) * (size_t)power_grid_size(n) * (dim + 2));
+        off_sync = take(8 * sizeof(unsigned));
+        off_kept = take(sizeof(int));
+        total = o;
+    }
+};
+
+int svd_power_grid(rsvd_handle_t h, int64_t m, int64_t n, const double* A, int64_t lda, int dim, uint64_t seed,
+                   double* U, int64_t ldu, double* S, double* V, int64_t ldv, int32_t* kept) {
+    PowerGridWs L(n, dim);
+    RSVD_TRY(prepare(h, L.total));
+    hipStream_t s = h->stream;
+    char* b = h->ws;
+    double* B = reinterpret_cast<double*>(b + L.off_B);
+    int* dk = reinterpret_cast<int*>(b + L.off_kept);
+    RSVD_CK(launch_gram_colmajor(A, lda, m, n, B, s));  // B = A^T A (SVD_class.hpp:193)
+    RSVD_CK(launch_power_grid(A, lda, m, n, B, dim, seed, power_iterations(n), U, ldu, V, ldv, S,
+                              reinterpret_cast<double*>(b + L.off_Y), reinterpret_cast<double*>(b + L.off_part),
+                              reinterpret_cast<unsigned*>(b + L.off_sync), dk, h->dflags + kFlagGramTimeout, s));
+    int k = 0;
+    RSVD_CK(hipMemcpyAsync(&k, dk, sizeof(int), hipMemcpyDeviceToHost, s));
+    RSVD_CK(hipStreamSynchronize(s));
+    *kept = k;
+    return RSVD_OK;
+}
+
 size_t ws_bytes(int64_t rows, int LP, int dtype) {
     return dtype == RSVD_F64 ? DenseWs<double>(rows, LP).total : DenseWs<float>(rows, LP).total;
 }
@@ -267,7 +305,7 @@ int rsvd_svd_workspace_bytes(int64_t m, int64_t n, int32_t dtype, int32_t method
     if (!bytes || m < 1 || n < 1) return RSVD_ERR_INVALID_ARG;
     if (!ok_dtype(dtype)) return RSVD_ERR_UNSUPPORTED;
     if (method == RSVD_SVD_POWER)
-        *bytes = ws_bytes(m, (int)rup(n, 16), RSVD_F64);
+        *bytes = n > 512 ? PowerGridWs(n, std::min(m, n)).total : ws_bytes(m, (int)rup(n, 16), RSVD_F64);
     else
         *bytes = ws_bytes(std::max(m, n), dense_lp(std::min(m, n)), dtype);
     return RSVD_OK;
@@ -326,10 +364,9 @@ int rsvd_svd(rsvd_handle_t h, int64_t m, int64_t n, const void* A, int64_t lda, 
             h->err = "r must be in [0, min(m, n)]";
             return RSVD_ERR_INVALID_ARG;
         }
-        if (n > 512) {
-            h->err = "SVD<Power> is built for n <= 512 (B = A^T A is n x n)";
-            return RSVD_ERR_UNSUPPORTED;
-        }
+        if (n > 512)  // B = A^T A no longer fits one workgroup: the grid power method
+            return svd_power_grid(h, m, n, static_cast<const double*>(A), lda, (int)dim, seed, static_cast<double*>(U),
+                                  ldu, static_cast<double*>(S), static_cast<double*>(V), ldv, kept);
         return svd_power(h, m, n, static_cast<const double*>(A), lda, (int)dim, seed, static_cast<double*>(U), ldu,
                          static_cast<double*>(S), static_cast<double*>(V), ldv, kept);
     }

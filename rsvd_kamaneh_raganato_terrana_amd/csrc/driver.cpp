@@ -410,7 +410,7 @@ static int sync_flags(rsvd_handle_t h, int* flags) {
     for (int w : sticky) RSVD_CK(hipMemsetAsync(h->dflags + w, 0, sizeof(int), h->stream));
     RSVD_CK(hipStreamSynchronize(h->stream));
     if (flags[kFlagGramTimeout]) {
-        h->err = "a Gram reduction timed out waiting for its producers";
+        h->err = "an in-kernel hand-off (Gram reduction / grid barrier) timed out waiting for its producers";
         return RSVD_ERR_HIP;
     }
     if (flags[kFlagJacobiTimeout]) {

@@ -216,6 +216,33 @@ def test_svd_power_matches_oracle(engine, m, n, r):
     assert rel_fro(sign_align(U[:, good], Uo[:, :kk][:, good]), Uo[:, :kk][:, good]) < 1e-8
 
 
+@pytest.mark.parametrize("m,n,r", [(700, 600, 8), (520, 1100, 6)])
+def test_svd_power_large_n_grid(engine, m, n, r):
+    """n > 512: B = A^T A (n x n) no longer fits one workgroup -- the grid power method (row
+    partition of B over the workgroups, src/PM.cpp:31-35) against the same oracle."""
+    k = min(m, n)
+    sig = 2.0 * 0.7 ** np.arange(min(k, 40))
+    A = _spectrum_matrix(m, n, sig, seed=m + n)
+    U, S, V = engine.svd_host(A, 1, r=r, seed=31)
+    Uo, So, Vo = oracle.power_svd(A, r=r, seed=31)
+    assert len(S) == r == len(So)
+    assert rel_fro(S, So) < 1e-10
+    Vcols = Vo[:r, :].T  # the oracle's V_ holds v_i in rows
+    assert rel_fro(sign_align(V, Vcols), Vcols) < 1e-8
+    assert rel_fro(sign_align(U, Uo[:, :r]), Uo[:, :r]) < 1e-8
+
+
+def test_svd_power_large_n_early_stop(engine):
+    """Rank 3 with n = 700: the grid power method stops at sigma < 1e-12 after three triplets
+    (SVD_class.hpp:198-208), like the one-workgroup kernel."""
+    m, n = 800, 700
+    A = _spectrum_matrix(m, n, np.array([3.0, 2.0, 1.0]), seed=4)
+    U, S, V = engine.svd_host(A, 1, r=10, seed=6)
+    Uo, So, Vo = oracle.power_svd(A, r=10, seed=6)
+    assert len(S) == 3 == len(So)
+    assert rel_fro(S, So) < 1e-10
+
+
 def test_svd_class_power_layout_and_early_exit(engine):
     import rsvd_kamaneh_raganato_terrana_amd as R
 
