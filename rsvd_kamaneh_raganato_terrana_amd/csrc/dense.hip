@@ -690,7 +690,7 @@ __global__ __launch_bounds__(kPgThreads) void power_grid_kernel(const double* __
         }
         // u /= sigma; B -= sigma^2 (u.u) v v^T (:210-212) with u.u = 1; V(:, i) = v; S[i] = sigma
         for (int64_t row = a0 + tid; row < a1; row += kPgThreads) U[row + (size_t)i * ldu] /= sigma;
-        const double f = su * vs * vs;  // sigma^2 (u.u) = |A_i v|^2 = su, with v = y0 vs
+        const double f = sigma * sigma * vs * vs;  // sigma^2 (u.u) with u.u = 1, v = y0 vs
         for (int64_t row = b0 + w; row < b1; row += kPgThreads / 64) {
             const double xr = y0[row];
             double* br = B + row * n;
@@ -704,6 +704,230 @@ __global__ __launch_bounds__(kPgThreads) void power_grid_kernel(const double* __
 }
 
 }  // namespace
+
+// ------------------------------------------------------------------------------------------------
+// SVD<ParallelJacobi> with the reference's own iteration (SVD_class.hpp:223-333,
+// JacobiOperations.cpp:120-203): two-sided Jacobi on the d x d triangle W with, per sweep, the
+// list of pairs whose weight W(p,q)^2 + W(q,p)^2 exceeds max(1e-12, 1e-12 maxDiag) (:253-254,
+// 266-282), sorted by decreasing weight (ties by decreasing p, then q: std::greater on the tuple,
+// :286) and applied IN THAT ORDER -- each rotation after the previous one (the _par helpers only
+// parallelise inside a rotation), skipping blocks already diagonal to maxDiag eps (:89-103); the
+// right rotation is dropped when deno = 2|m01| < 1e-10 (:168).  This is a sequential algorithm,
+// so one workgroup runs it: rows / columns of a rotation are updated in parallel, W, Jl, Jr live
+// in global memory (L2), the pair list is built by an atomic counter and bitonic-sorted.  tri > 0
+// (< 0): W is upper (lower) triangular, the other triangle read as exact zeros.  Jl / Jr
+// accumulate the left / right rotations (U = Q_U Jl, V = Q_V Jr are formed afterwards); then the
+// sign fix (:307-312) and the selection sort (:314-330).  W(p, q) = Win[p * sp + q * sq].
+namespace {
+
+constexpr int kPjThreads = 1024;
+
+struct PjEntry {
+    double w;
+    int key;  // p * 65536 + q
+    int pad;
+};
+
+__device__ __forceinline__ bool pj_before(const PjEntry& a, const PjEntry& b) {  // descending (w, p, q)
+    return a.w > b.w || (a.w == b.w && a.key > b.key);
+}
+
+template <typename TI>
+__global__ __launch_bounds__(kPjThreads) void pjacobi_ref_kernel(const TI* __restrict__ Win, int64_t sp, int64_t sq,
+                                                                 int tri, int d, int LP, double* __restrict__ W,
+                                                                 double* __restrict__ Jl, double* __restrict__ Jr,
+                                                                 double* __restrict__ S, PjEntry* __restrict__ list,
+                                                                 int* __restrict__ info) {
+    __shared__ double rot[4];
+    __shared__ double maxd_s;
+    __shared__ int cnt_s, skip_s[2], flag_s;  // skip_s double-buffered: thread 0 writes the next
+                                              // one while slower waves still read this one
+    const int tid = threadIdx.x;
+    for (int e = tid; e < d * d; e += kPjThreads) {
+        const int p = e / d, q = e % d;
+        const bool zero = (tri > 0 && p > q) || (tri < 0 && p < q);  // the triangle's exact zeros
+        W[(int64_t)p * LP + q] = zero ? 0.0 : (double)Win[(int64_t)p * sp + (int64_t)q * sq];
+        Jl[(int64_t)p * LP + q] = (p == q) ? 1.0 : 0.0;
+        Jr[(int64_t)p * LP + q] = (p == q) ? 1.0 : 0.0;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        double md = 0.0;
+        for (int i = 0; i < d; ++i) md = fmax(md, fabs(W[(int64_t)i * LP + i]));
+        maxd_s = md;
+    }
+    __syncthreads();
+    const double eps = 2.220446049250313e-16;
+    int sweeps = 0;
+    for (; sweeps < 200; ++sweeps) {
+        // weights above the threshold (:266-282)
+        if (tid == 0) cnt_s = 0;
+        __syncthreads();
+        const double threshold = fmax(1e-12, 1e-12 * maxd_s);
+        for (int e = tid; e < d * d; e += kPjThreads) {
+            const int p = e / d, q = e % d;
+            if (q < p) {
+                const double a = W[(int64_t)p * LP + q], b = W[(int64_t)q * LP + p];
+                const double wgt = a * a + b * b;
+                if (wgt > threshold) {
+                    const int at = atomicAdd(&cnt_s, 1);
+                    list[at].w = wgt;
+                    list[at].key = p * 65536 + q;
+                }
+            }
+        }
+        __syncthreads();
+        const int cnt = cnt_s;
+        if (cnt == 0) break;
+        // bitonic sort of the first npow2 entries (padding w = -1 sorts last)
+        int np2 = 1;
+        while (np2 < cnt) np2 <<= 1;
+        for (int e = cnt + tid; e < np2; e += kPjThreads) {
+            list[e].w = -1.0;
+            list[e].key = -1;
+        }
+        __syncthreads();
+        for (int kk = 2; kk <= np2; kk <<= 1)
+            for (int j = kk >> 1; j > 0; j >>= 1) {
+                for (int e = tid; e < np2; e += kPjThreads) {
+                    const int x = e ^ j;
+                    if (x > e) {
+                        const PjEntry a = list[e], b = list[x];
+                        const bool up = (e & kk) == 0;  // this run sorted "descending-first"
+                        if (up ? pj_before(b, a) : pj_before(a, b)) {
+                            list[e] = b;
+                            list[x] = a;
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+        // the rotations, in order (:288-303)
+        for (int e = 0; e < cnt; ++e) {
+            const int key = list[e].key, p = key >> 16, q = key & 0xFFFF;
+            if (tid == 0) {
+                const double m00 = W[(int64_t)p * LP + p], m01 = W[(int64_t)p * LP + q];
+                const double m10 = W[(int64_t)q * LP + p], m11 = W[(int64_t)q * LP + q];
+                const double md = maxd_s;
+                const int skip = (fabs(m01) < md * eps && fabs(m10) < md * eps) ? 1 : 0;  // :96-101
+                skip_s[e & 1] = skip;
+                if (!skip) {  // real_2x2_jacobi_svd_par (:140-202)
+                    const double t = m00 + m11, dd = m10 - m01;
+                    double c1 = 1.0, s1 = 0.0;
+                    if (dd != 0.0) {
+                        const double u = t / dd, tmp = sqrt(1.0 + u * u);
+                        s1 = 1.0 / tmp;
+                        c1 = u / tmp;
+                    }
+                    const double n00 = c1 * m00 + s1 * m10, n01 = c1 * m01 + s1 * m11;
+                    const double n11 = -s1 * m01 + c1 * m11;
+                    const double deno = 2.0 * fabs(n01);
+                    double cr = 1.0, sr = 0.0;
+                    if (deno >= 1e-10) {
+                        const double tau = (n00 - n11) / deno, w = sqrt(tau * tau + 1.0);
+                        const double t2 = tau > 0.0 ? 1.0 / (tau + w) : 1.0 / (tau - w);
+                        const double segno = t2 > 0.0 ? 1.0 : -1.0;
+                        const double nn = 1.0 / sqrt(t2 * t2 + 1.0);
+                        sr = -segno * (n01 / fabs(n01)) * fabs(t2) * nn;
+                        cr = nn;
+                    }
+                    rot[0] = c1 * cr + s1 * sr;     // c_left
+                    rot[1] = c1 * (-sr) + s1 * cr;  // s_left
+                    rot[2] = cr;
+                    rot[3] = sr;
+                }
+            }
+            __syncthreads();
+            if (skip_s[e & 1]) continue;  // uniform
+            const double cl = rot[0], sl = rot[1], cr = rot[2], sr = rot[3];
+            for (int i = tid; i < d; i += kPjThreads) {
+                // applyOnTheLeft_par(W, p, q, cl, sl) (:120-128)
+                const double xi = W[(int64_t)p * LP + i], yi = W[(int64_t)q * LP + i];
+                W[(int64_t)p * LP + i] = cl * xi + sl * yi;
+                W[(int64_t)q * LP + i] = -sl * xi + cl * yi;
+                // applyOnTheRight_par(U_, p, q, cl, -sl) (:130-138)
+                const double ui = Jl[(int64_t)i * LP + p], vi = Jl[(int64_t)i * LP + q];
+                Jl[(int64_t)i * LP + p] = cl * ui + sl * vi;
+                Jl[(int64_t)i * LP + q] = -sl * ui + cl * vi;
+            }
+            __syncthreads();
+            for (int i = tid; i < d; i += kPjThreads) {
+                // applyOnTheRight_par(W, p, q, cr, sr); applyOnTheRight_par(V_, p, q, cr, sr)
+                const double xi = W[(int64_t)i * LP + p], yi = W[(int64_t)i * LP + q];
+                W[(int64_t)i * LP + p] = cr * xi - sr * yi;
+                W[(int64_t)i * LP + q] = sr * xi + cr * yi;
+                const double ui = Jr[(int64_t)i * LP + p], vi = Jr[(int64_t)i * LP + q];
+                Jr[(int64_t)i * LP + p] = cr * ui - sr * vi;
+                Jr[(int64_t)i * LP + q] = sr * ui + cr * vi;
+            }
+            __syncthreads();
+            if (tid == 0)  // :298-299
+                maxd_s = fmax(maxd_s, fmax(fabs(W[(int64_t)p * LP + p]), fabs(W[(int64_t)q * LP + q])));
+        }
+        __syncthreads();
+    }
+    // S = |diag|, negative diagonal flips the U column (:307-312)
+    for (int i = tid; i < d; i += kPjThreads) {
+        const double a = W[(int64_t)i * LP + i];
+        S[i] = fabs(a);
+        if (a < 0.0)
+            for (int r = 0; r < d; ++r) Jl[(int64_t)r * LP + i] = -Jl[(int64_t)r * LP + i];
+    }
+    __syncthreads();
+    // selection sort, first maximum (:314-330)
+    for (int i = 0; i < d; ++i) {
+        if (tid == 0) {
+            int pos = i;
+            double mx = S[i];
+            for (int t = i + 1; t < d; ++t)
+                if (S[t] > mx) {
+                    mx = S[t];
+                    pos = t;
+                }
+            flag_s = (mx == 0.0) ? -1 : pos;
+        }
+        __syncthreads();
+        const int pos = flag_s;
+        if (pos < 0) break;
+        if (pos != i) {
+            if (tid == 0) {
+                const double ts = S[i];
+                S[i] = S[pos];
+                S[pos] = ts;
+            }
+            for (int r = tid; r < d; r += kPjThreads) {
+                double x = Jl[(int64_t)r * LP + pos];
+                Jl[(int64_t)r * LP + pos] = Jl[(int64_t)r * LP + i];
+                Jl[(int64_t)r * LP + i] = x;
+                x = Jr[(int64_t)r * LP + pos];
+                Jr[(int64_t)r * LP + pos] = Jr[(int64_t)r * LP + i];
+                Jr[(int64_t)r * LP + i] = x;
+            }
+        }
+        __syncthreads();
+    }
+    if (tid == 0) info[0] = sweeps;
+}
+
+}  // namespace
+
+size_t pjacobi_ref_list_bytes(int d) {
+    int64_t pairs = (int64_t)d * (d - 1) / 2, np2 = 1;
+    while (np2 < pairs) np2 <<= 1;
+    return (size_t)np2 * sizeof(PjEntry);
+}
+
+template <typename TI>
+hipError_t launch_pjacobi_ref(const TI* Win, int64_t sp, int64_t sq, int tri, int d, int LP, double* W, double* Jl,
+                              double* Jr, double* S, void* list, int* info, hipStream_t s) {
+    hipLaunchKernelGGL(pjacobi_ref_kernel<TI>, dim3(1), dim3(kPjThreads), 0, s, Win, sp, sq, tri, d, LP, W, Jl, Jr, S,
+                       reinterpret_cast<PjEntry*>(list), info);
+    return hipGetLastError();
+}
+template hipError_t launch_pjacobi_ref<double>(const double*, int64_t, int64_t, int, int, int, double*, double*, double*,
+                                               double*, void*, int*, hipStream_t);
+template hipError_t launch_pjacobi_ref<float>(const float*, int64_t, int64_t, int, int, int, double*, double*, double*,
+                                              double*, void*, int*, hipStream_t);
 
 hipError_t launch_gram_colmajor(const double* A, int64_t lda, int64_t m, int64_t n, double* B, hipStream_t s) {
     const int64_t nt = (n + 63) / 64;

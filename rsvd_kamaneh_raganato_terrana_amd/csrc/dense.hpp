@@ -40,6 +40,15 @@ int power_grid_size(int64_t n);
 hipError_t launch_power_grid(const double* A, int64_t lda, int64_t m, int64_t n, double* B, int dim, uint64_t seed,
                              int iters, double* U, int64_t ldu, double* V, int64_t ldv, double* S, double* Y,
                              double* part, unsigned* sync, int* kept, int* tmo, hipStream_t s);
+// SVD<ParallelJacobi> with the reference's iteration (weight-sorted sequential two-sided Jacobi,
+// SVD_class.hpp:223-333): W(p, q) = Win[p sp + q sq] (d x d; tri > 0 / < 0: upper / lower
+// triangular) copied to W (LP pitch); Jl / Jr (LP x
+// LP row-major) accumulate the left / right rotations; S (d) sorted descending with Jl / Jr columns
+// permuted alike; info[0] = sweeps.  list: pjacobi_ref_list_bytes(d) of scratch.  One workgroup.
+size_t pjacobi_ref_list_bytes(int d);
+template <typename TI>
+hipError_t launch_pjacobi_ref(const TI* Win, int64_t sp, int64_t sq, int tri, int d, int LP, double* W, double* Jl,
+                              double* Jr, double* S, void* list, int* info, hipStream_t s);
 // Iterations per singular value of the reference power method (src/PM.cpp:25-28).
 int power_iterations(int64_t n);
 // SVD<Power> on A (m x LP fp64 panel, n used columns) with B = A^T A (LP x LP, overwritten):

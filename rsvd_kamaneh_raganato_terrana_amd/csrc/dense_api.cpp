@@ -16,8 +16,11 @@
 // preconditions a rectangular A (Householder) and runs two-sided Jacobi on the min(m,n)^2
 // triangle.  Here: P = A (m >= n) or A^T (m < n) as a row-major panel, Q_P = orth(P) as above,
 // W = Q_P^T P (cross Gram), the one-sided Jacobi small SVD of the wide engine (jacobi.hip for
-// min(m,n) <= 64, the block Jacobi of wide_svd.hip up to 512): P = (Q_P U_w) S V_w^T.  Both
-// reference methods converge to the same SVD, so both map here.
+// min(m,n) <= 64, the block Jacobi of wide_svd.hip up to 512): P = (Q_P U_w) S V_w^T -- the
+// converged SVD, which is what the reference's Jacobi (cyclic, stop at 2 eps maxDiag) returns.
+// ParallelJacobi stops at the ABSOLUTE weight 1e-12 (off-diagonals up to ~1e-6 survive), so its
+// vectors depend on the rotation order; it runs the reference's own order here (dense.hip
+// pjacobi_ref_kernel: weight-sorted, sequential, one workgroup) on W = R_P / R_P^T / A (square).
 //
 // SVD<Power> (SVD_class.hpp:183-219, src/PM.cpp:4-81): B = A^T A by the fp64 Gram kernel, then
 // the power method with deflation in one workgroup (dense.hip power_svd_kernel).
@@ -179,20 +182,35 @@ int qr_typed(rsvd_handle_t h, int64_t m, int64_t n, const T* A, int64_t lda, int
 
 template <typename T>
 int svd_jacobi_typed(rsvd_handle_t h, int64_t m, int64_t n, const T* A, int64_t lda, T* U, int64_t ldu, T* S, T* V,
-                     int64_t ldv) {
+                     int64_t ldv, bool reference_order) {
     const bool tall = m >= n;
     const int64_t k = std::min(m, n), rows = std::max(m, n);
     DenseWs<T> L(rows, dense_lp(k));
     RSVD_TRY(prepare(h, L.total));
     DenseEngine<T> E(h, L);
     hipStream_t s = h->stream;
+    if (reference_order && m == n) {  // square: Jacobi on A itself (SVD_class.hpp:246-249), U = Jl, V = Jr
+        RSVD_CK(launch_pjacobi_ref<T>(A, 1, lda, 0, (int)k, L.LP, E.W, E.Uw, E.Vw, E.Sd, E.JX, h->dflags + 1, s));
+        RSVD_CK(launch_convert_scale<T>(E.Sd, S, (int)k, 1.0, s));
+        if (sizeof(T) == 4) {
+            const int L2 = L.LP * L.LP;
+            RSVD_CK(launch_convert_scale<float>(E.Uw, E.Uw32, L2, 1.0, s));
+            RSVD_CK(launch_convert_scale<float>(E.Vw, E.Vw32, L2, 1.0, s));
+        }
+        RSVD_CK(launch_panel_to_colmajor<T>(E.mat(E.Uw, E.Uw32), k, (int)k, L.LP, U, ldu, s));
+        RSVD_CK(launch_panel_to_colmajor<T>(E.mat(E.Vw, E.Vw32), k, (int)k, L.LP, V, ldv, s));
+        return RSVD_OK;
+    }
     if (tall)
         RSVD_CK(launch_colmajor_to_panel<T>(A, lda, m, (int)n, L.LP, E.P, s));
     else
         RSVD_CK(launch_transpose_to_panel<T>(A, lda, m, n, L.LP, E.P, s));
     RSVD_TRY(E.orth(E.P, (int)k, 0x5BDull + (uint64_t)rows));
     RSVD_CK(launch_gram_wide<T>(E.P, E.Q, rows, L.LP, L.gx, E.gslab, E.R1, nullptr, s));  // R1 = P^T Q = R_P^T
-    if (L.LP <= 64)
+    if (reference_order)  // W = R_P (tall) or R_P^T (wide, SVD_class.hpp:230-245) in R1 = R_P^T
+        RSVD_CK(launch_pjacobi_ref<double>(E.R1, tall ? 1 : L.LP, tall ? L.LP : 1, tall ? 1 : -1, (int)k, L.LP, E.W, E.Uw, E.Vw, E.Sd,
+                                           E.JX, h->dflags + 1, s));
+    else if (L.LP <= 64)
         RSVD_CK(launch_small_svd<double>(E.R1, (int)k, L.LP, E.Uw, E.Vw, E.Sd, h->dflags + 1, s));
     else
         RSVD_CK(launch_block_jacobi<double>(E.R1, (int)k, L.LP, E.JX, E.JJ, E.Uw, E.Vw, E.Sd, E.sync, h->dflags + 1, s));
@@ -204,13 +222,16 @@ int svd_jacobi_typed(rsvd_handle_t h, int64_t m, int64_t n, const T* A, int64_t 
     }
     const T* Uwt = E.mat(E.Uw, E.Uw32);
     const T* Vwt = E.mat(E.Vw, E.Vw32);
-    // P = (Q U_w) S V_w^T;  A = P (tall) or P^T (wide)
+    // P = (Q U_w) S V_w^T;  A = P (tall) or P^T (wide).  Reference order: W = Jl S Jr^T with W = R_P
+    // (tall: A = (Q Jl) S Jr^T) or W = R_P^T (wide: A = Jl S (Q Jr)^T)
     T* left = tall ? U : V;
     const int64_t ldl = tall ? ldu : ldv;
     T* right = tall ? V : U;
     const int64_t ldr = tall ? ldv : ldu;
-    RSVD_CK(launch_panel_gemm<T>(E.Q, rows, L.LP, Uwt, 0, left, ldl, (int)k, nullptr, nullptr, nullptr, s));
-    RSVD_CK(launch_panel_to_colmajor<T>(Vwt, k, (int)k, L.LP, right, ldr, s));
+    const T* Qside = (reference_order && !tall) ? Vwt : Uwt;
+    const T* Kside = (reference_order && !tall) ? Uwt : Vwt;
+    RSVD_CK(launch_panel_gemm<T>(E.Q, rows, L.LP, Qside, 0, left, ldl, (int)k, nullptr, nullptr, nullptr, s));
+    RSVD_CK(launch_panel_to_colmajor<T>(Kside, k, (int)k, L.LP, right, ldr, s));
     return RSVD_OK;
 }
 
@@ -375,11 +396,12 @@ int rsvd_svd(rsvd_handle_t h, int64_t m, int64_t n, const void* A, int64_t lda, 
         return RSVD_ERR_UNSUPPORTED;
     }
     *kept = (int32_t)k;
+    const bool ref_order = method == RSVD_SVD_PARALLEL_JACOBI;
     if (dtype == RSVD_F64)
         return svd_jacobi_typed<double>(h, m, n, static_cast<const double*>(A), lda, static_cast<double*>(U), ldu,
-                                        static_cast<double*>(S), static_cast<double*>(V), ldv);
+                                        static_cast<double*>(S), static_cast<double*>(V), ldv, ref_order);
     return svd_jacobi_typed<float>(h, m, n, static_cast<const float*>(A), lda, static_cast<float*>(U), ldu,
-                                   static_cast<float*>(S), static_cast<float*>(V), ldv);
+                                   static_cast<float*>(S), static_cast<float*>(V), ldv, ref_order);
 }
 
 int rsvd_qr_host_f64(rsvd_handle_t h, int64_t m, int64_t n, const double* A, int64_t lda, int32_t full, double* Q,

@@ -135,20 +135,13 @@ def test_qr_reduced_rejects_wide(engine):
 
 # ---- SVD<Jacobi> / SVD<ParallelJacobi> ------------------------------------------------------------
 @pytest.mark.parametrize("m,n", [(200, 50), (50, 200), (64, 64), (300, 150), (90, 400), (700, 320)])
-@pytest.mark.parametrize("method", [0, 2])
-def test_svd_jacobi_f64_matches_oracle(engine, m, n, method):
+def test_svd_jacobi_f64_matches_oracle(engine, m, n):
+    """SVD<Jacobi>: the converged SVD (the reference stops at 2 eps maxDiag, SVD_class.hpp:132-155)."""
     k = min(m, n)
     sig = 0.97 ** np.arange(k) + 0.01
     A = _spectrum_matrix(m, n, sig, seed=m * 7 + n)
-    U, S, V = engine.svd_host(A, method)
+    U, S, V = engine.svd_host(A, 0)
     Uo, So, Vo, _ = oracle.jacobi_svd(A)
-    if method == 2:
-        # the reference's ParallelJacobi stops at absolute thresholds 1e-12 (SVD_class.hpp:253-254):
-        # measured against its own Jacobi on these inputs it is 1e-11 .. 4e-8 off in S and
-        # 2e-5 .. 2.6e-2 in U, V.  Both methods here return the converged SVD, checked tightly
-        # against the Jacobi oracle below; against ParallelJacobi only S is comparable.
-        _, Sp, _, _ = oracle.jacobi_svd(A, parallel=True)
-        assert rel_fro(S, Sp) < 1e-7
     assert U.shape == (m, k) and S.shape == (k,) and V.shape == (n, k)
     assert np.all(np.diff(S) <= 0)
     assert rel_fro(S, So) < 1e-12
@@ -157,6 +150,36 @@ def test_svd_jacobi_f64_matches_oracle(engine, m, n, method):
     assert _orth_err(U) < 1e-12 and _orth_err(V) < 1e-12
     # the block Jacobi (k > 64) stops at |g| <= k eps sqrt(a b) per pair (wide_svd.hip)
     assert rel_fro((U * S) @ V.T, A) < (1e-13 if k <= 64 else 1e-12)
+
+
+@pytest.mark.parametrize("m,n", [(200, 50), (50, 200), (64, 64), (300, 150), (90, 400), (24, 24), (700, 320)])
+def test_svd_parallel_jacobi_matches_oracle(engine, m, n):
+    """SVD<ParallelJacobi>: the reference's own iteration (weight-sorted sequential rotations,
+    absolute weight stop 1e-12, SVD_class.hpp:223-333) against oracle.jacobi_svd(parallel=True).
+    Off-diagonals up to ~1e-6 survive that stop, so the vectors depend on the rotation path and
+    differ from the converged SVD by 2e-5 .. 2.6e-2 on these inputs; the GPU runs the same path.
+    Tolerance: north_star's 1e-4 on the leading half of U, V; S at 1e-10.
+    (700, 320): its 320 singular values cluster at 0.01 + 0.97^i, and the reference's result is
+    unstable under rounding there -- the oracle on the same A, preconditioned by numpy's
+    Householder QR instead of its own, moves the leading half by 5.2e-4 (and S by 5e-8).  For that
+    case the bound is the reference's own spread: 2e-3 on vectors, 2e-7 on S."""
+    k = min(m, n)
+    sig = 0.97 ** np.arange(k) + 0.01
+    A = _spectrum_matrix(m, n, sig, seed=m * 7 + n)
+    U, S, V = engine.svd_host(A, 2)
+    Up, Sp, Vp, _ = oracle.jacobi_svd(A, parallel=True)
+    chaotic = (m, n) == (700, 320)
+    h = k // 2
+    assert U.shape == (m, k) and S.shape == (k,) and V.shape == (n, k)
+    assert np.all(np.diff(S) <= 0)
+    assert rel_fro(S, Sp) < (2e-7 if chaotic else 1e-10)
+    vt = 2e-3 if chaotic else 1e-4
+    assert rel_fro(sign_align(U[:, :h], Up[:, :h]), Up[:, :h]) < vt
+    assert rel_fro(sign_align(V[:, :h], Vp[:, :h]), Vp[:, :h]) < vt
+    if not chaotic:  # the full factors follow the same path
+        assert rel_fro(sign_align(U, Up), Up) < 1e-6
+        assert rel_fro(sign_align(V, Vp), Vp) < 1e-6
+    assert _orth_err(U) < 1e-12 and _orth_err(V) < 1e-12
 
 
 def test_svd_identity_inputs(engine):
@@ -177,6 +200,36 @@ def test_svd_rank_deficient(engine):
     assert S[2] < 1e-9 * S[0]
     assert _orth_err(U) < 1e-12 and _orth_err(V) < 1e-12
     assert rel_fro((U * S) @ V.T, A) < 1e-13
+
+
+def test_svd_parallel_jacobi_rank_deficient(engine):
+    """tests/svd_test.cpp's SVD<ParallelJacobi> case on input/sparse_matrix.mtx (rank 2, square:
+    Jacobi on A itself, no preconditioning)."""
+    i, j = np.meshgrid(np.arange(100), np.arange(100), indexing="ij")
+    A = np.asfortranarray(100.0 * i + j + 1)
+    U, S, V = engine.svd_host(A, 2)
+    Up, Sp, Vp, _ = oracle.jacobi_svd(A, parallel=True)
+    assert rel_fro(S[:2], Sp[:2]) < 1e-12 and S[2] < 1e-9 * S[0]
+    # sigma_2 / sigma_1 = 2.5e-3 and the stop leaves off-diagonals ~1e-3: the second pair moves at 4e-9
+    assert rel_fro(sign_align(U[:, :2], Up[:, :2]), Up[:, :2]) < 1e-7
+    assert rel_fro(sign_align(V[:, :2], Vp[:, :2]), Vp[:, :2]) < 1e-7
+    assert _orth_err(U) < 1e-12 and _orth_err(V) < 1e-12
+    assert rel_fro((U * S) @ V.T, A) < 1e-8  # the oracle's own: 3.7e-9
+
+
+def test_svd_parallel_jacobi_f32_device(engine):
+    import torch
+
+    m, n = 90, 400
+    sig = 0.97 ** np.arange(m) + 0.01
+    A = _spectrum_matrix(m, n, sig, seed=m * 7 + n).astype(np.float32)
+    U, S, V = engine.svd(torch.from_numpy(A).cuda(), 2)
+    U, S, V = (x.cpu().double().numpy() for x in (U, S, V))
+    Up, Sp, Vp, _ = oracle.jacobi_svd(A.astype(np.float64), parallel=True)
+    h = m // 2
+    assert rel_fro(S, Sp) < 1e-5
+    assert rel_fro(sign_align(U[:, :h], Up[:, :h]), Up[:, :h]) < 1e-4
+    assert rel_fro(sign_align(V[:, :h], Vp[:, :h]), Vp[:, :h]) < 1e-4
 
 
 def test_svd_f32_device(engine):
@@ -225,7 +278,8 @@ def test_svd_power_large_n_grid(engine, m, n, r):
     A = _spectrum_matrix(m, n, sig, seed=m + n)
     U, S, V = engine.svd_host(A, 1, r=r, seed=31)
     Uo, So, Vo = oracle.power_svd(A, r=r, seed=31)
-    assert len(S) == r == len(So)
+    So = So[:r]  # the oracle's S_ keeps min(m, n) slots, zeros past r
+    assert len(S) == r and np.all(S > 0)
     assert rel_fro(S, So) < 1e-10
     Vcols = Vo[:r, :].T  # the oracle's V_ holds v_i in rows
     assert rel_fro(sign_align(V, Vcols), Vcols) < 1e-8
