@@ -30,6 +30,9 @@ struct WProjPlan {
     int blocks;      // output row blocks
     bool v2;         // LDS-DMA pipelined kernel (bf16 / e4m3 A, LP >= 128, 16-B aligned columns)
     bool ds = false; // v2 TN at LP = 128 with two k-steps per stage (128-B A runs; K a multiple of 64)
+    bool v3 = false; // v2 with launch-constant LDS read bases (bf16 A, LP 256 / 512; wide_proj.hip)
+    bool m32 = false; // v3 on v_mfma_f32_32x32x16_bf16 instead of 16x16x32
+    int abl = 0;      // lab-only ablations of the v3 kernel (tools/wide_lab.cpp), never set by the engine
 };
 // v2 requires: a 16-B aligned base, bf16 A with lda and m multiples of 8 or e4m3 A with lda and m
 // multiples of 16, and S panels zero-padded

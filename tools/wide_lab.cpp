@@ -246,9 +246,10 @@ __global__ void fill_random_kernel(uint16_t* p, size_t n16, int fp8) {
     }
 }
 
-static void bench_proj() {
+static void bench_proj(bool c4only = false) {
     struct Case { int64_t m, n; int LP; int fp8; };
     for (Case c : {Case{1 << 20, 1024, 128, 0}, Case{65536, 65536, 256, 0}, Case{131072, 8192, 512, 1}}) {
+        if (c4only && c.LP != 256) continue;
         const size_t esz = c.fp8 ? 1 : 2;
         void* A;
         CK(hipMalloc(&A, (size_t)c.m * c.n * esz));
@@ -259,8 +260,11 @@ static void bench_proj() {
         bf16_t* Sl = dev_random<bf16_t>((size_t)mx * c.LP);
         float* Out;
         CK(hipMalloc(&Out, (size_t)mx * c.LP * 4));
-        for (int v2 = 0; v2 < 2; ++v2) {
-            WProjPlan pnn = plan_wproj(c.m, c.n, c.LP, v2), ptn = plan_wproj(c.n, c.m, c.LP, v2, false, c.fp8);
+        for (int v2 = c4only ? 1 : 0; v2 < 4; ++v2) {
+            WProjPlan pnn = plan_wproj(c.m, c.n, c.LP, v2 > 0), ptn = plan_wproj(c.n, c.m, c.LP, v2 > 0, false, c.fp8);
+            if (v2 == 1) pnn.v3 = ptn.v3 = false;
+            if (v2 >= 2 && !pnn.v3 && !ptn.v3) continue;
+            pnn.m32 = ptn.m32 = (v2 == 3);
             float* slabs;
             CK(hipMalloc(&slabs, (size_t)std::max<int64_t>(pnn.splits * c.m, ptn.splits * c.n) * c.LP * 4));
             const double bytes = (double)c.m * c.n * esz, fl = 2.0 * c.m * c.n * c.LP;
@@ -269,7 +273,7 @@ static void bench_proj() {
             double t3 = time_us([&] { CK(launch_wproj(0, c.fp8, A, c.m, c.m, c.n, Sh, Sl, c.LP, ptn, slabs, Out, S)); });
             printf("proj%s m=%ld n=%ld LP=%d fp8=%d: NN1 %.1f us (%.0f GB/s) NN2 %.1f us (%.0f GB/s, %.0f TF) TN2 %.1f us"
                    " (%.0f GB/s, %.0f TF) splits nn=%d tn=%d\n",
-                   v2 ? "v2" : "v1", (long)c.m, (long)c.n, c.LP, c.fp8, t1, bytes / t1 / 1e3, t2, bytes / t2 / 1e3,
+                   v2 == 3 ? "v3m32" : (v2 == 2 ? "v3" : (v2 ? "v2" : "v1")), (long)c.m, (long)c.n, c.LP, c.fp8, t1, bytes / t1 / 1e3, t2, bytes / t2 / 1e3,
                    2 * fl / t2 / 1e6, t3, bytes / t3 / 1e3, 2 * fl / t3 / 1e6, pnn.splits, ptn.splits);
             CK(hipFree(slabs));
         }
@@ -328,7 +332,7 @@ static uint16_t f2bf_h(float x) {
 static void check_proj() {  // v2 (LDS-DMA) against v1 on random bf16 / e4m3 data
     for (int fp8 = 0; fp8 < 2; ++fp8)
     for (int LP : {128, 256, 512}) {
-        const int64_t m = 2048 + 64 + 16 * fp8, n = 1024 + 32 + 3 * fp8;
+        const int64_t m = 2048 + 72 - 8 * fp8, n = 1024 + 40 - 5 * fp8;  // ragged: K tails of 8 / 24 rows
         std::vector<uint16_t> hA((size_t)m * n), hS((size_t)std::max(m, n) * LP), hL(hS.size());
         std::mt19937 g(7);
         std::normal_distribution<float> d;
@@ -367,7 +371,9 @@ static void check_proj() {  // v2 (LDS-DMA) against v1 on random bf16 / e4m3 dat
             CK(hipMemcpy(Sl, hL.data(), rows_s * LP * 2, hipMemcpyHostToDevice));
             const int64_t ro = nn ? m : n, K = nn ? n : m;
             WProjPlan p1 = plan_wproj(ro, K, LP, false, nn, fp8), p2 = plan_wproj(ro, K, LP, true, nn, fp8);
-            {
+            for (int m32 = 0; m32 < 2; ++m32) {
+            p2.m32 = m32;
+            if (m32 && !p2.v3) continue;
             CK(launch_wproj(nn, fp8, A, m, m, n, Sh, Sl, LP, p1, sl, O1, S));
             CK(launch_wproj(nn, fp8, A, m, m, n, Sh, Sl, LP, p2, sl, O2, S));
             CK(hipStreamSynchronize(S));
@@ -379,8 +385,8 @@ static void check_proj() {  // v2 (LDS-DMA) against v1 on random bf16 / e4m3 dat
                 md = std::max(md, (double)fabs(a[i] - b[i]));
                 mx2 = std::max(mx2, (double)fabs(a[i]));
             }
-            printf("check fp8=%d LP=%d %s: max|v1-v2| = %.3e (max|v1| = %.3e) v2 splits=%d chunk=%ld\n",
-                   fp8, LP, nn ? "NN" : "TN", md, mx2, p2.splits, (long)p2.chunk);
+            printf("check fp8=%d LP=%d %s%s: max|v1-v2| = %.3e (max|v1| = %.3e) v2 splits=%d chunk=%ld\n",
+                   fp8, LP, nn ? "NN" : "TN", m32 ? " m32" : (p2.v3 ? " v3" : ""), md, mx2, p2.splits, (long)p2.chunk);
             }
         }
         CK(hipFree(A)); CK(hipFree(Sh)); CK(hipFree(Sl)); CK(hipFree(O1)); CK(hipFree(O2)); CK(hipFree(sl));
@@ -491,6 +497,27 @@ int main(int argc, char** argv) {
     if (what == "all" || what == "chol") bench_chol();
     if (what == "all" || what == "jac") bench_jac();
     if (what == "all" || what == "proj") bench_proj();
+    if (what == "proj4") bench_proj(true);
+    if (what == "abl") {  // v3 ablations at C4 (timing only; results meaningless)
+        const int64_t m = 65536, n = 65536;
+        const int LP = 256;
+        void* A;
+        CK(hipMalloc(&A, (size_t)m * n * 2));
+        hipLaunchKernelGGL(fill_random_kernel, dim3(4096), dim3(256), 0, S, (uint16_t*)A, (size_t)m * n, 0);
+        bf16_t* Sh = dev_random<bf16_t>((size_t)m * LP);
+        bf16_t* Sl = dev_random<bf16_t>((size_t)m * LP);
+        float* Out;
+        CK(hipMalloc(&Out, (size_t)m * LP * 4));
+        const double fl = 4.0 * m * n * LP;
+        for (int ab = 0; ab < 8; ++ab) {
+            WProjPlan pn = plan_wproj(m, n, LP, true), pt = plan_wproj(n, m, LP, true, false, false);
+            pn.abl = pt.abl = ab;
+            double t1 = time_us([&] { CK(launch_wproj(1, 0, A, m, m, n, Sh, Sl, LP, pn, nullptr, Out, S)); });
+            double t2 = time_us([&] { CK(launch_wproj(0, 0, A, m, m, n, Sh, Sl, LP, pt, nullptr, Out, S)); });
+            printf("abl %d (%s%s%s): NN2 %.1f us (%.0f TF)  TN2 %.1f us (%.0f TF)\n", ab, ab & 1 ? "nobar " : "",
+                   ab & 2 ? "nodma " : "", ab & 4 ? "nolds" : "", t1, fl / t1 / 1e6, t2, fl / t2 / 1e6);
+        }
+    }
     if (what == "all" || what == "check") check_proj();
     if (what == "probe") probe_glds();
     if (what == "s8") check_s8();
