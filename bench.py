@@ -13,8 +13,10 @@ Configurations (BASELINE.json "configs"; --config, default c4):
   c5  131072 x 8192 e4m3 (per-tensor scale), l = 512, q = 2       (configs[4])
 Scaling over N GPUs (torchrun, one process per GPU, RCCL): c2 / c3 are weak-scaled (each rank
 owns m rows, the global matrix is N m x n); c4 / c5 are strong-scaled (the global m x n matrix is
-row-partitioned, src/rSVD.cpp:20-23).  The n-side panels are summed with all_reduce and
-orthonormalised redundantly, U stays row-sharded.
+row-partitioned, src/rSVD.cpp:20-23).  The n side is sharded as well (rsvd_set_collectives):
+A^T Q is reduce-scattered, each rank orthonormalises its n/N rows (Gram all-reduced), the next
+skinny operand and V are all-gathered; U stays row-sharded.  Only the l x l small SVD is
+replicated.
 value = whole-job algorithmic TFLOP/s (F_proj + F_qr + F_small of the global
 problem) / max-over-ranks wall time; ms_per_step = rSVD wall-clock.
 
@@ -299,6 +301,8 @@ def main():
 
     if rank == 0:
         par = "single-gpu" if world == 1 else (f"row-partition x{world}" if strong else f"row-shard x{world}")
+        if world > 1 and info.get("n_shard_rows"):
+            par += f", n side sharded ({info['n_shard_rows']} rows/GPU)"
         line = {
             "metric": "rSVD wall-clock + achieved TFLOP/s, dense m x n rank-k",
             "value": value,

@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define RSVD_ABI_VERSION 4
+#define RSVD_ABI_VERSION 5
 
 typedef enum {
     RSVD_OK = 0,
@@ -93,6 +93,7 @@ typedef struct {
     int32_t jacobi_sweeps;     /* sweeps of the small SVD                                      */
     int32_t splits_nn, splits_tn; /* K splits chosen for the projections                         */
     int32_t power_kept;        /* SVDMethod::Power: triplets found before sigma < 1e-12 (else 0)  */
+    int32_t n_shard_rows;      /* n-side rows per rank of a sharded n side (ABI 5), 0: replicated */
 } rsvd_info_t;
 
 typedef struct rsvd_handle_s *rsvd_handle_t;
@@ -101,6 +102,18 @@ typedef struct rsvd_handle_s *rsvd_handle_t;
  * ranks, in place, ordered after the work already enqueued on `stream`.  Return 0 on success.
  * (The Python front end binds it to torch.distributed.all_reduce over RCCL.) */
 typedef int (*rsvd_allreduce_fn)(void *buf, int64_t count, int32_t dtype, void *stream, void *user);
+
+/* Collective hook of the n-side sharding (ABI 5).  op RSVD_COLL_REDUCE_SCATTER: `send` holds
+ * world x count elements, rank r receives the sum over ranks of elements [r count, (r + 1) count)
+ * in `recv` (recv may alias send + rank count, in place).  op RSVD_COLL_ALL_GATHER: every rank
+ * contributes `count` elements at `send` and receives all world x count, rank r's at
+ * recv + r count (send may alias recv + rank count).  dtype: RSVD_F64, RSVD_F32 or RSVD_BF16.
+ * Ordered after the work enqueued on `stream`; return 0 on success.  (The Python front end binds
+ * it to torch.distributed.reduce_scatter_tensor / all_gather_into_tensor over RCCL.) */
+typedef int (*rsvd_collective_fn)(int32_t op, void *send, void *recv, int64_t count, int32_t dtype, void *stream,
+                                  void *user);
+#define RSVD_COLL_REDUCE_SCATTER 1
+#define RSVD_COLL_ALL_GATHER 2
 
 const char *rsvd_status_string(int status);
 int rsvd_abi_version(void);
@@ -121,6 +134,14 @@ int rsvd_get_info(rsvd_handle_t h, rsvd_info_t *info);
 /* Row-sharded runs: this handle owns rows [offset, offset + m_local) of a global m x n A; the
  * hook sums the n x l partial products A_g^T Q_g and the l x l Grams across ranks. */
 int rsvd_set_comm(rsvd_handle_t h, int rank, int world, rsvd_allreduce_fn fn, void *user);
+/* Optional (ABI 5), after rsvd_set_comm: with a collective hook the wide engine (bf16 / e4m3 A,
+ * or l > 64) also shards the n side -- rank r owns rows [r c, (r + 1) c) of the
+ * n x l panels, c = n / world rounded up to 32: A^T Q is reduce-scattered instead of all-reduced,
+ * each rank orthonormalises its rows (CholeskyQR with the l x l Gram all-reduced), the next
+ * skinny operand and the final V are all-gathered.  fn = NULL switches back to the replicated
+ * n side.  SVDMethod::Power runs keep the replicated n side.  rsvd_workspace_bytes covers the
+ * padded n-side panels of any world up to 64. */
+int rsvd_set_collectives(rsvd_handle_t h, rsvd_collective_fn fn, void *user);
 
 /* Row partition of src/rSVD.cpp:20-23 / src/PM.cpp:31-35: rows of rank `rank` out of `world`.
  * Host-only arithmetic (no device needed).  Returns the local row count, *offset = first row. */

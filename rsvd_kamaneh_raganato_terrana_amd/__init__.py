@@ -16,6 +16,7 @@ from .api import (  # noqa: F401
     generateOmega,
     intermediate_step,
     make_allreduce_hook,
+    make_collective_hook,
     qr_decomposition_full,
     qr_decomposition_reduced,
     rSVD,
@@ -24,7 +25,8 @@ from .api import (  # noqa: F401
 
 __all__ = [
     "build", "row_partition", "RSVDError", "Engine", "QRMode", "SVDMethod", "colmajor",
-    "default_engine", "empty_colmajor", "generateOmega", "intermediate_step", "make_allreduce_hook", "rSVD",
+    "default_engine", "empty_colmajor", "generateOmega", "intermediate_step", "make_allreduce_hook",
+    "make_collective_hook", "rSVD",
     "rSVD_image_compression",
     "SVD", "qr_decomposition_full", "qr_decomposition_reduced",
 ]

@@ -33,7 +33,7 @@ QR_AUTO, QR_GS2, QR_CHOLQR2 = 0, 1, 2
 # Every symbol include/rsvd_c.h declares (checked by tests/test_capi_exports.py).
 EXPORTS = (
     "rsvd_status_string", "rsvd_abi_version", "rsvd_create", "rsvd_destroy", "rsvd_set_stream",
-    "rsvd_last_error", "rsvd_sync", "rsvd_get_info", "rsvd_set_comm", "rsvd_row_partition",
+    "rsvd_last_error", "rsvd_sync", "rsvd_get_info", "rsvd_set_comm", "rsvd_set_collectives", "rsvd_row_partition",
     "rsvd_workspace_bytes", "rsvd_set_workspace", "rsvd_set_timing", "rsvd_get_timing", "rsvd_run", "rsvd_range_finder",
     "rsvd_generate_omega", "rsvd_run_host_f64", "rsvd_range_finder_host_f64",
     "rsvd_generate_omega_host_f64", "rsvd_qr", "rsvd_svd", "rsvd_qr_workspace_bytes",
@@ -54,6 +54,7 @@ class Info(ctypes.Structure):
     _fields_ = [
         ("cholqr_fallbacks", ctypes.c_int32), ("jacobi_sweeps", ctypes.c_int32),
         ("splits_nn", ctypes.c_int32), ("splits_tn", ctypes.c_int32), ("power_kept", ctypes.c_int32),
+        ("n_shard_rows", ctypes.c_int32),
     ]
 
 
@@ -67,6 +68,10 @@ class Timing(ctypes.Structure):
 
 ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int32,
                                 ctypes.c_void_p, ctypes.c_void_p)
+# rsvd_collective_fn(op, send, recv, count, dtype, stream, user) -- ABI 5
+COLLECTIVE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                 ctypes.c_int32, ctypes.c_void_p, ctypes.c_void_p)
+COLL_REDUCE_SCATTER, COLL_ALL_GATHER = 1, 2
 
 
 def _sources():
@@ -137,6 +142,7 @@ def lib():
     L.rsvd_sync.argtypes = [vp]
     L.rsvd_get_info.argtypes = [vp, ctypes.POINTER(Info)]
     L.rsvd_set_comm.argtypes = [vp, ctypes.c_int, ctypes.c_int, ALLREDUCE_FN, vp]
+    L.rsvd_set_collectives.argtypes = [vp, COLLECTIVE_FN, vp]
     L.rsvd_row_partition.restype = i64
     L.rsvd_row_partition.argtypes = [i64, ctypes.c_int, ctypes.c_int, ctypes.POINTER(i64)]
     L.rsvd_workspace_bytes.argtypes = [ctypes.POINTER(Desc), ctypes.POINTER(ctypes.c_size_t)]

@@ -97,6 +97,69 @@ def make_allreduce_hook(get_buffer, group=None):
     return _capi.ALLREDUCE_FN(_hook)
 
 
+def make_collective_hook(get_buffer, group=None):
+    """The C ABI's rsvd_collective_fn (include/rsvd_c.h, ABI 5) over torch.distributed: the
+    reduce-scatter of A^T Q and the all-gathers of the next skinny operand and of V that the
+    n-side sharding needs.  Like the all-reduce hook it only ever touches
+    slices of the handle's workspace and returns non-zero instead of raising through C.  RCCL
+    ("nccl") runs reduce_scatter_tensor / all_gather_into_tensor in place; a backend without them
+    (gloo) gets the same result from one all_reduce (reduce-scatter: sum everything, keep this
+    rank's chunk; all-gather: zero the other chunks, sum)."""
+    torch = _torch()
+    import torch.distributed as dist
+
+    sizes = {_capi.F64: (torch.float64, 8), _capi.F32: (torch.float32, 4), _capi.BF16: (torch.bfloat16, 2)}
+
+    def _hook(op, send, recv, count, dtype, stream, user):
+        try:
+            ws = get_buffer()
+            if ws is None or send is None or recv is None or dtype not in sizes or count < 0:
+                return 1
+            tdt, esz = sizes[dtype]
+            world = dist.get_world_size(group)
+            rank = dist.get_rank(group)
+            base = ws.data_ptr()
+
+            def view(ptr, n):
+                off = ptr - base
+                if off < 0 or off % esz or off + n * esz > ws.numel():
+                    raise ValueError("slice outside the workspace")
+                return ws[off: off + n * esz].view(tdt)
+
+            if op == _capi.COLL_REDUCE_SCATTER:
+                full, part = view(send, world * count), view(recv, count)
+                if dist.get_backend(group) == "nccl":
+                    dist.reduce_scatter_tensor(part, full, op=dist.ReduceOp.SUM, group=group)
+                else:
+                    dist.all_reduce(full, op=dist.ReduceOp.SUM, group=group)
+                    if recv != send + rank * count * esz:
+                        part.copy_(full[rank * count:(rank + 1) * count])
+                return 0
+            if op == _capi.COLL_ALL_GATHER:
+                full, part = view(recv, world * count), view(send, count)
+                if dist.get_backend(group) == "nccl":
+                    dist.all_gather_into_tensor(full, part, group=group)
+                else:
+                    mine = full[rank * count:(rank + 1) * count]
+                    if send != recv + rank * count * esz:
+                        mine.copy_(part)
+                    keep = mine.clone()
+                    full.zero_()
+                    mine.copy_(keep)
+                    if tdt == torch.bfloat16:  # exact: every element is non-zero on one rank only
+                        f = full.float()
+                        dist.all_reduce(f, op=dist.ReduceOp.SUM, group=group)
+                        full.copy_(f)
+                    else:
+                        dist.all_reduce(full, op=dist.ReduceOp.SUM, group=group)
+                return 0
+            return 1
+        except Exception:  # never unwind through C
+            return 1
+
+    return _capi.COLLECTIVE_FN(_hook)
+
+
 class Engine:
     """One GPU handle (HIP stream + workspace); mirrors what a C++ caller gets from librsvd_hip."""
 
@@ -139,10 +202,15 @@ class Engine:
             check(lib().rsvd_set_workspace(self.h, ctypes.c_void_p(self._ws.data_ptr()), nbytes), self.h)
         return self._ws
 
-    def set_comm(self, rank: int, world: int, group=None):
-        """Row-sharded runs: bind the exchange hook to torch.distributed.all_reduce (RCCL)."""
+    def set_comm(self, rank: int, world: int, group=None, shard_n: bool = True):
+        """Row-sharded runs: bind the exchange hooks to torch.distributed over RCCL -- the
+        all-reduce (m-side Grams; A^T Q when the n side is replicated) and, with shard_n, the
+        reduce-scatter / all-gather hook that shards the n side across ranks as well."""
         self._hook = make_allreduce_hook(lambda: self._ws, group)
         check(lib().rsvd_set_comm(self.h, rank, world, self._hook, None), self.h)
+        self._coll = make_collective_hook(lambda: self._ws, group) if shard_n and world > 1 else None
+        check(lib().rsvd_set_collectives(self.h, self._coll if self._coll is not None else _capi.COLLECTIVE_FN(), None),
+              self.h)
 
     def set_timing(self, enable: bool = True):
         """hipEvent timing of every projection GEMM launch (benchmarking only)."""

@@ -302,6 +302,7 @@ int run_typed(rsvd_handle_t h, const rsvd_desc_t* d, const void* A, const void* 
     RSVD_CK(hipMemsetAsync(h->ws + L.off_ctr, 0, 64 * sizeof(unsigned), h->stream));
     h->info.splits_nn = L.pnn.splits;
     h->info.splits_tn = L.ptn.splits;
+    h->info.n_shard_rows = 0;
     Engine<T> E(h, L);
     E.qr_mode = d->qr_mode;
     RSVD_TRY(E.load_omega(omega, ldo, d->seed));
@@ -502,6 +503,13 @@ int rsvd_set_comm(rsvd_handle_t h, int rank, int world, rsvd_allreduce_fn fn, vo
     h->world = world;
     h->allreduce = fn;
     h->ar_user = user;
+    return RSVD_OK;
+}
+
+int rsvd_set_collectives(rsvd_handle_t h, rsvd_collective_fn fn, void* user) {
+    if (!h) return RSVD_ERR_INVALID_ARG;
+    h->coll = fn;
+    h->coll_user = user;
     return RSVD_OK;
 }
 

@@ -28,6 +28,8 @@ struct rsvd_handle_s {
     int rank = 0, world = 1;
     rsvd_allreduce_fn allreduce = nullptr;
     void* ar_user = nullptr;
+    rsvd_collective_fn coll = nullptr;  // n-side sharding (wide engine), rsvd_set_collectives
+    void* coll_user = nullptr;
     // timing mode: hipEvent pairs around every projection kernel (kind 0 = A*X, 1 = A^T*Q, 2 = the
     // sketch A*Omega, which also counts as kind 0)
     bool timing = false;

@@ -11,8 +11,13 @@
 // with the wide kernels (wide.hpp): bf16-MFMA projections for bf16 / fp8 A (fp32 / fp64 A use the
 // narrow MFMA kernels per 64-column group), CholeskyQR(2) with fp64 Grams for any LP <= 512, and
 // the block Jacobi small SVD for LP >= 128 (jacobi.hip's one-workgroup kernel below).
-// Row sharding (world > 1) follows driver.cpp: m-side Grams and the n-side products are summed
-// through the all-reduce hook; every rank holds Q_B, S, V and its rows of U.
+// Row sharding (world > 1): m-side Grams are summed through the all-reduce hook; every rank
+// holds S, V and its rows of U.  The n side is either replicated (A^T Q all-reduced, every rank
+// orthonormalises the whole n x l panel) or -- with the collective hook (rsvd_set_collectives) --
+// sharded: rank r owns n-side rows [r nc, (r + 1) nc) (nc = n / world rounded up to 32, the
+// panels zero-padded to world nc rows).  A^T Q is reduce-scattered, each rank runs the CholeskyQR
+// of its rows (l x l Gram all-reduced, like the m side), the bf16 hi / lo panels of the next
+// skinny operand are all-gathered for A X, and V = Q_B V_w is formed per shard and all-gathered.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -54,13 +59,20 @@ struct WideLayout {
 
     int64_t mpad, npad;  // bf16 panel rows, zero-padded to a multiple of 32 (wproj2 reads whole k-steps)
     bool s8 = false;     // the sketch runs e4m3 x e4m3 on the fp8 MFMA
+    // n-side sharding: chunk rows nc per rank, the n-side panels hold nfull = world nc rows
+    bool nsh = false;
+    int64_t nc = 0, nfull = 0;
+    GramPlan gnc, gxc;
 
     // a_aligned: A's base is 16-B aligned (the LDS-DMA projection kernel needs 16-B source chunks)
-    WideLayout(const rsvd_desc_t* d, bool a_aligned = true)
+    WideLayout(const rsvd_desc_t* d, bool a_aligned = true, int world = 1)
         : m(d->m), n(d->n), l(d->l), LP(wide_lp(d->l, d->dtype)) {
         lowp = lowp_dtype(d->dtype);
         mpad = rup(m, 32);
-        npad = rup(n, 32);
+        nsh = world > 1;
+        nc = nsh ? rup((n + world - 1) / world, 32) : n;
+        nfull = nsh ? nc * world : n;
+        npad = std::max(rup(n, 32), nfull);
         int64_t pslab = 1;
         if (lowp) {
             // (m a multiple of the 16-B chunk: a chunk is either inside A's rows or wholly past them,
@@ -78,9 +90,12 @@ struct WideLayout {
         gm = plan_gram_wide(m, LP, 0);
         gn = plan_gram_wide(n, LP, 0);
         gx = plan_gram_wide(n, LP, 1);
+        gnc = plan_gram_wide(nc, LP, 0);
+        gxc = plan_gram_wide(nc, LP, 1);
         const size_t gslab = (size_t)std::max({(int64_t)gm.blocks * gm.chunks, (int64_t)gn.blocks * gn.chunks,
-                                               (int64_t)gx.blocks * gx.chunks}) * 1024;
-        const int64_t mx = std::max(m, n);
+                                               (int64_t)gx.blocks * gx.chunks, (int64_t)gnc.blocks * gnc.chunks,
+                                               (int64_t)gxc.blocks * gxc.chunks}) * 1024;
+        const int64_t mx = std::max({m, n, nc});
         const size_t L2 = (size_t)LP * LP;
         size_t o = 0;
         auto take = [&](size_t bytes) {
@@ -88,8 +103,8 @@ struct WideLayout {
             o = align256(o + bytes);
             return at;
         };
-        off_Xn = take(sizeof(T) * n * LP);
-        off_Zn = take(sizeof(T) * n * LP);
+        off_Xn = take(sizeof(T) * nfull * LP);
+        off_Zn = take(sizeof(T) * nfull * LP);
         off_Ym = take(sizeof(T) * m * LP);
         off_Qm = take(sizeof(T) * m * LP);
         off_T1 = take(sizeof(T) * mx * LP);
@@ -140,6 +155,8 @@ struct WideEngine {
     // normalised by the global row count estimate world * m_g.
     int64_t row_off = 0, m_total = 0, m_norm = 0;
     uint64_t seed = 0;
+    bool nsh = false;  // n side sharded (L.nsh and a run that supports it)
+    int64_t c0 = 0;    // first n-side row of this rank's shard (rank nc)
 
     WideEngine(rsvd_handle_t h_, const WideLayout<T>& L_, int dtype_) : h(h_), L(L_), s(h_->stream), dtype(dtype_) {
         char* b = h->ws;
@@ -178,6 +195,25 @@ struct WideEngine {
             return RSVD_ERR_COMM;
         }
         return RSVD_OK;
+    }
+
+    int collective(int op, void* send, void* recv, int64_t count, int32_t dt) {
+        if (h->coll(op, send, recv, count, dt, (void*)s, h->coll_user) != 0) {
+            h->err = op == RSVD_COLL_REDUCE_SCATTER ? "reduce-scatter hook failed" : "all-gather hook failed";
+            return RSVD_ERR_COMM;
+        }
+        return RSVD_OK;
+    }
+    int32_t tdt() const { return sizeof(T) == 8 ? RSVD_F64 : RSVD_F32; }
+    // the next skinny operand of A X to every rank: its bf16 hi / lo panels (or the T panel)
+    int gather_x() {
+        if (!nsh) return RSVD_OK;
+        const int64_t cnt = L.nc * L.LP;
+        if (L.lowp) {
+            RSVD_TRY(collective(RSVD_COLL_ALL_GATHER, Xh + c0 * L.LP, Xh, cnt, RSVD_BF16));
+            return collective(RSVD_COLL_ALL_GATHER, Xl + c0 * L.LP, Xl, cnt, RSVD_BF16);
+        }
+        return collective(RSVD_COLL_ALL_GATHER, Xn + c0 * L.LP, Xn, cnt, tdt());
     }
 
     int ev_begin(int kind, int& idx) {
@@ -228,7 +264,9 @@ struct WideEngine {
         } else {
             RSVD_CK(launch_proj_tn<T>(reinterpret_cast<const T*>(A), lda, L.m, L.n, Q, L.LP, L.ptn, pslab, Z, s, done));
         }
-        return allreduce(Z, L.n * L.LP, sizeof(T) == 8 ? RSVD_F64 : RSVD_F32);
+        // sharded n side: this rank keeps the sum of its rows [c0, c0 + nc) (rows >= n are zero)
+        if (nsh) return collective(RSVD_COLL_REDUCE_SCATTER, Z, Z + c0 * L.LP, L.nc * L.LP, tdt());
+        return allreduce(Z, L.n * L.LP, tdt());
     }
 
     double tol() const { return sizeof(T) == 4 ? 1e-13 : 1e-28; }
@@ -250,10 +288,18 @@ struct WideEngine {
 
     // Q = orth(P): CholeskyQR (passes = 1) or CholeskyQR2; output panels (repair = true) get the
     // rank-deficiency completion (predicated on the breakdown flag of this orth).
+    // The n side, sharded: P, Q, hi, lo are the full panels; this rank's rows [c0, c0 + nc) are used.
     int orth(const T* P, bool mside, T* Q, int passes, bf16_t* hi, bf16_t* lo, bool repair) {
-        const int64_t rows = mside ? L.m : L.n;
-        const GramPlan& gp = mside ? L.gm : L.gn;
-        const bool sharded = mside && h->world > 1;
+        const bool nshard = !mside && nsh;
+        const int64_t rows = mside ? L.m : (nshard ? L.nc : L.n);
+        const GramPlan& gp = mside ? L.gm : (nshard ? L.gnc : L.gn);
+        const bool sharded = (mside || nshard) && h->world > 1;
+        if (nshard) {
+            P += c0 * L.LP;
+            Q += c0 * L.LP;
+            if (hi) hi += c0 * L.LP;
+            if (lo) lo += c0 * L.LP;
+        }
         int* flag = h->dflags + 4 + (orth_index < 12 ? orth_index : 11);
         ++orth_index;
         if (qr_mode == RSVD_QR_CHOLQR2 || qr_mode == RSVD_QR_GS2) passes = 2;
@@ -264,9 +310,12 @@ struct WideEngine {
             RSVD_TRY(cholqr_pass(T1, rows, gp, Q, sharded, hi, lo, flag, nullptr));
         }
         if (repair) {
-            const int64_t off = mside ? row_off : 0, tot = mside ? m_total : L.n, nrm = mside ? m_norm : L.n;
+            // sharded panels draw disjoint stream rows per rank (rank 2^40 + local row), as the m side
+            const int64_t off = (mside || nshard) ? row_off : 0, tot = (mside || nshard) ? m_total : L.n;
+            const int64_t nrm = mside ? m_norm : L.n;
+            const int64_t valid = nshard ? std::max<int64_t>(0, std::min<int64_t>(L.nc, L.n - c0)) : rows;
             RSVD_CK(launch_repair_panel<T>(Q, rows, L.l, L.LP, colflag, flag, seed ^ (0x5EEDull + orth_index), off,
-                                           tot, nrm, T1, s));
+                                           tot, nrm, T1, s, valid));
             // a breakdown in the repaired pass is reported (sticky) by rsvd_sync as RSVD_ERR_NUMERICAL
             RSVD_TRY(cholqr_pass(T1, rows, gp, Q, sharded, hi, lo, h->dflags + kFlagUnrepaired, flag));
         }
@@ -301,6 +350,7 @@ struct WideEngine {
             const bool last = i == q - 1;
             RSVD_TRY(proj_tn(A, lda, Qm, Qh, Ql, Zn));
             RSVD_TRY(orth(Zn, false, Xn, inter_passes, Xh, Xl, false));
+            RSVD_TRY(gather_x());
             RSVD_TRY(proj_nn(A, lda, Xn, Xh, Xl, Ym));
             RSVD_TRY(orth(Ym, true, Qm, last ? 2 : inter_passes, Qh, Ql, last));
         }
@@ -340,7 +390,12 @@ struct WideEngine {
         RSVD_TRY(range_finder(A, d->lda, d->q));
         RSVD_TRY(proj_tn(A, d->lda, Qm, Qh, Ql, Zn));               // B^T = A^T Q
         RSVD_TRY(orth(Zn, false, Xn, 2, nullptr, nullptr, true));  // Q_B
-        RSVD_CK(launch_gram_wide<T>(Xn, Zn, L.n, L.LP, L.gx, gslab, R1, nullptr, s));  // R = Q_B^T B^T
+        if (nsh) {  // R = Q_B^T B^T summed over the n shards
+            RSVD_CK(launch_gram_wide<T>(Xn + c0 * L.LP, Zn + c0 * L.LP, L.nc, L.LP, L.gxc, gslab, R1, nullptr, s));
+            RSVD_TRY(allreduce(R1, (int64_t)L.LP * L.LP, RSVD_F64));
+        } else {
+            RSVD_CK(launch_gram_wide<T>(Xn, Zn, L.n, L.LP, L.gx, gslab, R1, nullptr, s));  // R = Q_B^T B^T
+        }
         // Inf / NaN in A reach R through B^T = A^T Q whatever the orthonormalisations did with them
         RSVD_CK(launch_check_finite<double>(R1, L.LP * L.LP, h->dflags + kFlagNonFinite, s));
         if (d->method == RSVD_SVD_POWER || d->method == RSVD_SVD_POWER_IC) return power_stage(d, U, ldu, S, V, ldv);
@@ -360,8 +415,15 @@ struct WideEngine {
         }
         RSVD_CK(launch_panel_gemm<T>(Qm, L.m, L.LP, mat(Uw, Uw32), 0, reinterpret_cast<T*>(U), ldu, L.l, nullptr,
                                      nullptr, nullptr, s));
-        RSVD_CK(launch_panel_gemm<T>(Xn, L.n, L.LP, mat(Vw, Vw32), 0, reinterpret_cast<T*>(V), ldv, L.l, nullptr,
-                                     nullptr, nullptr, s));
+        if (nsh) {  // V rows of this shard as a panel (in Zn, free by now), all-gathered, then V
+            RSVD_CK(launch_panel_gemm<T>(Xn + c0 * L.LP, L.nc, L.LP, mat(Vw, Vw32), 0, Zn + c0 * L.LP, 0, 0, nullptr,
+                                         nullptr, nullptr, s));
+            RSVD_TRY(collective(RSVD_COLL_ALL_GATHER, Zn + c0 * L.LP, Zn, L.nc * L.LP, tdt()));
+            RSVD_CK(launch_panel_to_colmajor<T>(Zn, L.n, L.l, L.LP, reinterpret_cast<T*>(V), ldv, s));
+        } else {
+            RSVD_CK(launch_panel_gemm<T>(Xn, L.n, L.LP, mat(Vw, Vw32), 0, reinterpret_cast<T*>(V), ldv, L.l, nullptr,
+                                         nullptr, nullptr, s));
+        }
         return finish(d, S, V, ldv);
     }
 };
@@ -369,9 +431,18 @@ struct WideEngine {
 template <typename T>
 int wide_typed(rsvd_handle_t h, const rsvd_desc_t* d, const void* A, const void* omega, int64_t ldo, void* U,
                int64_t ldu, void* S, void* V, int64_t ldv, void* Qout, int64_t ldq) {
-    WideLayout<T> L(d, (reinterpret_cast<uintptr_t>(A) & 15) == 0);
+    // n-side sharding: a collective hook on a sharded handle, not for SVDMethod::Power (its stage
+    // runs on the whole Q_B) nor for the range-finder-only entry point (Qout)
+    const bool nshard = h->world > 1 && h->coll && !Qout && d->method != RSVD_SVD_POWER &&
+                        d->method != RSVD_SVD_POWER_IC;
+    WideLayout<T> L(d, (reinterpret_cast<uintptr_t>(A) & 15) == 0, nshard ? h->world : 1);
     RSVD_TRY(ensure_ws(h, L.total));
     RSVD_CK(reset_run_flags(h->dflags, h->stream));
+    if (L.nsh && L.nfull > L.n) {  // the zero rows past n of the sharded n-side panels (A^T Q, Q_B)
+        const size_t bpr = sizeof(T) * L.LP;
+        for (size_t off : {L.off_Zn, L.off_Xn})
+            RSVD_CK(hipMemsetAsync(h->ws + off + L.n * bpr, 0, (L.nfull - L.n) * bpr, h->stream));
+    }
     if (L.lowp) {  // the zero padding rows of the bf16 panels (never written by the kernels)
         const size_t bpr = (size_t)2 * L.LP;
         for (size_t off : {L.off_Xh, L.off_Xl})
@@ -379,11 +450,14 @@ int wide_typed(rsvd_handle_t h, const rsvd_desc_t* d, const void* A, const void*
         for (size_t off : {L.off_Qh, L.off_Ql})
             if (L.mpad > L.m) RSVD_CK(hipMemsetAsync(h->ws + off + L.m * bpr, 0, (L.mpad - L.m) * bpr, h->stream));
     }
+    h->info.n_shard_rows = L.nsh ? (int32_t)L.nc : 0;
     h->info.splits_nn = L.lowp ? L.wnn.splits : L.pnn.splits;
     h->info.splits_tn = L.lowp ? L.wtn.splits : L.ptn.splits;
     WideEngine<T> E(h, L, d->dtype);
     E.qr_mode = d->qr_mode;
     E.seed = d->seed;
+    E.nsh = L.nsh;
+    E.c0 = L.nsh ? (int64_t)h->rank * L.nc : 0;
     if (h->world > 1) {
         E.row_off = (int64_t)h->rank << 40;
         E.m_total = (int64_t)h->world << 40;
@@ -405,11 +479,17 @@ int wide_typed(rsvd_handle_t h, const rsvd_desc_t* d, const void* A, const void*
 bool wide_path(const rsvd_desc_t* d) { return lowp_dtype(d->dtype) || d->l > 64; }
 
 int wide_workspace_bytes(const rsvd_desc_t* d, size_t* bytes) {
-    // the larger of the two projection plans (LDS-DMA kernel or not: decided per run by alignment)
-    if (d->dtype == RSVD_F64)
-        *bytes = WideLayout<double>(d).total;
-    else
-        *bytes = std::max(WideLayout<float>(d, true).total, WideLayout<float>(d, false).total);
+    // the largest over the projection plans (LDS-DMA kernel or not: decided per run by alignment)
+    // and over n-side shardings of up to 64 ranks (the zero-padded n-side panels; the handle's
+    // world is not known here)
+    size_t b = 0;
+    for (int world = 1; world <= 64; ++world) {
+        if (d->dtype == RSVD_F64)
+            b = std::max(b, WideLayout<double>(d, true, world).total);
+        else
+            b = std::max({b, WideLayout<float>(d, true, world).total, WideLayout<float>(d, false, world).total});
+    }
+    *bytes = b;
     return RSVD_OK;
 }
 

@@ -31,7 +31,7 @@ struct WProjPlan {
     bool v2;         // LDS-DMA pipelined kernel (bf16 / e4m3 A, LP >= 128, 16-B aligned columns)
     bool ds = false; // v2 TN at LP = 128 with two k-steps per stage (128-B A runs; K a multiple of 64)
     bool v3 = false; // v2 with launch-constant LDS read bases (bf16 A, LP 256 / 512; wide_proj.hip)
-    bool m32 = false; // v3 on v_mfma_f32_32x32x16_bf16 instead of 16x16x32
+    int sd = 1;       // v3: S-panel prefetch distance in k-steps (1 or 2; A runs as far ahead as LDS allows)
     int abl = 0;      // lab-only ablations of the v3 kernel (tools/wide_lab.cpp), never set by the engine
 };
 // v2 requires: a 16-B aligned base, bf16 A with lda and m multiples of 8 or e4m3 A with lda and m
@@ -90,7 +90,7 @@ hipError_t launch_convert_scale(const double* x, T* y, int n, double sc, hipStre
 template <typename T>
 hipError_t launch_repair_panel(const T* Q, int64_t rows, int l, int LP, const int* colflag, const int* flag,
                                uint64_t seed, int64_t row_off, int64_t rows_total, int64_t norm_rows, T* Out,
-                               hipStream_t s);
+                               hipStream_t s, int64_t valid_rows = -1);
 // fp32 / fp64 panel -> bf16 hi (+ lo) panels (rows x LP).
 template <typename T>
 hipError_t launch_split_bf16(const T* P, int64_t rows, int LP, bf16_t* hi, bf16_t* lo, hipStream_t s);

@@ -620,63 +620,63 @@ __global__ __launch_bounds__(512) void wproj2_kernel(const void* __restrict__ Av
 }
 
 // ------------------------------------------------------------------------------------------------
-// v3 (bf16 A, LP in {256, 512}): the v2 pipeline with every LDS fragment read addressed as
-// (per-lane base, fixed for the whole launch) + (per-step slot offset, one v_add per base) +
-// (immediate offset for the tile index).  v2's XOR swizzle put the tile index inside the XOR, so
-// the compiler rebuilt 80+ addresses per k-step -- 1.4 VALU per MFMA, enough to starve the MFMA
-// issue (rocprof: 57 % MFMA busy at C4, 110 VALU per 64 MFMA).  Here the row images are
-// conflict-free by PLACEMENT instead: a [32 k][RB bytes] image is cut into 1-KiB LDS-DMA pieces of
-// 1024 / RB rows, laid out at a padded pitch, and each k row is assigned to a (piece, part) so that
-// the rows one transposed read touches start at distinct bank offsets; columns stay in natural
-// order, so a tile index is a constant offset.
-//   M32 = false (v_mfma_f32_16x16x32_bf16): one ds_read_b64_tr_b16 touches rows {0-3, 8-11} + 4 j
-//   + 16 i, eight 32-B runs: row r goes to piece slot sigma(r) (bits 2 and 3 swapped), pitch 1056.
-//   M32 = true (v_mfma_f32_32x32x16_bf16, which holds the SIMD's issue for 8 of 32 cycles instead
-//   of 8 of 16): a 32-lane half touches rows 4 b .. 4 b + 3, four 64-B runs: row r = 4 B + s goes
-//   to piece s + 4 (B / RP), part B % RP, pitch 1088.
+// v3 (bf16 A, LP in {256, 512}).  Two changes against v2, both measured at C4 (wide_lab):
+// (1) Every LDS fragment read is (per-lane base, fixed for the launch) + (slot offset, one v_add
+//     per base and step) + (immediate tile offset).  v2's XOR swizzle put the tile index inside the
+//     XOR, so the compiler rebuilt 80+ addresses per k-step -- 110 VALU per 64 MFMA, 57 % MFMA
+//     busy.  The row images are conflict-free by PLACEMENT instead: a [32 k][RB bytes] image is cut
+//     into 1-KiB LDS-DMA pieces of 1024 / RB rows at a 1056-B pitch, and k row r goes to piece slot
+//     sigma(r) (bits 2 and 3 swapped), so the eight rows one ds_read_b64_tr_b16 touches ({0-3,
+//     8-11} + 4 j + 16 i) start at eight different 32-B bank offsets; columns stay in natural
+//     order, so a tile index is a constant offset.  (A 32x32x16-MFMA form of the same kernel, which
+//     blocks issue for 8 of 32 cycles instead of 8 of 16, measured 5 % slower: dropped.)
+// (2) A and S have separate LDS rings.  Ablations (nobar / nodma / nolds) showed the DMA stream,
+//     not the MFMA or the LDS reads, bounding the kernel: bytes in flight per CU were capped by
+//     the shared ring (two 48-KiB stages), ~16 B/clk/CU at HBM latency.  A (HBM, read once) now
+//     runs DA steps ahead in its own ring, S (L2-resident panel re-read by every workgroup) SD
+//     steps ahead in a smaller one.
 // The TN A image ([WI j][32 i], 64-B rows, read by ds_read_b128) keeps an XOR swizzle whose term
-// depends on the lane only.  Stages are [A image][S hi][S lo]: every immediate stays below 64 KiB.
+// depends on the lane only.  LDS: [A ring: NA x AIMG][S ring: (SD + 1) x NS x SIMG].
 __host__ __device__ constexpr int v3_sigma(int r) { return (r & ~12) | ((r >> 1) & 4) | ((r << 1) & 8); }
 
-template <bool M32, int RB>  // a [32 k][RB bytes] image, RB in {256, 512, 1024}
+template <int RB>  // a [32 k][RB bytes] image, RB in {256, 512, 1024}
 struct RowImg {
-    static constexpr int RP = 1024 / RB, PITCH = M32 ? 1088 : 1056, PIECES = 32 / RP;
+    static constexpr int RP = 1024 / RB, PITCH = 1056, PIECES = 32 / RP;
     static constexpr int BYTES = PIECES * PITCH;
     __host__ __device__ static constexpr int off(int r) {
-        if (M32) {
-            const int s = r & 3, B = r >> 2;
-            return (s + 4 * (B / RP)) * PITCH + (B % RP) * RB;
-        }
         const int s = v3_sigma(r), G = s >> 3, idx = s & 7;
         return ((G / RP) * 8 + idx) * PITCH + (G % RP) * RB;
     }
     __host__ __device__ static constexpr int row_of(int pc, int part) {  // the row piece pc holds in `part`
-        if (M32) return 4 * ((pc >> 2) * RP + part) + (pc & 3);
         return v3_sigma(((pc >> 3) * RP + part) * 8 + (pc & 7));
     }
 };
 
-template <int LP, bool NN, bool SPLIT, bool M32>
+template <int LP, bool NN, bool SPLIT, int SD>
 struct W3Shape {
     static constexpr int WR = W2Cfg<LP, false>::WR, WC = W2Cfg<LP, false>::WC, G = W2Cfg<LP, false>::G;
     static constexpr int WI = WR * 64;
     static constexpr int NS = SPLIT ? 2 : 1;
-    typedef RowImg<M32, LP * 2> SImg;
-    typedef RowImg<M32, WI * 2> AImg;
+    typedef RowImg<LP * 2> SImg;
+    typedef RowImg<WI * 2> AImg;
     static constexpr int SIMG = SImg::BYTES;
-    static constexpr int AIMG = NN ? AImg::BYTES : KS * WI * 2;
-    static constexpr int SPC = SImg::PIECES;                  // pieces per S image
-    static constexpr int APC = NN ? AImg::PIECES : AIMG / 1024;  // pieces of the A image
-    static constexpr int SPW = SPC / 8, APW = APC / 8;         // ... per wave
+    static constexpr int AIMG0 = NN ? AImg::BYTES : KS * WI * 2;
+    static constexpr int AIMG = (AIMG0 + 255) / 256 * 256;
+    static constexpr int SPC = SImg::PIECES;                   // pieces per S image
+    static constexpr int APC = NN ? AImg::PIECES : AIMG0 / 1024;  // pieces of the A image
+    static constexpr int SPW = SPC / 8, APW = APC / 8;          // ... per wave
     static constexpr int APITCH = NN ? AImg::PITCH : 1024;
-    static constexpr int STAGE = (AIMG + NS * SIMG + 255) / 256 * 256;
-    static constexpr int NST0 = 163840 / STAGE;
-    static constexpr int NST = NST0 > 4 ? 4 : NST0;
-    static constexpr int GL = NS * SPW + APW;  // glds per thread per stage
-    static constexpr size_t LDS = (size_t)NST * STAGE;
-    static_assert(SPC % 8 == 0 && APC % 8 == 0 && NST >= 2, "v3 stage shape");
-    static_assert(AIMG + (NS - 1) * SIMG + (M32 ? SImg::off(16) - SImg::off(0) + 2 * 16 * G : 32 * G) < 65536,
-                  "immediate offsets");
+    static constexpr int SSLOT = (NS * SIMG + 255) / 256 * 256;
+    static constexpr int NSS = SD + 1;                         // S ring slots
+    static constexpr int NA0 = (163840 - NSS * SSLOT) / AIMG;
+    static constexpr int NA = NA0 > 8 ? 8 : NA0;               // A ring slots
+    static constexpr int DA = NA - 1;                          // A prefetch distance (steps)
+    static constexpr int SBASE = NA * AIMG;
+    static constexpr int GL = NS * SPW + APW;                  // glds per thread per step
+    static constexpr size_t LDS = (size_t)SBASE + (size_t)NSS * SSLOT;
+    static_assert(SPC % 8 == 0 && APC % 8 == 0, "v3 piece split");
+    static_assert(DA >= SD && LDS <= 163840, "v3 rings");
+    static_assert((NS - 1) * SIMG + 32 * G < 65536, "immediate offsets");
 };
 
 template <typename F, int... I>
@@ -703,21 +703,19 @@ __device__ __forceinline__ i32x4 read128_o(uint32_t a) {
 
 // ABL (lab ablations, results meaningless): bit 0 no barrier / DMA waits, bit 1 no DMA, bit 2 no
 // LDS fragment reads.  The product path instantiates ABL = 0 only.
-template <bool NN, int LP, bool SPLIT, int KN, bool M32, int ABL = 0>
+template <bool NN, int LP, bool SPLIT, int KN, int SD, int ABL = 0>
 __global__ __launch_bounds__(512) void wproj3_kernel(const bf16_t* __restrict__ A, int64_t lda, int64_t rows_out,
                                                      int64_t K, int64_t arows, const bf16_t* __restrict__ Shi,
                                                      const bf16_t* __restrict__ Slo, float* __restrict__ out,
                                                      int64_t slab_stride, int64_t kchunk, int nrowblk) {
-    typedef W3Shape<LP, NN, SPLIT, M32> SH;
+    typedef W3Shape<LP, NN, SPLIT, SD> SH;
     typedef typename SH::SImg SImg;
     typedef typename SH::AImg AImg;
-    constexpr int WR = SH::WR, G = SH::G, WI = SH::WI, NS = SH::NS, NST = SH::NST;
-    // MFMA tiles per wave: 16x16 -> RT x G tiles of 16; 32x32 -> RT2 x G2 tiles of 32
-    constexpr int TM = M32 ? 32 : 16, NT = 64 / TM, NG = 16 * G / TM;
-    constexpr int AREGS = M32 ? 16 : 4;
+    constexpr int WR = SH::WR, G = SH::G, WI = SH::WI, NS = SH::NS, NA = SH::NA, DA = SH::DA, NSS = SH::NSS;
     extern __shared__ __attribute__((aligned(1024))) char smem_raw[];
     const int tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int r = lane & 15, h = lane >> 4, q = r >> 2, p = r & 3;
     const int wr = w % WR, wc = w / WR;
     const int bid = xcd_remap(blockIdx.x, gridDim.x);
     const int rb = bid % nrowblk, sp = bid / nrowblk;
@@ -746,27 +744,31 @@ __global__ __launch_bounds__(512) void wproj3_kernel(const bf16_t* __restrict__ 
             i = (i + 8 <= arows) ? i : arows - 8;
             aoff[t] = (int64_t)rr * lda + i;
             arow[t] = rr;
-        } else {  // 16 rows j x 4 chunks; chunk position cc holds rows 8 (cc ^ swizzle(j))
+        } else {  // 16 rows j x 4 chunks; chunk position cc holds rows 8 (cc ^ ((j >> 1) & 3))
             const int u = pc * 64 + lane, j = u >> 2, cc = u & 3;
             int64_t jc = row0 + j;
             jc = jc < rows_out ? jc : rows_out - 1;
-            const int i = 8 * (cc ^ (M32 ? ((j >> 2) & 3) : ((j >> 1) & 3)));
+            const int i = 8 * (cc ^ ((j >> 1) & 3));
             aoff[t] = jc * lda + i;
             arow[t] = i;
         }
     }
 
-    auto issue = [&](int st) {
+    auto issueS = [&](int st) {
         if constexpr ((ABL & 2) != 0) return;
-        char* slot = smem_raw + (st % NST) * SH::STAGE;
+        char* slot = smem_raw + SH::SBASE + (st % NSS) * SH::SSLOT;
         const int64_t k0 = kbeg + (int64_t)st * KS;
 #pragma unroll
         for (int a = 0; a < NS; ++a) {
             const bf16_t* S = (a ? Slo : Shi) + k0 * LP;
 #pragma unroll
-            for (int t = 0; t < SH::SPW; ++t)
-                glds16(S + soff[t], slot + SH::AIMG + a * SH::SIMG + (t * 8 + w) * SImg::PITCH);
+            for (int t = 0; t < SH::SPW; ++t) glds16(S + soff[t], slot + a * SH::SIMG + (t * 8 + w) * SImg::PITCH);
         }
+    };
+    auto issueA = [&](int st) {
+        if constexpr ((ABL & 2) != 0) return;
+        char* slot = smem_raw + (st % NA) * SH::AIMG;
+        const int64_t k0 = kbeg + (int64_t)st * KS;
         const bool tail = k0 + KS > K;  // (uniform) the last step of a ragged K: clamp the A reads
 #pragma unroll
         for (int t = 0; t < SH::APW; ++t) {
@@ -782,131 +784,52 @@ __global__ __launch_bounds__(512) void wproj3_kernel(const bf16_t* __restrict__ 
         }
     };
 
-    // per-lane LDS read bases within a stage (see the image comment above)
-    uint32_t lS1, lS2, lA1, lA2;
-    if constexpr (M32) {
-        const int h = lane >> 5, q = (lane & 15) >> 2, p = lane & 3, g16 = (lane >> 4) & 1;
-        const int kr = 8 * h + q;
-        lS1 = SImg::off(kr) + 2 * (wc * G * 16 + 16 * g16 + 4 * p);
-        lS2 = SImg::off(kr + 4) + 2 * (wc * G * 16 + 16 * g16 + 4 * p);
-        if constexpr (NN) {
-            lA1 = AImg::off(kr) + 2 * (wr * 64 + 16 * g16 + 4 * p);
-            lA2 = AImg::off(kr + 4) + 2 * (wr * 64 + 16 * g16 + 4 * p);
-        } else {  // row j = wr 64 + 32 t + r, k = 16 c + 8 h + 0..7: chunk (2 c + h) ^ ((r >> 2) & 3)
-            const int r = lane & 31, sw = (r >> 2) & 3;
-            lA1 = (wr * 64 + r) * 64 + 16 * (h ^ sw);
-            lA2 = (wr * 64 + r) * 64 + 16 * ((2 + h) ^ sw);
-        }
+    // per-lane LDS read bases within a slot
+    const int colS = wc * G * 16 + 4 * p;
+    const int k1 = 8 * h + q, k2 = k1 + 4;
+    const uint32_t lS1 = SImg::off(k1) + 2 * colS, lS2 = SImg::off(k2) + 2 * colS;
+    uint32_t lA1, lA2;
+    if constexpr (NN) {
+        const int colA = wr * 64 + 4 * p;
+        lA1 = AImg::off(k1) + 2 * colA;
+        lA2 = AImg::off(k2) + 2 * colA;
     } else {
-        const int r = lane & 15, h = lane >> 4, q = r >> 2, p = r & 3;
-        const int k1 = 8 * h + q, k2 = k1 + 4;
-        lS1 = SImg::off(k1) + 2 * (wc * G * 16 + 4 * p);
-        lS2 = SImg::off(k2) + 2 * (wc * G * 16 + 4 * p);
-        if constexpr (NN) {
-            lA1 = AImg::off(k1) + 2 * (wr * 64 + 4 * p);
-            lA2 = AImg::off(k2) + 2 * (wr * 64 + 4 * p);
-        } else {
-            lA1 = (wr * 64 + r) * 64 + 16 * (h ^ ((r >> 1) & 3));
-            lA2 = 0;
-        }
+        lA1 = (wr * 64 + r) * 64 + 16 * (h ^ ((r >> 1) & 3));
+        lA2 = 0;
     }
-    // 32x32: the k rows 16 .. 31 of an image sit a constant distance from rows 0 .. 15
-    constexpr int S16 = SImg::off(16) - SImg::off(0);
-    constexpr int A16 = NN ? AImg::off(16) - AImg::off(0) : 0;
 
-    typedef __attribute__((ext_vector_type(16))) float f32x16;
-    f32x4 acc[M32 ? 1 : RT][M32 ? 1 : G];
-    f32x16 acc32[M32 ? NT : 1][M32 ? NG : 1];
-    if constexpr (M32) {
+    f32x4 acc[RT][G];
 #pragma unroll
-        for (int t = 0; t < NT; ++t)
+    for (int t = 0; t < RT; ++t)
 #pragma unroll
-            for (int g = 0; g < NG; ++g)
-#pragma unroll
-                for (int e = 0; e < 16; ++e) acc32[t][g][e] = 0.f;
-    } else {
-#pragma unroll
-        for (int t = 0; t < RT; ++t)
-#pragma unroll
-            for (int g = 0; g < G; ++g) acc[t][g] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-    (void)AREGS;
+        for (int g = 0; g < G; ++g) acc[t][g] = f32x4{0.f, 0.f, 0.f, 0.f};
 
     if ((KN & 2) && w >= 4) __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int st = 0; st < NST - 1; ++st)
-        if (st < nsteps) issue(st);
+    // prologue: the issues of the virtual iterations -DA .. -1 (S(i + SD), A(i + DA)), so that the
+    // steady-state wait below counts the same glds in every iteration
+    for (int i = -DA; i < 0; ++i) {
+        if (i + SD >= 0 && i + SD < nsteps) issueS(i + SD);
+        if (i + DA < nsteps) issueA(i + DA);
+    }
 
+    const uint32_t lds0 = lds_addr(smem_raw);
     for (int st = 0; st < nsteps; ++st) {
         if constexpr ((ABL & 1) == 0) {
-            if (st + NST - 2 < nsteps) wait_vm<(NST - 2) * SH::GL>();
+            // S(st) and A(st) have landed once at most the glds issued after S(st) are in flight:
+            // A(st - SD + DA) and the SD - 1 full iterations since (conservatively all, at the end)
+            if (st - 1 + DA < nsteps) wait_vm<SH::APW + (SD - 1) * SH::GL>();
             else wait_vm<0>();
             __builtin_amdgcn_s_barrier();
         }
-        if (st + NST - 1 < nsteps) issue(st + NST - 1);
-        const uint32_t slot = lds_addr(smem_raw) + (uint32_t)((st % NST) * SH::STAGE);
-        const uint32_t bS1 = slot + lS1, bS2 = slot + lS2, bA1 = slot + lA1, bA2 = slot + lA2;
+        if (st + SD < nsteps) issueS(st + SD);
+        if (st + DA < nsteps) issueA(st + DA);
+        const uint32_t sS = lds0 + SH::SBASE + (uint32_t)((st % NSS) * SH::SSLOT);
+        const uint32_t sA = lds0 + (uint32_t)((st % NA) * SH::AIMG);
+        const uint32_t bS1 = sS + lS1, bS2 = sS + lS2, bA1 = sA + lA1, bA2 = sA + lA2;
         auto wait_b = [&](i32x2* b) {
             if (SPLIT) wait_lgkm0(b[0], b[1], b[2], b[3]);
             else wait_lgkm0(b[0], b[1]);
         };
-        if constexpr (M32) {
-            auto chunk = [&](auto cc) {  // k rows 16 c .. 16 c + 15 of the step
-                constexpr int c = decltype(cc)::value;
-                i32x2 a1[NT], a2[NT];
-                i32x4 a4[NT];
-                bf16x8_t af[NT];
-                auto aread = [&](auto tc) {
-                    constexpr int t = decltype(tc)::value;
-                    if constexpr (NN) {
-                        a1[t] = tr_read_o<c * A16 + 64 * t>(bA1);
-                        a2[t] = tr_read_o<c * A16 + 64 * t>(bA2);
-                    } else {
-                        a4[t] = read128_o<2048 * t>(c ? bA2 : bA1);
-                    }
-                };
-                static_for<NT>(aread);
-                auto bread = [&](auto gc, i32x2* b) {
-                    constexpr int g = decltype(gc)::value;
-                    b[0] = tr_read_o<SH::AIMG + c * S16 + 64 * g>(bS1);
-                    b[1] = tr_read_o<SH::AIMG + c * S16 + 64 * g>(bS2);
-                    if constexpr (SPLIT) {
-                        b[2] = tr_read_o<SH::AIMG + SH::SIMG + c * S16 + 64 * g>(bS1);
-                        b[3] = tr_read_o<SH::AIMG + SH::SIMG + c * S16 + 64 * g>(bS2);
-                    }
-                };
-                i32x2 bb[2][4];
-                bread(std::integral_constant<int, 0>{}, bb[0]);
-                wait_b(bb[0]);
-#pragma unroll
-                for (int t = 0; t < NT; ++t) {
-                    if (NN) wait_lgkm0(a1[t], a2[t]);
-                    else wait_lgkm0(a4[t]);
-                    af[t] = NN ? join2(a1[t], a2[t]) : __builtin_bit_cast(bf16x8_t, a4[t]);
-                }
-                auto gstep = [&](auto gc) {
-                    constexpr int g = decltype(gc)::value;
-                    if constexpr (g + 1 < NG) bread(std::integral_constant<int, g + 1>{}, bb[(g + 1) & 1]);
-                    __builtin_amdgcn_sched_barrier(0);
-                    const i32x2* b = bb[g & 1];
-                    const bf16x8_t bh = join2(b[0], b[1]);
-#pragma unroll
-                    for (int t = 0; t < NT; ++t)
-                        acc32[t][g] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[t], bh, acc32[t][g], 0, 0, 0);
-                    if constexpr (SPLIT) {
-                        const bf16x8_t bl = join2(b[2], b[3]);
-#pragma unroll
-                        for (int t = 0; t < NT; ++t)
-                            acc32[t][g] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[t], bl, acc32[t][g], 0, 0, 0);
-                    }
-                    __builtin_amdgcn_sched_barrier(0);
-                    if constexpr (g + 1 < NG) wait_b(bb[(g + 1) & 1]);
-                };
-                static_for<NG>(gstep);
-            };
-            chunk(std::integral_constant<int, 0>{});
-            chunk(std::integral_constant<int, 1>{});
-        } else {
         i32x2 a1[RT], a2[RT];
         i32x4 a4[RT];
         bf16x8_t af[RT];
@@ -930,11 +853,11 @@ __global__ __launch_bounds__(512) void wproj3_kernel(const bf16_t* __restrict__ 
                 b[1] = b[3] = i32x2{(int)bS2 + g, (int)bS1};
                 return;
             }
-            b[0] = tr_read_o<SH::AIMG + 32 * g>(bS1);
-            b[1] = tr_read_o<SH::AIMG + 32 * g>(bS2);
+            b[0] = tr_read_o<32 * g>(bS1);
+            b[1] = tr_read_o<32 * g>(bS2);
             if constexpr (SPLIT) {
-                b[2] = tr_read_o<SH::AIMG + SH::SIMG + 32 * g>(bS1);
-                b[3] = tr_read_o<SH::AIMG + SH::SIMG + 32 * g>(bS2);
+                b[2] = tr_read_o<SH::SIMG + 32 * g>(bS1);
+                b[3] = tr_read_o<SH::SIMG + 32 * g>(bS2);
             }
         };
         i32x2 bb[2][4];
@@ -963,46 +886,30 @@ __global__ __launch_bounds__(512) void wproj3_kernel(const bf16_t* __restrict__ 
             if constexpr (g + 1 < G) wait_b(bb[(g + 1) & 1]);
         };
         static_for<G>(gstep);
-        }
     }
 
     float* dst = out + (int64_t)sp * slab_stride;
-    if constexpr (M32) {  // D: col = lane & 31, row = (e & 3) + 8 (e >> 2) + 4 (lane >> 5)
-        const int r = lane & 31, h = lane >> 5;
 #pragma unroll
-        for (int t = 0; t < NT; ++t)
+    for (int t = 0; t < RT; ++t)
 #pragma unroll
-            for (int e = 0; e < 16; ++e) {
-                const int64_t row = row0 + wr * 64 + 32 * t + (e & 3) + 8 * (e >> 2) + 4 * h;
-                if (row < rows_out) {
+        for (int j = 0; j < 4; ++j) {
+            const int64_t row = row0 + wr * 64 + 16 * t + 4 * h + j;
+            if (row < rows_out) {
 #pragma unroll
-                    for (int g = 0; g < NG; ++g) dst[row * LP + wc * G * 16 + 32 * g + r] = acc32[t][g][e];
-                }
+                for (int g = 0; g < G; ++g) dst[row * LP + wc * G * 16 + 16 * g + r] = acc[t][g][j];
             }
-    } else {
-        const int r = lane & 15, h = lane >> 4;
-#pragma unroll
-        for (int t = 0; t < RT; ++t)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const int64_t row = row0 + wr * 64 + 16 * t + 4 * h + j;
-                if (row < rows_out) {
-#pragma unroll
-                    for (int g = 0; g < G; ++g) dst[row * LP + wc * G * 16 + 16 * g + r] = acc[t][g][j];
-                }
-            }
-    }
+        }
 }
 
-template <bool NN, int LP, bool SPLIT, bool M32, int ABL = 0>
+template <bool NN, int LP, bool SPLIT, int SD, int ABL = 0>
 hipError_t wproj3_go(const void* A, int64_t lda, int64_t m, int64_t n, const bf16_t* Shi, const bf16_t* Slo,
                      const WProjPlan& p, float* slabs, float* Out, hipStream_t s, hipEvent_t done) {
-    typedef W3Shape<LP, NN, SPLIT, M32> SH;
+    typedef W3Shape<LP, NN, SPLIT, SD> SH;
     const int64_t rows_out = NN ? m : n, K = NN ? n : m;
     float* o = p.splits == 1 ? Out : slabs;
     const int64_t stride = rows_out * LP;
     constexpr int KN = NN ? 3 : 0;  // as v2 (profiles/r02_wide_lab_knobs.txt)
-    hipLaunchKernelGGL((wproj3_kernel<NN, LP, SPLIT, KN, M32, ABL>), dim3(p.blocks * p.splits), dim3(512), SH::LDS, s,
+    hipLaunchKernelGGL((wproj3_kernel<NN, LP, SPLIT, KN, SD, ABL>), dim3(p.blocks * p.splits), dim3(512), SH::LDS, s,
                        reinterpret_cast<const bf16_t*>(A), lda, rows_out, K, m, Shi, Slo, o, stride, p.chunk, p.blocks);
     hipError_t e = hipGetLastError();
     if (e == hipSuccess && done) e = hipEventRecord(done, s);
@@ -1058,24 +965,26 @@ hipError_t wproj_lp(int nn, int fp8, const void* A, int64_t lda, int64_t m, int6
     }
     if constexpr (LP == 256 || LP == 512) {
         if (p.v2 && p.v3 && !fp8) {
-#define GO3(M)                                                                                         \
-    {                                                                                                  \
-        if (nn) return split ? wproj3_go<true, LP, true, M>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d) \
-                             : wproj3_go<true, LP, false, M>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d); \
-        return split ? wproj3_go<false, LP, true, M>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d)        \
-                     : wproj3_go<false, LP, false, M>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d);      \
+#define GO3(SD)                                                                                         \
+    {                                                                                                   \
+        if (nn) return split ? wproj3_go<true, LP, true, SD>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d) \
+                             : wproj3_go<true, LP, false, SD>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d); \
+        return split ? wproj3_go<false, LP, true, SD>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d)        \
+                     : wproj3_go<false, LP, false, SD>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d);      \
     }
             if constexpr (LP == 256) {  // lab ablations of the C4 NN2 / TN2 kernels
                 if (p.abl && split) {
 #define AB(X) \
-    case X: return nn ? wproj3_go<true, 256, true, false, X>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d) \
-                      : wproj3_go<false, 256, true, false, X>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d);
+    case X: return nn ? wproj3_go<true, 256, true, 1, X>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d) \
+                      : wproj3_go<false, 256, true, 1, X>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d);
                     switch (p.abl) { AB(1) AB(2) AB(3) AB(4) AB(5) AB(6) AB(7) default: break; }
 #undef AB
                 }
             }
-            if (p.m32) GO3(true);
-            GO3(false);
+            if constexpr (LP == 256) {  // (LP = 512 split: a third S slot does not fit)
+                if (p.sd == 2) GO3(2);
+            }
+            GO3(1);
 #undef GO3
         }
     }

@@ -850,7 +850,7 @@ __global__ __launch_bounds__(256) void panel_gemm_kernel(const T* __restrict__ I
 template <typename T>
 __global__ void repair_kernel(const T* __restrict__ Q, int64_t rows, int l, int LP, const int* __restrict__ colflag,
                               const int* __restrict__ flag, uint64_t seed, int64_t row_off, int64_t rows_total,
-                              int64_t norm_rows, T* __restrict__ Out) {
+                              int64_t norm_rows, int64_t valid_rows, T* __restrict__ Out) {
     if (*flag == 0) return;
     const double sc = 1.0 / sqrt((double)norm_rows);
     const int64_t total = rows * LP;
@@ -858,7 +858,8 @@ __global__ void repair_kernel(const T* __restrict__ Q, int64_t rows, int l, int 
         const int64_t i = e / LP;
         const int c = (int)(e - i * LP);
         T v = Q[e];
-        if (c < l && colflag[c]) v = (T)(gauss_elem((uint64_t)(row_off + i + rows_total * (int64_t)c), seed) * sc);
+        if (c < l && colflag[c])  // (rows past valid_rows: the zero padding of a sharded panel stays zero)
+            v = i < valid_rows ? (T)(gauss_elem((uint64_t)(row_off + i + rows_total * (int64_t)c), seed) * sc) : (T)0;
         Out[e] = v;
     }
 }
@@ -1038,9 +1039,9 @@ hipError_t launch_panel_gemm(const T* In, int64_t rows, int LP, const T* Mm, int
 template <typename T>
 hipError_t launch_repair_panel(const T* Q, int64_t rows, int l, int LP, const int* colflag, const int* flag,
                                uint64_t seed, int64_t row_off, int64_t rows_total, int64_t norm_rows, T* Out,
-                               hipStream_t s) {
+                               hipStream_t s, int64_t valid_rows) {
     hipLaunchKernelGGL((repair_kernel<T>), dim3(grid_1d(rows * LP)), dim3(256), 0, s, Q, rows, l, LP, colflag, flag,
-                       seed, row_off, rows_total, norm_rows, Out);
+                       seed, row_off, rows_total, norm_rows, valid_rows < 0 ? rows : valid_rows, Out);
     return hipGetLastError();
 }
 
@@ -1084,7 +1085,7 @@ hipError_t launch_convert_scale(const double* x, T* y, int n, double sc, hipStre
     template hipError_t launch_panel_gemm<T>(const T*, int64_t, int, const T*, int, T*, int64_t, int, bf16_t*,      \
                                              bf16_t*, const int*, hipStream_t);                                     \
     template hipError_t launch_repair_panel<T>(const T*, int64_t, int, int, const int*, const int*, uint64_t,       \
-                                               int64_t, int64_t, int64_t, T*, hipStream_t);                         \
+                                               int64_t, int64_t, int64_t, T*, hipStream_t, int64_t);                \
     template hipError_t launch_split_bf16<T>(const T*, int64_t, int, bf16_t*, bf16_t*, hipStream_t);
 RSVD_INST(float)
 RSVD_INST(double)

@@ -1,8 +1,9 @@
 """GPU, world_size 2: the row-sharded engine path end to end on one MI355X.
 
-Two processes share cuda:0 and exchange through the engine's all-reduce hook over gloo (RCCL
-refuses two ranks on one device; the hook and the engine code are the same that bench.py drives
-over RCCL on N GPUs).  Rank g owns rows rsvd_row_partition(m, 2, g) of A (src/rSVD.cpp:20-23);
+Two processes share cuda:0 and exchange through the engine's all-reduce and collective hooks over
+gloo (RCCL refuses two ranks on one device; the hooks and the engine code are the same that
+bench.py drives over RCCL on N GPUs).  Every case runs with the n side sharded (reduce-scatter /
+all-gather, the default) and replicated (all-reduce).  Rank g owns rows rsvd_row_partition(m, 2, g) of A (src/rSVD.cpp:20-23);
 the gathered U rows, S and V must match the single-process oracle on the same A and Omega.
 Tolerances: fp64 1e-9 (S) / 1e-8 (leading half of U, V) -- the sharded CholeskyQR factors the
 all-reduced Gram (a different summation order than the single-GPU in-kernel reduction); fp32 /
@@ -39,7 +40,7 @@ def _matrix(case):
     return gapped_matrix(m, n, 2 * l, decay=0.93 if l < 256 else 0.985, seed=5).astype(np.float64)
 
 
-def _worker(rank, port, case, q):
+def _worker(rank, port, case, q, shard_n):
     try:
         sys.path.insert(0, REPO)
         sys.path.insert(0, os.path.join(REPO, "tests"))
@@ -59,9 +60,11 @@ def _worker(rank, port, case, q):
         tdt = {"f64": torch.float64, "f32": torch.float32, "bf16": torch.bfloat16}[dt]
         Ag = torch.from_numpy(np.ascontiguousarray(A[off:off + rows].T)).cuda().to(tdt).t()
         eng = R.Engine(0)
-        eng.set_comm(rank, WORLD)
+        eng.set_comm(rank, WORLD, shard_n=shard_n)
         U, S, V = eng.rsvd(Ag, l, q=qq, seed=4242)
         torch.cuda.synchronize()
+        nsh = eng.info()["n_shard_rows"]
+        assert (nsh == -(-(-(-n // WORLD)) // 32) * 32) if shard_n else nsh == 0, nsh
         q.put((rank, off, U.cpu().double().numpy(), S.cpu().double().numpy(), V.cpu().double().numpy(),
                Ag.float().cpu().double().numpy()))
         eng.close()
@@ -72,13 +75,13 @@ def _worker(rank, port, case, q):
         q.put((rank, None, traceback.format_exc(), None, None, None))
 
 
-def _run_world2(case):
+def _run_world2(case, shard_n=True):
     import torch.multiprocessing as mp
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, port, case, q)) for r in range(WORLD)]
+    procs = [ctx.Process(target=_worker, args=(r, port, case, q, shard_n)) for r in range(WORLD)]
     for p in procs:
         p.start()
     res = [q.get(timeout=300) for _ in range(WORLD)]
@@ -90,13 +93,14 @@ def _run_world2(case):
     return res
 
 
+@pytest.mark.parametrize("shard_n", [True, False])
 @pytest.mark.parametrize("dt", ["f64", "f32"])
-def test_row_sharded_rank_deficient_is_orthonormal(dt):
+def test_row_sharded_rank_deficient_is_orthonormal(dt, shard_n):
     """The reference's rank-2 input/sparse_matrix.mtx (A[i,j] = 100 i + j + 1) split over 2 ranks,
     l = 16: the breakdown columns of every output panel are completed (repair pass with disjoint
     Philox rows per rank), so U and V are orthonormal -- as the reference's Householder Q always is
     (src/rSVD.cpp:60-61) -- and sigma_1, sigma_2 are the known answers."""
-    res = _run_world2((100, 100, 16, 2, dt, "sparse_matrix"))
+    res = _run_world2((100, 100, 16, 2, dt, "sparse_matrix"), shard_n)
     U = np.vstack([r[2] for r in res])
     S, V = res[0][3], res[0][4]
     tol = 1e-10 if dt == "f64" else 1e-5
@@ -110,12 +114,13 @@ def test_row_sharded_rank_deficient_is_orthonormal(dt):
 
 @pytest.mark.parametrize("case", [(600, 300, 32, 2, "f64"), (1024, 512, 64, 2, "f32"), (2048, 1024, 128, 1, "bf16"),
                                   (4096, 2048, 256, 2, "bf16")])
-def test_row_sharded_world2_matches_oracle(case):
+@pytest.mark.parametrize("shard_n", [True, False])
+def test_row_sharded_world2_matches_oracle(case, shard_n):
     import oracle
     from conftest import rel_fro, sign_align
 
     m, n, l, qq, dt = case
-    res = _run_world2(case)
+    res = _run_world2(case, shard_n)
     U = np.vstack([r[2] for r in res])
     A = np.vstack([r[5] for r in res])  # the values the GPU saw (bf16 / fp32 rounded)
     S0, V0 = res[0][3], res[0][4]

@@ -264,7 +264,7 @@ static void bench_proj(bool c4only = false) {
             WProjPlan pnn = plan_wproj(c.m, c.n, c.LP, v2 > 0), ptn = plan_wproj(c.n, c.m, c.LP, v2 > 0, false, c.fp8);
             if (v2 == 1) pnn.v3 = ptn.v3 = false;
             if (v2 >= 2 && !pnn.v3 && !ptn.v3) continue;
-            pnn.m32 = ptn.m32 = (v2 == 3);
+            pnn.sd = ptn.sd = (v2 == 3) ? 2 : 1;
             float* slabs;
             CK(hipMalloc(&slabs, (size_t)std::max<int64_t>(pnn.splits * c.m, ptn.splits * c.n) * c.LP * 4));
             const double bytes = (double)c.m * c.n * esz, fl = 2.0 * c.m * c.n * c.LP;
@@ -273,7 +273,7 @@ static void bench_proj(bool c4only = false) {
             double t3 = time_us([&] { CK(launch_wproj(0, c.fp8, A, c.m, c.m, c.n, Sh, Sl, c.LP, ptn, slabs, Out, S)); });
             printf("proj%s m=%ld n=%ld LP=%d fp8=%d: NN1 %.1f us (%.0f GB/s) NN2 %.1f us (%.0f GB/s, %.0f TF) TN2 %.1f us"
                    " (%.0f GB/s, %.0f TF) splits nn=%d tn=%d\n",
-                   v2 == 3 ? "v3m32" : (v2 == 2 ? "v3" : (v2 ? "v2" : "v1")), (long)c.m, (long)c.n, c.LP, c.fp8, t1, bytes / t1 / 1e3, t2, bytes / t2 / 1e3,
+                   v2 == 3 ? "v3sd2" : (v2 == 2 ? "v3" : (v2 ? "v2" : "v1")), (long)c.m, (long)c.n, c.LP, c.fp8, t1, bytes / t1 / 1e3, t2, bytes / t2 / 1e3,
                    2 * fl / t2 / 1e6, t3, bytes / t3 / 1e3, 2 * fl / t3 / 1e6, pnn.splits, ptn.splits);
             CK(hipFree(slabs));
         }
@@ -372,7 +372,7 @@ static void check_proj() {  // v2 (LDS-DMA) against v1 on random bf16 / e4m3 dat
             const int64_t ro = nn ? m : n, K = nn ? n : m;
             WProjPlan p1 = plan_wproj(ro, K, LP, false, nn, fp8), p2 = plan_wproj(ro, K, LP, true, nn, fp8);
             for (int m32 = 0; m32 < 2; ++m32) {
-            p2.m32 = m32;
+            p2.sd = 1 + m32;
             if (m32 && !p2.v3) continue;
             CK(launch_wproj(nn, fp8, A, m, m, n, Sh, Sl, LP, p1, sl, O1, S));
             CK(launch_wproj(nn, fp8, A, m, m, n, Sh, Sl, LP, p2, sl, O2, S));
@@ -386,7 +386,7 @@ static void check_proj() {  // v2 (LDS-DMA) against v1 on random bf16 / e4m3 dat
                 mx2 = std::max(mx2, (double)fabs(a[i]));
             }
             printf("check fp8=%d LP=%d %s%s: max|v1-v2| = %.3e (max|v1| = %.3e) v2 splits=%d chunk=%ld\n",
-                   fp8, LP, nn ? "NN" : "TN", m32 ? " m32" : (p2.v3 ? " v3" : ""), md, mx2, p2.splits, (long)p2.chunk);
+                   fp8, LP, nn ? "NN" : "TN", m32 ? " v3sd2" : (p2.v3 ? " v3" : ""), md, mx2, p2.splits, (long)p2.chunk);
             }
         }
         CK(hipFree(A)); CK(hipFree(Sh)); CK(hipFree(Sl)); CK(hipFree(O1)); CK(hipFree(O2)); CK(hipFree(sl));
@@ -489,6 +489,86 @@ static void check_s8() {
     CK(hipFree(A)); CK(hipFree(S8)); CK(hipFree(Sb)); CK(hipFree(O)); CK(hipFree(sl));
 }
 
+// LDS-DMA vs register-path load throughput per CU from an L2-resident (or HBM-sized) buffer:
+// every wave moves `iters` x 1 KiB.  mode 0: global_load_lds_dwordx4 (8 in flight per wave);
+// 1: global_load_dwordx4 to VGPRs + ds_write_b128; 2: global_load_dwordx4 only (summed).
+// mixed stream as the C4 projection sees it: per 3 KiB, 1 KiB from a streaming (HBM) buffer and
+// 2 KiB from a 2-MiB L2-resident one; DEPTH glds in flight per wave
+template <int DEPTH>
+__global__ __launch_bounds__(512) void dma_mix_kernel(const uint8_t* __restrict__ big, const uint8_t* __restrict__ hot,
+                                                      int iters, float* out) {
+    extern __shared__ __attribute__((aligned(1024))) char smem[];
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const size_t base = ((size_t)blockIdx.x * 8 + w) * (size_t)iters * 1024;
+    for (int i = 0; i < iters; ++i) {
+        const uint8_t* g = (i % 3 == 0) ? big + base + (size_t)i * 1024 + lane * 16
+                                        : hot + (((size_t)i * 1024 + (size_t)blockIdx.x * 8192) & ((2u << 20) - 1)) + lane * 16;
+        char* l = smem + (w * 16 + (i & 15)) * 1024;
+        __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)l, 16, 0, 0);
+        __builtin_amdgcn_s_waitcnt((DEPTH & 0xF) | ((DEPTH >> 4) << 14) | (0x7 << 4) | (0xF << 8));
+    }
+    __builtin_amdgcn_s_waitcnt((0x7 << 4) | (0xF << 8));
+    __syncthreads();
+    out[blockIdx.x * 512 + threadIdx.x] = ((float*)smem)[threadIdx.x];
+}
+
+template <int MODE>
+__global__ __launch_bounds__(512) void dma_bench_kernel(const uint8_t* __restrict__ src, size_t mask, int iters,
+                                                        float* out) {
+    extern __shared__ __attribute__((aligned(1024))) char smem[];
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    size_t base = ((size_t)blockIdx.x * 8 + w) * 1024 * 64;
+    uint4 accu = make_uint4(0, 0, 0, 0);
+    for (int i = 0; i < iters; ++i) {
+        const uint8_t* g = src + ((base + (size_t)i * 1024) & mask) + lane * 16;
+        char* l = smem + (w * 8 + (i & 7)) * 1024;
+        if constexpr (MODE == 0) {
+            __builtin_amdgcn_global_load_lds(g, (__attribute__((address_space(3))) void*)l, 16, 0, 0);
+            if ((i & 7) == 7) __builtin_amdgcn_s_waitcnt((0 & 0xF) | (0x7 << 4) | (0xF << 8));
+        } else if constexpr (MODE == 1) {
+            const uint4 v = *reinterpret_cast<const uint4*>(g);
+            *reinterpret_cast<uint4*>(l + lane * 16) = v;
+        } else {
+            const uint4 v = *reinterpret_cast<const uint4*>(g);
+            accu.x += v.x; accu.y ^= v.y; accu.z += v.z; accu.w ^= v.w;
+        }
+    }
+    __syncthreads();
+    if (MODE == 2) out[blockIdx.x * 512 + threadIdx.x] = (float)(accu.x + accu.y + accu.z + accu.w);
+    else out[blockIdx.x * 512 + threadIdx.x] = ((float*)smem)[threadIdx.x];
+}
+
+static void dma_bench() {
+    uint8_t* src;
+    const size_t big = (size_t)8 << 30;
+    CK(hipMalloc(&src, big));
+    CK(hipMemset(src, 1, big));
+    float* out;
+    CK(hipMalloc(&out, 256 * 512 * 4 * 4));
+    for (size_t foot : {(size_t)2 << 20, (size_t)8 << 30}) {
+        const int iters = 4096;
+        const double bytes = 256.0 * 8 * iters * 1024;
+        double t0 = time_us([&] { hipLaunchKernelGGL(dma_bench_kernel<0>, dim3(256), dim3(512), 65536, S, src, foot - 1, iters, out); });
+        double t1 = time_us([&] { hipLaunchKernelGGL(dma_bench_kernel<1>, dim3(256), dim3(512), 65536, S, src, foot - 1, iters, out); });
+        double t2 = time_us([&] { hipLaunchKernelGGL(dma_bench_kernel<2>, dim3(256), dim3(512), 65536, S, src, foot - 1, iters, out); });
+        printf("dma footprint %zu MiB: glds %.1f us (%.0f GB/s = %.1f B/clk/CU @2.1GHz)  load+ds_write %.1f us (%.0f GB/s)  load only %.1f us (%.0f GB/s)\n",
+               foot >> 20, t0, bytes / t0 / 1e3, bytes / t0 / 1e3 / 256 / 2.1, t1, bytes / t1 / 1e3, t2, bytes / t2 / 1e3);
+    }
+    {
+        const int iters = 3 * 1024;
+        const double bytes = 256.0 * 8 * iters * 1024;
+        auto run = [&](auto kern) {
+            return time_us([&] { hipLaunchKernelGGL(kern, dim3(256), dim3(512), 131072, S, src, src + ((size_t)7 << 30), iters, out); });
+        };
+        double t4 = run(dma_mix_kernel<4>), t8 = run(dma_mix_kernel<8>), t12 = run(dma_mix_kernel<12>), t15 = run(dma_mix_kernel<15>);
+        printf("dma mix (1/3 HBM stream, 2/3 L2): depth 4 %.0f GB/s, 8 %.0f GB/s, 12 %.0f GB/s, 15 %.0f GB/s (B/clk/CU @2.1GHz: %.1f %.1f %.1f %.1f)\n",
+               bytes / t4 / 1e3, bytes / t8 / 1e3, bytes / t12 / 1e3, bytes / t15 / 1e3, bytes / t4 / 1e3 / 537.6,
+               bytes / t8 / 1e3 / 537.6, bytes / t12 / 1e3 / 537.6, bytes / t15 / 1e3 / 537.6);
+    }
+    CK(hipFree(src));
+    CK(hipFree(out));
+}
+
 int main(int argc, char** argv) {
     const std::string what = argc > 1 ? argv[1] : "all";
     CK(hipStreamCreate(&S));
@@ -521,6 +601,7 @@ int main(int argc, char** argv) {
     if (what == "all" || what == "check") check_proj();
     if (what == "probe") probe_glds();
     if (what == "s8") check_s8();
+    if (what == "dma") dma_bench();
     CK(hipStreamDestroy(S));
     return 0;
 }
