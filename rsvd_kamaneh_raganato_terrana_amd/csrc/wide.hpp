@@ -32,6 +32,7 @@ struct WProjPlan {
     bool ds = false; // v2 TN at LP = 128 with two k-steps per stage (128-B A runs; K a multiple of 64)
     bool v3 = false; // v2 with launch-constant LDS read bases (bf16 A, LP 256 / 512; wide_proj.hip)
     int sd = 1;       // v3: S-panel prefetch distance in k-steps (1 or 2; A runs as far ahead as LDS allows)
+    bool tn2 = false; // v3 TN at LP = 256 with two k-steps per A slot (128-B A lines)
     int abl = 0;      // lab-only ablations of the v3 kernel (tools/wide_lab.cpp), never set by the engine
 };
 // v2 requires: a 16-B aligned base, bf16 A with lda and m multiples of 8 or e4m3 A with lda and m

@@ -917,6 +917,183 @@ hipError_t wproj3_go(const void* A, int64_t lda, int64_t m, int64_t n, const bf1
     return launch_sum_slabs<float>(slabs, stride, p.splits, stride, Out, s);
 }
 
+// v3 TN at LP = 256 with two k-steps per A slot: the A image of a slot is [WI j][64 i] (128-B
+// rows), so every A column contributes ONE full 128-B line per slot instead of two 64-B halves in
+// consecutive steps (v2's DS idea, affordable here because A and S have separate rings: A 2 x 32 KiB,
+// S 2 x 33 KiB per hi / lo pair).  Row j's 16-B unit u (rows 8 u .. 8 u + 7 of the 64) sits at unit
+// u ^ ((j >> 1) & 7): a ds_read_b128 of 16 lanes (rows r = 0..15, one unit) covers all 16 bank
+// positions.  The S images are v3's (32-step, row placement by sigma).
+template <bool SPLIT, int KN>
+__global__ __launch_bounds__(512) void wproj3tn2_kernel(const bf16_t* __restrict__ A, int64_t lda, int64_t rows_out,
+                                                        int64_t K, int64_t arows, const bf16_t* __restrict__ Shi,
+                                                        const bf16_t* __restrict__ Slo, float* __restrict__ out,
+                                                        int64_t slab_stride, int64_t kchunk, int nrowblk) {
+    constexpr int LP = 256;
+    typedef W3Shape<LP, false, SPLIT, 1> SH;
+    typedef typename SH::SImg SImg;
+    constexpr int WR = SH::WR, G = SH::G, WI = SH::WI, NS = SH::NS;
+    constexpr int ASLOT = WI * 128, APW2 = ASLOT / 1024 / 8;  // A slot bytes; pieces per wave
+    constexpr int SBASE = 2 * ASLOT;                           // [A 2 slots][S 2 slots]
+    extern __shared__ __attribute__((aligned(1024))) char smem_raw[];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int r = lane & 15, h = lane >> 4, q = r >> 2, p = r & 3;
+    const int wr = w % WR, wc = w / WR;
+    const int bid = xcd_remap(blockIdx.x, gridDim.x);
+    const int rb = bid % nrowblk, sp = bid / nrowblk;
+    const int64_t row0 = (int64_t)rb * WI;
+    const int64_t kbeg = (int64_t)sp * kchunk;
+    const int64_t kend = (kbeg + kchunk < K) ? kbeg + kchunk : K;
+    const int nsteps = (int)((kend - kbeg + KS - 1) / KS);
+    const int nd = (nsteps + 1) / 2;
+
+    int32_t soff[SH::SPW];
+#pragma unroll
+    for (int t = 0; t < SH::SPW; ++t) {
+        constexpr int LPR = 64 / SImg::RP;
+        const int pc = t * 8 + w;
+        soff[t] = SImg::row_of(pc, lane / LPR) * LP + 8 * (lane % LPR);
+    }
+    int64_t aoff[APW2];
+    int arow[APW2];
+#pragma unroll
+    for (int t = 0; t < APW2; ++t) {
+        const int u = (t * 8 + w) * 64 + lane, j = u >> 3, pu = u & 7;
+        int64_t jc = row0 + j;
+        jc = jc < rows_out ? jc : rows_out - 1;
+        const int i = 8 * (pu ^ ((j >> 1) & 7));
+        aoff[t] = jc * lda + i;
+        arow[t] = i;
+    }
+    auto issueS = [&](int st) {
+        char* slot = smem_raw + SBASE + (st & 1) * SH::SSLOT;
+        const int64_t k0 = kbeg + (int64_t)st * KS;
+#pragma unroll
+        for (int a = 0; a < NS; ++a) {
+            const bf16_t* S = (a ? Slo : Shi) + k0 * LP;
+#pragma unroll
+            for (int t = 0; t < SH::SPW; ++t) glds16(S + soff[t], slot + a * SH::SIMG + (t * 8 + w) * SImg::PITCH);
+        }
+    };
+    auto issueA = [&](int d) {
+        char* slot = smem_raw + (d & 1) * ASLOT;
+        const int64_t k0 = kbeg + (int64_t)d * 2 * KS;
+        const bool tail = k0 + 2 * KS > arows;
+#pragma unroll
+        for (int t = 0; t < APW2; ++t) {
+            const bf16_t* src = A + k0 + aoff[t];
+            if (tail && k0 + arow[t] + 8 > arows) src = A + (arows - 8 - arow[t]) + aoff[t];
+            glds16<(KN & 1) ? 2 : 0>(src, slot + (t * 8 + w) * 1024);
+        }
+    };
+
+    const int colS = wc * G * 16 + 4 * p;
+    const int k1 = 8 * h + q, k2 = k1 + 4;
+    const uint32_t lS1 = SImg::off(k1) + 2 * colS, lS2 = SImg::off(k2) + 2 * colS;
+    const int sw = (r >> 1) & 7;
+    const uint32_t lA0 = (wr * 64 + r) * 128 + 16 * (h ^ sw), lA1 = (wr * 64 + r) * 128 + 16 * ((4 + h) ^ sw);
+
+    f32x4 acc[RT][G];
+#pragma unroll
+    for (int t = 0; t < RT; ++t)
+#pragma unroll
+        for (int g = 0; g < G; ++g) acc[t][g] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    if (nsteps > 0) {
+        issueS(0);
+        issueA(0);
+    }
+    const uint32_t lds0 = lds_addr(smem_raw);
+    for (int st = 0; st < nsteps; ++st) {
+        const int d = st >> 1, hs = st & 1;
+        // step 2d needs A(d) and S(2d): nothing younger is in flight; step 2d + 1 needs S(2d + 1),
+        // issued before A(d + 1) in step 2d
+        if (hs == 0 || d + 1 >= nd) wait_vm<0>();
+        else wait_vm<SH::APW * 0 + APW2>();
+        __builtin_amdgcn_s_barrier();
+        if (st + 1 < nsteps) issueS(st + 1);
+        if (hs == 0 && d + 1 < nd) issueA(d + 1);
+        const uint32_t sS = lds0 + SBASE + (uint32_t)((st & 1) * SH::SSLOT);
+        const uint32_t sA = lds0 + (uint32_t)((d & 1) * ASLOT);
+        const uint32_t bS1 = sS + lS1, bS2 = sS + lS2, bA = sA + (hs ? lA1 : lA0);
+        auto wait_b = [&](i32x2* b) {
+            if (SPLIT) wait_lgkm0(b[0], b[1], b[2], b[3]);
+            else wait_lgkm0(b[0], b[1]);
+        };
+        i32x4 a4[RT];
+        bf16x8_t af[RT];
+        auto aread = [&](auto tc) {
+            constexpr int t = decltype(tc)::value;
+            a4[t] = read128_o<2048 * t>(bA);
+        };
+        static_for<RT>(aread);
+        auto bread = [&](auto gc, i32x2* b) {
+            constexpr int g = decltype(gc)::value;
+            b[0] = tr_read_o<32 * g>(bS1);
+            b[1] = tr_read_o<32 * g>(bS2);
+            if constexpr (SPLIT) {
+                b[2] = tr_read_o<SH::SIMG + 32 * g>(bS1);
+                b[3] = tr_read_o<SH::SIMG + 32 * g>(bS2);
+            }
+        };
+        i32x2 bb[2][4];
+        bread(std::integral_constant<int, 0>{}, bb[0]);
+        wait_b(bb[0]);
+#pragma unroll
+        for (int t = 0; t < RT; ++t) {
+            wait_lgkm0(a4[t]);
+            af[t] = __builtin_bit_cast(bf16x8_t, a4[t]);
+        }
+        auto gstep = [&](auto gc) {
+            constexpr int g = decltype(gc)::value;
+            if constexpr (g + 1 < G) bread(std::integral_constant<int, g + 1>{}, bb[(g + 1) & 1]);
+            __builtin_amdgcn_sched_barrier(0);
+            const i32x2* b = bb[g & 1];
+            const bf16x8_t bh = join2(b[0], b[1]);
+#pragma unroll
+            for (int t = 0; t < RT; ++t) acc[t][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[t], bh, acc[t][g], 0, 0, 0);
+            if constexpr (SPLIT) {
+                const bf16x8_t bl = join2(b[2], b[3]);
+#pragma unroll
+                for (int t = 0; t < RT; ++t) acc[t][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[t], bl, acc[t][g], 0, 0, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (g + 1 < G) wait_b(bb[(g + 1) & 1]);
+        };
+        static_for<G>(gstep);
+    }
+
+    float* dst = out + (int64_t)sp * slab_stride;
+#pragma unroll
+    for (int t = 0; t < RT; ++t)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int64_t row = row0 + wr * 64 + 16 * t + 4 * h + j;
+            if (row < rows_out) {
+#pragma unroll
+                for (int g = 0; g < G; ++g) dst[row * LP + wc * G * 16 + 16 * g + r] = acc[t][g][j];
+            }
+        }
+}
+
+template <bool SPLIT>
+hipError_t wproj3tn2_go(const void* A, int64_t lda, int64_t m, int64_t n, const bf16_t* Shi, const bf16_t* Slo,
+                        const WProjPlan& p, float* slabs, float* Out, hipStream_t s, hipEvent_t done) {
+    typedef W3Shape<256, false, SPLIT, 1> SH;
+    constexpr size_t lds = 2 * (size_t)SH::WI * 128 + 2 * (size_t)SH::SSLOT;
+    static_assert(lds <= 163840, "TN2 LDS");
+    const int64_t rows_out = n, K = m;
+    float* o = p.splits == 1 ? Out : slabs;
+    const int64_t stride = rows_out * 256;
+    hipLaunchKernelGGL((wproj3tn2_kernel<SPLIT, 0>), dim3(p.blocks * p.splits), dim3(512), lds, s,
+                       reinterpret_cast<const bf16_t*>(A), lda, rows_out, K, m, Shi, Slo, o, stride, p.chunk, p.blocks);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess && done) e = hipEventRecord(done, s);
+    if (e != hipSuccess || p.splits == 1) return e;
+    return launch_sum_slabs<float>(slabs, stride, p.splits, stride, Out, s);
+}
+
+
 template <bool FP8, bool NN, int LP, bool SPLIT, bool DS = false, bool S8 = false>
 hipError_t wproj2_go(const void* A, int64_t lda, int64_t m, int64_t n, const bf16_t* Shi, const bf16_t* Slo,
                      const WProjPlan& p, float* slabs, float* Out, hipStream_t s, hipEvent_t done) {
@@ -982,6 +1159,9 @@ hipError_t wproj_lp(int nn, int fp8, const void* A, int64_t lda, int64_t m, int6
                 }
             }
             if constexpr (LP == 256) {  // (LP = 512 split: a third S slot does not fit)
+                if (!nn && p.tn2 && p.sd == 1)
+                    return split ? wproj3tn2_go<true>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d)
+                                 : wproj3tn2_go<false>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d);
                 if (p.sd == 2) GO3(2);
             }
             GO3(1);
@@ -1026,6 +1206,7 @@ WProjPlan plan_wproj(int64_t rows_out, int64_t K, int LP, bool v2, bool nn, bool
     WProjPlan p;
     p.v2 = v2 && LP >= 128;
     p.v3 = p.v2 && !fp8 && (LP == 256 || LP == 512);
+    p.tn2 = p.v3 && !nn && LP == 256;  // two k-steps per A slot: K chunks of whole 64-row pairs
     p.ds = p.v2 && LP == 128 && !nn && !fp8 && K % 64 == 0;  // double-step TN stages (whole 64-row K chunks)
     const int WI = p.v2 ? (LP == 128 ? (p.ds ? 256 : 512) : (LP == 256 ? 256 : 128)) : wproj_rows_per_block(LP);
     p.blocks = (int)((rows_out + WI - 1) / WI);
@@ -1036,7 +1217,7 @@ WProjPlan plan_wproj(int64_t rows_out, int64_t K, int LP, bool v2, bool nn, bool
     if (splits > 128) splits = 128;
     if (splits < 1) splits = 1;
     int64_t chunk = (K + splits - 1) / splits;
-    const int kq = p.ds ? 2 * KS : KS;
+    const int kq = (p.ds || p.tn2) ? 2 * KS : KS;
     chunk = (chunk + kq - 1) / kq * kq;
     p.chunk = chunk;
     p.splits = (int)((K + chunk - 1) / chunk);

@@ -264,7 +264,7 @@ static void bench_proj(bool c4only = false) {
             WProjPlan pnn = plan_wproj(c.m, c.n, c.LP, v2 > 0), ptn = plan_wproj(c.n, c.m, c.LP, v2 > 0, false, c.fp8);
             if (v2 == 1) pnn.v3 = ptn.v3 = false;
             if (v2 >= 2 && !pnn.v3 && !ptn.v3) continue;
-            pnn.sd = ptn.sd = (v2 == 3) ? 2 : 1;
+            if (v2 == 3) ptn.tn2 = false;  // v3 TN with single-step A slots
             float* slabs;
             CK(hipMalloc(&slabs, (size_t)std::max<int64_t>(pnn.splits * c.m, ptn.splits * c.n) * c.LP * 4));
             const double bytes = (double)c.m * c.n * esz, fl = 2.0 * c.m * c.n * c.LP;
@@ -273,7 +273,7 @@ static void bench_proj(bool c4only = false) {
             double t3 = time_us([&] { CK(launch_wproj(0, c.fp8, A, c.m, c.m, c.n, Sh, Sl, c.LP, ptn, slabs, Out, S)); });
             printf("proj%s m=%ld n=%ld LP=%d fp8=%d: NN1 %.1f us (%.0f GB/s) NN2 %.1f us (%.0f GB/s, %.0f TF) TN2 %.1f us"
                    " (%.0f GB/s, %.0f TF) splits nn=%d tn=%d\n",
-                   v2 == 3 ? "v3sd2" : (v2 == 2 ? "v3" : (v2 ? "v2" : "v1")), (long)c.m, (long)c.n, c.LP, c.fp8, t1, bytes / t1 / 1e3, t2, bytes / t2 / 1e3,
+                   v2 == 3 ? "v3(tn1)" : (v2 == 2 ? "v3" : (v2 ? "v2" : "v1")), (long)c.m, (long)c.n, c.LP, c.fp8, t1, bytes / t1 / 1e3, t2, bytes / t2 / 1e3,
                    2 * fl / t2 / 1e6, t3, bytes / t3 / 1e3, 2 * fl / t3 / 1e6, pnn.splits, ptn.splits);
             CK(hipFree(slabs));
         }
@@ -372,7 +372,7 @@ static void check_proj() {  // v2 (LDS-DMA) against v1 on random bf16 / e4m3 dat
             const int64_t ro = nn ? m : n, K = nn ? n : m;
             WProjPlan p1 = plan_wproj(ro, K, LP, false, nn, fp8), p2 = plan_wproj(ro, K, LP, true, nn, fp8);
             for (int m32 = 0; m32 < 2; ++m32) {
-            p2.sd = 1 + m32;
+            if (m32) p2.tn2 = false;
             if (m32 && !p2.v3) continue;
             CK(launch_wproj(nn, fp8, A, m, m, n, Sh, Sl, LP, p1, sl, O1, S));
             CK(launch_wproj(nn, fp8, A, m, m, n, Sh, Sl, LP, p2, sl, O2, S));
@@ -386,7 +386,7 @@ static void check_proj() {  // v2 (LDS-DMA) against v1 on random bf16 / e4m3 dat
                 mx2 = std::max(mx2, (double)fabs(a[i]));
             }
             printf("check fp8=%d LP=%d %s%s: max|v1-v2| = %.3e (max|v1| = %.3e) v2 splits=%d chunk=%ld\n",
-                   fp8, LP, nn ? "NN" : "TN", m32 ? " v3sd2" : (p2.v3 ? " v3" : ""), md, mx2, p2.splits, (long)p2.chunk);
+                   fp8, LP, nn ? "NN" : "TN", m32 ? " v3(tn1)" : (p2.v3 ? (p2.tn2 ? " v3tn2" : " v3") : ""), md, mx2, p2.splits, (long)p2.chunk);
             }
         }
         CK(hipFree(A)); CK(hipFree(Sh)); CK(hipFree(Sl)); CK(hipFree(O1)); CK(hipFree(O2)); CK(hipFree(sl));
