@@ -250,9 +250,16 @@ def main():
         bound, achieved, peak, unit = "mfma", flop_launch / t_s / 1e12, PEAK_TFLOPS[dt], "TFLOP/s"
     key = f"{args.config}_{dt}_{m_local}x{n}_l{l}_q{q}"
     lowp = dt in ("bf16", "fp8")
-    if lowp:  # the LDS-DMA kernel wproj2_kernel<FP8, NN, LP, SPLIT> (hi/lo split skinny operand)
-        nn_k = "true" if kname.startswith("proj_nn") else "false"
-        kpref = f"wproj2_kernel<{'true' if dt == 'fp8' else 'false'}, {nn_k}, {lp_pad(l)}, true"  # [, DS]>
+    if lowp:  # the LDS-DMA kernels (hi/lo split skinny operand): wproj3 (bf16, LP 256 / 512; TN at
+        # LP 256 with two-step A slots: wproj3tn2), wproj2<FP8, NN, LP, SPLIT> otherwise
+        nn = kname.startswith("proj_nn")
+        LPk = lp_pad(l)
+        if dt == "bf16" and LPk == 256 and not nn:
+            kpref = "wproj3tn2_kernel<true"
+        elif dt == "bf16" and LPk in (256, 512):
+            kpref = f"wproj3_kernel<{'true' if nn else 'false'}, {LPk}, true"
+        else:
+            kpref = f"wproj2_kernel<{'true' if dt == 'fp8' else 'false'}, {'true' if nn else 'false'}, {LPk}, true"
     else:
         kpref = "proj_tn_kernel" if kname.startswith("proj_tn") else "proj_nn_kernel"
     tr = pmc_traffic(key, kpref)
