@@ -34,6 +34,7 @@ struct WProjPlan {
     int sd = 1;       // v3: S-panel prefetch distance in k-steps (1 or 2; A runs as far ahead as LDS allows)
     bool tn2 = false; // v3 TN at LP = 256 with two k-steps per A slot (128-B A lines)
     int abl = 0;      // lab-only ablations of the v3 kernel (tools/wide_lab.cpp), never set by the engine
+    int kn = -1;      // lab-only knob override of the LP = 256 v3 kernels (-1: the engine's choice)
 };
 // v2 requires: a 16-B aligned base, bf16 A with lda and m multiples of 8 or e4m3 A with lda and m
 // multiples of 16, and S panels zero-padded

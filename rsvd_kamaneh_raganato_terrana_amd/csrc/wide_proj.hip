@@ -909,8 +909,21 @@ hipError_t wproj3_go(const void* A, int64_t lda, int64_t m, int64_t n, const bf1
     float* o = p.splits == 1 ? Out : slabs;
     const int64_t stride = rows_out * LP;
     constexpr int KN = NN ? 3 : 0;  // as v2 (profiles/r02_wide_lab_knobs.txt)
-    hipLaunchKernelGGL((wproj3_kernel<NN, LP, SPLIT, KN, SD, ABL>), dim3(p.blocks * p.splits), dim3(512), SH::LDS, s,
-                       reinterpret_cast<const bf16_t*>(A), lda, rows_out, K, m, Shi, Slo, o, stride, p.chunk, p.blocks);
+    auto go = [&](auto knc) {
+        hipLaunchKernelGGL((wproj3_kernel<NN, LP, SPLIT, decltype(knc)::value, SD, ABL>), dim3(p.blocks * p.splits),
+                           dim3(512), SH::LDS, s, reinterpret_cast<const bf16_t*>(A), lda, rows_out, K, m, Shi, Slo, o,
+                           stride, p.chunk, p.blocks);
+    };
+    if constexpr (LP == 256 && ABL == 0 && SD == 1) {  // lab knob sweep (p.kn >= 0); the engine uses KN
+        switch (p.kn < 0 ? KN : p.kn) {
+            case 0: go(std::integral_constant<int, 0>{}); break;
+            case 1: go(std::integral_constant<int, 1>{}); break;
+            case 2: go(std::integral_constant<int, 2>{}); break;
+            default: go(std::integral_constant<int, 3>{}); break;
+        }
+    } else {
+        go(std::integral_constant<int, KN>{});
+    }
     hipError_t e = hipGetLastError();
     if (e == hipSuccess && done) e = hipEventRecord(done, s);
     if (e != hipSuccess || p.splits == 1) return e;
@@ -999,6 +1012,7 @@ __global__ __launch_bounds__(512) void wproj3tn2_kernel(const bf16_t* __restrict
 #pragma unroll
         for (int g = 0; g < G; ++g) acc[t][g] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+    if ((KN & 2) && w >= 4) __builtin_amdgcn_s_setprio(1);
     if (nsteps > 0) {
         issueS(0);
         issueA(0);
@@ -1085,8 +1099,17 @@ hipError_t wproj3tn2_go(const void* A, int64_t lda, int64_t m, int64_t n, const 
     const int64_t rows_out = n, K = m;
     float* o = p.splits == 1 ? Out : slabs;
     const int64_t stride = rows_out * 256;
-    hipLaunchKernelGGL((wproj3tn2_kernel<SPLIT, 0>), dim3(p.blocks * p.splits), dim3(512), lds, s,
-                       reinterpret_cast<const bf16_t*>(A), lda, rows_out, K, m, Shi, Slo, o, stride, p.chunk, p.blocks);
+    auto go = [&](auto knc) {
+        hipLaunchKernelGGL((wproj3tn2_kernel<SPLIT, decltype(knc)::value>), dim3(p.blocks * p.splits), dim3(512), lds, s,
+                           reinterpret_cast<const bf16_t*>(A), lda, rows_out, K, m, Shi, Slo, o, stride, p.chunk,
+                           p.blocks);
+    };
+    switch (p.kn < 0 ? 0 : p.kn) {  // KN 0 in the engine; the others for the lab knob sweep
+        case 1: go(std::integral_constant<int, 1>{}); break;
+        case 2: go(std::integral_constant<int, 2>{}); break;
+        case 3: go(std::integral_constant<int, 3>{}); break;
+        default: go(std::integral_constant<int, 0>{}); break;
+    }
     hipError_t e = hipGetLastError();
     if (e == hipSuccess && done) e = hipEventRecord(done, s);
     if (e != hipSuccess || p.splits == 1) return e;

@@ -578,6 +578,26 @@ int main(int argc, char** argv) {
     if (what == "all" || what == "jac") bench_jac();
     if (what == "all" || what == "proj") bench_proj();
     if (what == "proj4") bench_proj(true);
+    if (what == "kn") {  // v3 knob sweep at C4: bit 0 non-temporal A, bit 1 s_setprio on waves 4-7
+        const int64_t m = 65536, n = 65536;
+        const int LP = 256;
+        void* A;
+        CK(hipMalloc(&A, (size_t)m * n * 2));
+        hipLaunchKernelGGL(fill_random_kernel, dim3(4096), dim3(256), 0, S, (uint16_t*)A, (size_t)m * n, 0);
+        bf16_t* Sh = dev_random<bf16_t>((size_t)m * LP);
+        bf16_t* Sl = dev_random<bf16_t>((size_t)m * LP);
+        float* Out;
+        CK(hipMalloc(&Out, (size_t)m * LP * 4));
+        for (int rep = 0; rep < 2; ++rep)
+            for (int kn = 0; kn < 4; ++kn) {
+                WProjPlan pn = plan_wproj(m, n, LP, true), pt = plan_wproj(n, m, LP, true, false, false);
+                pn.kn = pt.kn = kn;
+                double t0 = time_us([&] { CK(launch_wproj(1, 0, A, m, m, n, Sh, nullptr, LP, pn, nullptr, Out, S)); });
+                double t1 = time_us([&] { CK(launch_wproj(1, 0, A, m, m, n, Sh, Sl, LP, pn, nullptr, Out, S)); });
+                double t2 = time_us([&] { CK(launch_wproj(0, 0, A, m, m, n, Sh, Sl, LP, pt, nullptr, Out, S)); });
+                printf("rep %d kn %d: NN1 %.1f us  NN2 %.1f us  TN2 %.1f us\n", rep, kn, t0, t1, t2);
+            }
+    }
     if (what == "abl") {  // v3 ablations at C4 (timing only; results meaningless)
         const int64_t m = 65536, n = 65536;
         const int LP = 256;
