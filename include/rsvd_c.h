@@ -73,6 +73,15 @@ typedef enum {
  * CHOLQR2 = two CholeskyQR passes on every panel. */
 typedef enum { RSVD_QR_AUTO = 0, RSVD_QR_GS2 = 1, RSVD_QR_CHOLQR2 = 2 } rsvd_qr_mode_t;
 
+/* rsvd_desc_t.flags.  LOWP_INTERMEDIATES (bf16 / e4m3 A, q >= 2): the two projections of power
+ * iterations 1 .. q-1 take the fp32 skinny operand as its bf16 rounding alone (one MFMA pass
+ * instead of the hi + lo pair); the last iteration, B^T = A^T Q and the outputs keep 16-bit
+ * operands.  An error injected there is damped by the later iterations by about
+ * (sigma_{l+1} / sigma_{l/2})^2 each: on spectra that decay across the sketch (e.g. 0.985^i at
+ * l = 256) the results stay within 1e-5 of the full-precision path, on flat ones (0.999^i) they
+ * drift to ~5e-3.  Off by default. */
+#define RSVD_FLAG_LOWP_INTERMEDIATES 1
+
 typedef struct {
     int64_t m, n;              /* A is m x n                                                   */
     int64_t lda;               /* >= m                                                         */
@@ -81,7 +90,7 @@ typedef struct {
     int32_t dtype;             /* rsvd_dtype_t                                                 */
     int32_t method;            /* rsvd_svd_method_t                                            */
     int32_t qr_mode;           /* rsvd_qr_mode_t                                               */
-    int32_t reserved;
+    int32_t flags;             /* RSVD_FLAG_* (ABI 5; the former reserved word, 0 = defaults)  */
     uint64_t seed;             /* Philox key for Omega when no Omega is supplied               */
     double a_scale;            /* A = a_scale * (stored A); 0 means 1 (any dtype; S scales by
                                   |a_scale|, V flips sign when a_scale < 0)                        */

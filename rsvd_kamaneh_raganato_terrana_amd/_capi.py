@@ -29,6 +29,7 @@ STATUS = {
 F64, F32, BF16, FP8_E4M3 = 0, 1, 2, 3
 SVD_JACOBI, SVD_POWER, SVD_PARALLEL_JACOBI, SVD_POWER_IC = 0, 1, 2, 3
 QR_AUTO, QR_GS2, QR_CHOLQR2 = 0, 1, 2
+FLAG_LOWP_INTERMEDIATES = 1
 
 # Every symbol include/rsvd_c.h declares (checked by tests/test_capi_exports.py).
 EXPORTS = (
@@ -45,7 +46,7 @@ class Desc(ctypes.Structure):
     _fields_ = [
         ("m", ctypes.c_int64), ("n", ctypes.c_int64), ("lda", ctypes.c_int64),
         ("l", ctypes.c_int32), ("q", ctypes.c_int32), ("dtype", ctypes.c_int32),
-        ("method", ctypes.c_int32), ("qr_mode", ctypes.c_int32), ("reserved", ctypes.c_int32),
+        ("method", ctypes.c_int32), ("qr_mode", ctypes.c_int32), ("flags", ctypes.c_int32),
         ("seed", ctypes.c_uint64), ("a_scale", ctypes.c_double),
     ]
 

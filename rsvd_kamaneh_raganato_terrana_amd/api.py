@@ -248,23 +248,26 @@ class Engine:
         return t_dtype if t_dtype in (torch.float64, torch.float32) else torch.float32
 
     def desc(self, A, l: int, q: int = 2, method: int = SVDMethod.Jacobi, seed: int = 0,
-             qr_mode: int = QRMode.Auto, a_scale: float = 1.0) -> Desc:
+             qr_mode: int = QRMode.Auto, a_scale: float = 1.0, flags: int = 0) -> Desc:
         dt = self.abi_dtype(A.dtype)
         lda = A.stride(1) if A.stride(0) == 1 else None
         if lda is None:
             raise ValueError("A must be column-major (use colmajor())")
         return Desc(m=A.shape[0], n=A.shape[1], lda=max(lda, A.shape[0]), l=l, q=q, dtype=dt,
-                    method=int(method), qr_mode=int(qr_mode), reserved=0, seed=seed, a_scale=a_scale)
+                    method=int(method), qr_mode=int(qr_mode), flags=int(flags), seed=seed, a_scale=a_scale)
 
     def rsvd(self, A, l: int, q: int = 2, method: int = SVDMethod.Jacobi, omega=None, seed: int = 0,
-             qr_mode: int = QRMode.Auto, out=None, a_scale: float = 1.0, check_errors: bool = True):
+             qr_mode: int = QRMode.Auto, out=None, a_scale: float = 1.0, check_errors: bool = True,
+             lowp_intermediates: bool = False):
         """Device rSVD: A (m x n, CUDA, column-major f64/f32/bf16/e4m3) -> U (m x l), S (l), V (n x l).
 
         check_errors=True synchronises and raises on the run's device-side failures (rsvd_sync);
-        False leaves the run queued (asynchronous) -- call sync() later to check."""
+        False leaves the run queued (asynchronous) -- call sync() later to check.
+        lowp_intermediates: RSVD_FLAG_LOWP_INTERMEDIATES (include/rsvd_c.h; bf16 / e4m3 A, q >= 2)."""
         torch = _torch()
         A, _ = colmajor(A)
-        d = self.desc(A, l, q, method, seed, qr_mode, a_scale)
+        d = self.desc(A, l, q, method, seed, qr_mode, a_scale,
+                      _capi.FLAG_LOWP_INTERMEDIATES if lowp_intermediates else 0)
         self.reserve(d)
         self._bind_stream()
         m, n = A.shape

@@ -74,6 +74,7 @@ int check_desc_msg(const rsvd_desc_t* d, const char** err) {
     }
     if (d->dtype < RSVD_F64 || d->dtype > RSVD_FP8_E4M3) { *err = "unsupported dtype"; return RSVD_ERR_UNSUPPORTED; }
     if (d->qr_mode < RSVD_QR_AUTO || d->qr_mode > RSVD_QR_CHOLQR2) { *err = "bad qr_mode"; return RSVD_ERR_INVALID_ARG; }
+    if (d->flags & ~RSVD_FLAG_LOWP_INTERMEDIATES) { *err = "unknown flags"; return RSVD_ERR_INVALID_ARG; }
     if (d->method != RSVD_SVD_JACOBI && d->method != RSVD_SVD_PARALLEL_JACOBI && d->method != RSVD_SVD_POWER &&
         d->method != RSVD_SVD_POWER_IC) {
         *err = "Unsupported SVD method";  // src/rSVD.cpp:123 wording

@@ -148,6 +148,7 @@ struct WideEngine {
     int* colflag;
     unsigned* sync;
     int inter_passes = 1;  // power-iteration intermediates only carry a subspace (driver.cpp)
+    bool lowp_inter = false;  // RSVD_FLAG_LOWP_INTERMEDIATES
     int qr_mode = RSVD_QR_AUTO;
     int orth_index = 0;
     // Repair draws of the m side: rank g's rows are stream rows [g 2^40, g 2^40 + m_g) of a
@@ -348,10 +349,12 @@ struct WideEngine {
         RSVD_TRY(orth(Ym, true, Qm, q == 0 ? 2 : inter_passes, Qh, Ql, q == 0));
         for (int i = 0; i < q; ++i) {
             const bool last = i == q - 1;
-            RSVD_TRY(proj_tn(A, lda, Qm, Qh, Ql, Zn));
+            // RSVD_FLAG_LOWP_INTERMEDIATES: iterations before the last take the bf16 operand alone
+            const bool one = L.lowp && lowp_inter && !last;
+            RSVD_TRY(proj_tn(A, lda, Qm, Qh, one ? nullptr : Ql, Zn));
             RSVD_TRY(orth(Zn, false, Xn, inter_passes, Xh, Xl, false));
             RSVD_TRY(gather_x());
-            RSVD_TRY(proj_nn(A, lda, Xn, Xh, Xl, Ym));
+            RSVD_TRY(proj_nn(A, lda, Xn, Xh, one ? nullptr : Xl, Ym));
             RSVD_TRY(orth(Ym, true, Qm, last ? 2 : inter_passes, Qh, Ql, last));
         }
         return RSVD_OK;
@@ -455,6 +458,7 @@ int wide_typed(rsvd_handle_t h, const rsvd_desc_t* d, const void* A, const void*
     h->info.splits_tn = L.lowp ? L.wtn.splits : L.ptn.splits;
     WideEngine<T> E(h, L, d->dtype);
     E.qr_mode = d->qr_mode;
+    E.lowp_inter = (d->flags & RSVD_FLAG_LOWP_INTERMEDIATES) != 0;
     E.seed = d->seed;
     E.nsh = L.nsh;
     E.c0 = L.nsh ? (int64_t)h->rank * L.nc : 0;

@@ -73,7 +73,7 @@ def test_row_partition_matches_reference_split(lib, rows, world):
 
 
 def _desc(**kw):
-    d = dict(m=4096, n=4096, lda=4096, l=64, q=2, dtype=_capi.F32, method=0, qr_mode=0, reserved=0, seed=0)
+    d = dict(m=4096, n=4096, lda=4096, l=64, q=2, dtype=_capi.F32, method=0, qr_mode=0, flags=0, seed=0)
     d.update(kw)
     return _capi.Desc(**d)
 
@@ -90,8 +90,9 @@ def test_workspace_bytes_and_argument_checks(lib):
     assert nb64.value > nb.value
     # 1 = RSVD_ERR_INVALID_ARG, 2 = RSVD_ERR_UNSUPPORTED
     for bad, code in ((dict(l=0), 1), (dict(q=-1), 1), (dict(lda=100), 1), (dict(l=513), 2), (dict(m=10, l=16), 2),
-                      (dict(dtype=7), 2), (dict(method=7), 2)):
+                      (dict(dtype=7), 2), (dict(method=7), 2), (dict(flags=2), 1)):
         assert lib.rsvd_workspace_bytes(ctypes.byref(_desc(**bad)), ctypes.byref(nb)) == code, bad
+    assert lib.rsvd_workspace_bytes(ctypes.byref(_desc(flags=_capi.FLAG_LOWP_INTERMEDIATES)), ctypes.byref(nb)) == 0
     # the wide engine (l > 64, bf16 / e4m3 A): l-wide panels, bf16 hi/lo copies, slabs -- O((m + n) l)
     for dt, l in ((_capi.F32, 128), (_capi.BF16, 256), (_capi.FP8_E4M3, 512), (_capi.F64, 100)):
         assert lib.rsvd_workspace_bytes(ctypes.byref(_desc(dtype=dt, l=l)), ctypes.byref(nb)) == 0, (dt, l)

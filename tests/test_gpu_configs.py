@@ -121,3 +121,22 @@ def test_host_entry_point_reports_non_finite(engine):
     A[3, 3] = np.inf
     with pytest.raises(RSVDError, match="numerical"):
         engine.rsvd_host(A, 8, q=1)
+
+
+def test_lowp_intermediates_flag(engine):
+    """RSVD_FLAG_LOWP_INTERMEDIATES (include/rsvd_c.h): power iteration 1 of q = 2 on the bf16
+    operand alone.  On a spectrum that decays across the sketch (0.985^i, l = 256) the error it
+    injects is damped by the last iteration: the result stays within the 1e-4 bar of the oracle
+    and within 1e-4 of the full-precision path (DESIGN.md §3.2 has the flat-spectrum limit)."""
+    torch = _torch()
+    m, n, l = 4096, 2048, 256
+    A32 = gapped_matrix(m, n, 2 * l, decay=0.985, seed=17).astype(np.float32) * 4
+    Ad = _dev_colmajor(A32, torch.bfloat16)
+    A_exact = Ad.float().cpu().double().numpy()
+    Om = engine.generate_omega(n, l, seed=99, dtype=torch.bfloat16).cpu().double().numpy()
+    Uo, So, Vo = oracle.rsvd(A_exact, l, q=2, Omega=Om)
+    U, S, V = engine.rsvd(Ad, l, q=2, seed=99, lowp_intermediates=True)
+    U, S, V = (x.cpu().double().numpy() for x in (U, S, V))
+    _check(U, S, V, Uo, So, Vo, A_exact, 1e-4, 1e-3)
+    U2, S2, V2 = engine.rsvd(Ad, l, q=2, seed=99)
+    assert rel_fro(S, S2.cpu().double().numpy()) < 1e-4
