@@ -75,6 +75,9 @@ hipError_t launch_gram_wide(const T* P, const T* P2, int64_t rows, int LP, const
 // Also writes Rinv as fp32 when Rinv32 != nullptr.  `work`: LP x LP fp64.  `pred`: as above.
 hipError_t launch_chol_wide(const double* G, int l, int LP, double tol, double* R, double* Rinv, float* Rinv32,
                             int* colflag, int* flag, double* work, const int* pred, hipStream_t s);
+// 1 (default): chol_reg_kernel for LP <= 128, chol_wide_kernel above; 0: chol_wide_kernel everywhere;
+// 2: also chol_reg_kernel at LP = 256 (lab A/B only).
+extern int chol_variant;
 // Out (rows x LP) = In (rows x LP) * M (LP x LP, row-major, in the panel precision T; `upper`:
 // only k <= c of M is read).  Out layouts: row-major panel (ldo = 0) or the caller's column-major matrix (first
 // `cols` columns, leading dimension ldo).  Optionally also writes the bf16 hi / lo panels of Out

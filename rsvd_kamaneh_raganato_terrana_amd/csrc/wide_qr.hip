@@ -343,15 +343,23 @@ __device__ __forceinline__ double rsqrt_nr(double d) {
     return y;
 }
 
-// Wave-level factor of the 16x16 diagonal block p (lane j: col[i] = D[i][j], upper part valid):
-// R block and D^-1 block to global (R, Rinv diagonal blocks) and D^-1 to the LDS buffer Di;
-// breakdown rows to bad[16] and the flags.
-__device__ __forceinline__ void chol_diag16(double (&col)[16], int p16, int l, int LP, double tol,
-                                            const double* d0, double* Di, int* bad, double* R, double* Rinv,
-                                            int* colflag, int* flag, int lane) {
+// Wave-level factor of a 16x16 diagonal block for the single-wave critical path of the block
+// Cholesky (lane j: col[i] = T[i][j]; the upper part is valid).  Measured: the predicated form
+// (`if (j >= i) col[i] -= ...`) followed by a separate back substitution ran 6 us per block, a
+// dependent chain of ~2000 VALU/readlane instructions on one wave.  Here every update is
+// unconditional (lanes j < i only carry lower-triangle values no later step reads), and D^-1 is
+// formed in the same pivot loop: row k of Y = D^-T (lane j: Y[k][j] = D^-1[j][k]) is
+// (e_j[k] - acc[k]) / D[k][k], and each broadcast D[k][i] feeds both the factor update and
+// acc[i] += D[k][i] Y[k][j] -- one readlane per element for both.  Writes the R and R^-1 diagonal
+// blocks (global), D^-1 (Di, LDS, row-major), the breakdown rows (bad) and flags.
+__device__ __forceinline__ void chol_diag16_fast(double (&col)[16], int p16, int l, int LP, double tol,
+                                                 const double* d0, double* Di, int* bad, double* R, double* Rinv,
+                                                 int* colflag, int* flag, int lane) {
     const int j = lane & 15;
     int badmask = 0;
-    double inv[16];
+    double acc[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.0;
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
         const int gk = p16 + k;
@@ -361,36 +369,33 @@ __device__ __forceinline__ void chol_diag16(double (&col)[16], int p16, int l, i
         if (isbad) badmask |= 1 << k;
         const bool unit = pad || isbad;
         const double y = unit ? 1.0 : rsqrt_nr(dkk);
-        inv[k] = y;
         const double rk = unit ? 1.0 : dkk * y;
-        if (j > k) col[k] = unit ? 0.0 : col[k] * y;
-        if (j == k) col[k] = rk;
+        const double v = unit ? 0.0 : col[k] * y;
+        col[k] = (j == k) ? rk : v;
+        const double yk = ((j == k ? 1.0 : 0.0) - acc[k]) * y;  // Y[k][j] = D^-1[j][k]
+        if (lane < 16) Di[j * 16 + k] = yk;
 #pragma unroll
         for (int i = k + 1; i < 16; ++i) {
             const double dki = readlane_d(col[k], i);  // D[k][i]
-            if (j >= i) col[i] -= dki * col[k];
+            col[i] = fma(-dki, col[k], col[i]);
+            acc[i] = fma(dki, yk, acc[i]);
         }
     }
 #pragma unroll
     for (int i = 0; i < 16; ++i)
         if (i > j) col[i] = 0.0;
-    // D^-1 column j by back substitution: x[i] = -(sum_{k>i} D[i][k] x[k]) / D[i][i]
-    double x[16];
-#pragma unroll
-    for (int i = 15; i >= 0; --i) {
-        double s = 0.0;
-#pragma unroll
-        for (int k = i + 1; k < 16; ++k) s += readlane_d(col[i], k) * x[k];  // D[i][k] from lane k
-        x[i] = (i == j) ? inv[i] : ((i < j) ? -s * inv[i] : 0.0);
-    }
     if (lane < 16) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            Di[i * 16 + j] = x[i];
-            Rinv[(int64_t)(p16 + i) * LP + p16 + j] = x[i];
-            R[(int64_t)(p16 + i) * LP + p16 + j] = col[i];
-        }
+        for (int i = 0; i < 16; ++i) R[(int64_t)(p16 + i) * LP + p16 + j] = col[i];
         bad[lane] = (badmask >> lane) & 1;
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's D^-1 rows landed
+    __builtin_amdgcn_wave_barrier();
+    if (lane < 16) {
+#pragma unroll
+        for (int i = 0; i < 16; i += 2)
+            *reinterpret_cast<double2*>(Rinv + (int64_t)(p16 + j) * LP + p16 + i) =
+                *reinterpret_cast<const double2*>(Di + j * 16 + i);
     }
     if (lane == 0 && badmask) {
         atomicAdd(flag, __popc(badmask));
@@ -560,8 +565,10 @@ __global__ __launch_bounds__(kCholThreads) void chol_wide_kernel(const double* _
                 double col[16];
 #pragma unroll
                 for (int i = 0; i < 16; ++i) col[i] = Tsc[i * 16 + r];
-                chol_diag16(col, 16 * b1, l, LP, tol, d0, Dd + (b1 & 1) * 256, bad + (b1 & 1) * 16, R, Rinv,
-                            colflag, flag, lane);
+                __builtin_amdgcn_s_waitcnt(0xc07f);
+                __builtin_amdgcn_wave_barrier();
+                chol_diag16_fast(col, 16 * b1, l, LP, tol, d0, Dd + (b1 & 1) * 256, bad + (b1 & 1) * 16, R, Rinv,
+                                 colflag, flag, lane);
             } else if (p >= 0) {
                 // local tile t of the (nt2 x nt2) upper triangle; t = 0 is wave 0's
                 TriWalk tw(wv, nt2);
@@ -612,6 +619,169 @@ __global__ __launch_bounds__(kCholThreads) void chol_wide_kernel(const double* _
 
 size_t chol_lds_bytes(int LP) {
     return (size_t)512 * 8 + (size_t)LP * 8 + (size_t)16 * (LP + kCholPad) * 8 + 256 * 8 + 32 * 4 + 64;
+}
+
+// ------------------------------------------------------------------------------------------------
+// Register-resident Cholesky (LP <= 256).  chol_wide_kernel keeps the Gram being reduced in global
+// memory (L2), so every block step pays two L2 round trips per tile on top of its barriers
+// (10 us per 16-column step at LP = 256).  Here the upper block triangle of G lives in the
+// REGISTERS of one 512-thread workgroup: upper-triangle tile t (row-major order) belongs to wave
+// t % 8, slot t / 8, in MFMA output layout (lane (r, h): rows h + 4 j, column r) -- LP = 256 is 136
+// tiles, 17 slots = 136 VGPRs per lane.  Row-major dealing spreads every tile row over consecutive
+// waves, so the trailing triangle of each step is balanced to one tile per row.  Per block step p:
+//   (A) the owner of tile (p, p) factors it (16x16 upper Cholesky + inverse, lane j owning column j),
+//       D^-1 to LDS;                                                              -- barrier
+//   (B) the owners of row p form the strip R[p][jb] = D_p^-T W[p][jb] (4 MFMAs), to R and to LDS;
+//                                                                                 -- barrier
+//   (C) every wave updates its trailing tiles W[ib][jb] -= R[p][ib]^T R[p][jb] from the LDS strip.
+// (C) of step p and (A) of step p + 1 touch only the owner's registers, so two barriers per step.
+// Same operations in the same order as chol_wide_kernel: bit-identical R.
+constexpr int kCholRegWaves = 8;
+
+template <int NP> struct CholReg {
+    static constexpr int LP = 16 * NP, NW = kCholRegWaves, NT = NP * (NP + 1) / 2, S = (NT + NW - 1) / NW;
+    // the first SL slots of every wave (rows retired earliest) live in LDS: VGPR budget at 2 waves/SIMD
+    static constexpr int SL = S > 10 ? S - 10 : 0;
+    static constexpr int LDR = LP + kCholPad;
+    static constexpr size_t lds_bytes = (size_t)(512 + 256 + LP + 16 * LDR + NW * SL * 256) * 8 + 32 * 4;
+};
+
+template <int NP>
+__global__ __launch_bounds__(64 * kCholRegWaves) void chol_reg_kernel(const double* __restrict__ G, int l, double tol,
+                                                                      double* __restrict__ R, double* __restrict__ Rinv,
+                                                                      int* __restrict__ colflag, int* __restrict__ flag,
+                                                                      const int* __restrict__ pred) {
+    if (pred && *pred == 0) return;
+    typedef CholReg<NP> C;
+    constexpr int LP = C::LP, NW = C::NW, NT = C::NT, S = C::S, SL = C::SL, LDR = C::LDR;
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    double* Di = reinterpret_cast<double*>(smem_raw);  // [2][256]
+    double* Tsc = Di + 512;                            // [256]
+    double* d0 = Tsc + 256;                            // [LP]
+    double* Rs = d0 + LP;                              // [16][LDR]
+    double* wl = Rs + 16 * LDR;                        // [NW][SL][64 lanes][4]
+    int* bad = reinterpret_cast<int*>(wl + NW * SL * 256);  // [2][16]
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int r = lane & 15, h = lane >> 4;
+    double* wlw = wl + wv * SL * 256 + lane * 4;
+    CHOL_TS(97);
+
+    int tib[S], tjb[S];
+    double wt[S - SL > 0 ? S - SL : 1][4];
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+        tib[s] = NP;  // empty slot: never active
+        tjb[s] = NP;
+        const int t = s * NW + wv;
+        if (t < NT) tri_decode(t, NP, tib[s], tjb[s]);
+        double v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int i = 16 * tib[s] + h + 4 * j, c = 16 * tjb[s] + r;
+            v[j] = (t < NT && i < l && c < l) ? G[(int64_t)i * LP + c] : 0.0;
+        }
+        if (s < SL) {
+            *reinterpret_cast<double2*>(wlw + s * 256) = make_double2(v[0], v[1]);
+            *reinterpret_cast<double2*>(wlw + s * 256 + 2) = make_double2(v[2], v[3]);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) wt[s < SL ? 0 : s - SL][j] = v[j];
+        }
+    }
+    auto get = [&](int s, double (&v)[4]) {
+        if (s < SL) {
+            const double2 a = *reinterpret_cast<const double2*>(wlw + s * 256);
+            const double2 b = *reinterpret_cast<const double2*>(wlw + s * 256 + 2);
+            v[0] = a.x; v[1] = a.y; v[2] = b.x; v[3] = b.y;
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) v[j] = wt[s < SL ? 0 : s - SL][j];
+        }
+    };
+    for (int i = tid; i < LP; i += 64 * NW) {
+        d0[i] = (i < l) ? G[(int64_t)i * LP + i] : 0.0;
+        colflag[i] = 0;
+    }
+    __syncthreads();
+    CHOL_TS(200);
+
+    for (int p = 0; p < NP; ++p) {
+        const int p16 = 16 * p;
+        // (A) factor the diagonal tile (p, p) on its owner wave
+        const int tpp = p * NP - p * (p - 1) / 2;
+        if (wv == tpp % NW) {
+            const int sp = tpp / NW;
+#pragma unroll
+            for (int s = 0; s < S; ++s)
+                if (s == sp) {
+                    double v[4];
+                    get(s, v);
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) Tsc[(h + 4 * j) * 16 + r] = v[j];
+                }
+            __builtin_amdgcn_s_waitcnt(0xc07f);
+            __builtin_amdgcn_wave_barrier();
+            double col[16];
+#pragma unroll
+            for (int i = 0; i < 16; ++i) col[i] = Tsc[i * 16 + r];
+            __builtin_amdgcn_s_waitcnt(0xc07f);
+            __builtin_amdgcn_wave_barrier();
+            chol_diag16_fast(col, p16, l, LP, tol, d0, Di + (p & 1) * 256, bad + (p & 1) * 16, R, Rinv,
+                            colflag, flag, lane);
+        }
+        __syncthreads();
+        if (p < 32) CHOL_TS(1 + 3 * p);
+        if (p == NP - 1) break;
+        // (B) strip R[p][jb] = D_p^-T W[p][jb] (0 for rows that broke down or are padding)
+        {
+            const double* Dp = Di + (p & 1) * 256;
+            const int* bd = bad + (p & 1) * 16;
+            double x[4];
+#pragma unroll
+            for (int kk = 0; kk < 4; ++kk) x[kk] = Dp[(4 * kk + h) * 16 + r];
+            int zero_rows = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) zero_rows |= (bd[h + 4 * j] || p16 + h + 4 * j >= l) << j;
+#pragma unroll
+            for (int s = 0; s < S; ++s)
+                if (tib[s] == p && tjb[s] > p) {
+                    double v[4];
+                    get(s, v);
+                    f64x4 acc = MD::zero();
+#pragma unroll
+                    for (int kk = 0; kk < 4; ++kk) acc = MD::mma(x[kk], v[kk], acc);
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const int i = h + 4 * j;
+                        const double o = ((zero_rows >> j) & 1) ? 0.0 : acc[j];
+                        R[(int64_t)(p16 + i) * LP + 16 * tjb[s] + r] = o;
+                        Rs[i * LDR + 16 * tjb[s] + r] = o;
+                    }
+                }
+        }
+        __syncthreads();
+        if (p < 32) CHOL_TS(2 + 3 * p);
+        // (C) trailing update of the tiles below row p
+#pragma unroll
+        for (int s = 0; s < S; ++s)
+            if (tib[s] > p && tib[s] < NP) {
+                f64x4 acc = MD::zero();
+#pragma unroll
+                for (int kk = 0; kk < 4; ++kk)
+                    acc = MD::mma(Rs[(4 * kk + h) * LDR + 16 * tib[s] + r], Rs[(4 * kk + h) * LDR + 16 * tjb[s] + r], acc);
+                if (s < SL) {
+                    double v[4];
+                    get(s, v);
+                    *reinterpret_cast<double2*>(wlw + s * 256) = make_double2(v[0] - acc[0], v[1] - acc[1]);
+                    *reinterpret_cast<double2*>(wlw + s * 256 + 2) = make_double2(v[2] - acc[2], v[3] - acc[3]);
+                } else {
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) wt[s < SL ? 0 : s - SL][j] -= acc[j];
+                }
+            }
+        if (p < 32) CHOL_TS(3 + 3 * p);
+    }
 }
 
 // R^-1 = blocked back substitution, one workgroup (4 waves) per 16-column block jb, all block
@@ -1004,11 +1174,26 @@ hipError_t launch_gram_wide(const T* P, const T* P2, int64_t rows, int LP, const
     return hipGetLastError();
 }
 
+int chol_variant = 1;
+
 hipError_t launch_chol_wide(const double* G, int l, int LP, double tol, double* R, double* Rinv, float* Rinv32,
                             int* colflag, int* flag, double* work, const int* pred, hipStream_t s) {
     if (LP % 16 || LP > 512) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(chol_wide_kernel, dim3(1), dim3(kCholThreads), chol_lds_bytes(LP), s, G, l, LP, tol, work, R,
-                       Rinv, colflag, flag, pred);
+    // LP = 256: chol_wide_kernel (its wave-0 look-ahead overlaps the diagonal factor with the other waves'
+    // updates; the register-resident kernel spills there, 174 vs 161 us measured); LP <= 128: chol_reg_kernel
+    // (LP = 128: 63 vs 71 us, LP = 64: 31 vs 37 us, tools/wide_lab chol)
+    if (chol_variant >= 1 && LP == 128)
+        hipLaunchKernelGGL(chol_reg_kernel<8>, dim3(1), dim3(64 * kCholRegWaves), CholReg<8>::lds_bytes, s, G, l, tol,
+                           R, Rinv, colflag, flag, pred);
+    else if (chol_variant >= 1 && LP == 64)
+        hipLaunchKernelGGL(chol_reg_kernel<4>, dim3(1), dim3(64 * kCholRegWaves), CholReg<4>::lds_bytes, s, G, l, tol,
+                           R, Rinv, colflag, flag, pred);
+    else if (chol_variant == 2 && LP == 256)  // lab only
+        hipLaunchKernelGGL(chol_reg_kernel<16>, dim3(1), dim3(64 * kCholRegWaves), CholReg<16>::lds_bytes, s, G, l,
+                           tol, R, Rinv, colflag, flag, pred);
+    else
+        hipLaunchKernelGGL(chol_wide_kernel, dim3(1), dim3(kCholThreads), chol_lds_bytes(LP), s, G, l, LP, tol, work,
+                           R, Rinv, colflag, flag, pred);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(rinv_wide_kernel, dim3(LP / 16), dim3(256), 0, s, LP, R, Rinv, Rinv32, pred);
@@ -1107,8 +1292,22 @@ void chol_prof_dump(int LP) {
         trail += (t[2 + 2 * p] - t[1 + 2 * p]) * us;
         prev = t[2 + 2 * p];
     }
-    printf("  LP=%d factor phases (us): init+diag0 %.1f strip %.1f trailing+diag %.1f\n", LP, (t[0] - t[97]) * us,
-           strip, trail);
+    if (chol_variant == 0) {
+        printf("  LP=%d factor phases (us): init+diag0 %.1f strip %.1f trailing+diag %.1f\n", LP, (t[0] - t[97]) * us,
+               strip, trail);
+        return;
+    }
+    double A = 0, B = 0, Cc = 0;
+    prev = t[200];
+    for (int p = 0; p < np && p < 32; ++p) {
+        A += (t[1 + 3 * p] - prev) * us;
+        if (p == np - 1) break;
+        B += (t[2 + 3 * p] - t[1 + 3 * p]) * us;
+        Cc += (t[3 + 3 * p] - t[2 + 3 * p]) * us;
+        prev = t[3 + 3 * p];
+    }
+    printf("  LP=%d reg phases (us, wave 0): init %.1f  diag+wait %.1f  strip %.1f  update %.1f\n", LP,
+           (t[200] - t[97]) * us, A, B, Cc);
 }
 }  // namespace rsvd
 #endif

@@ -149,7 +149,15 @@ static void bench_chol() {
         CK(hipMalloc(&cf, LP * 4));
         CK(hipMalloc(&fl, 4));
         CK(hipMemset(fl, 0, 4));
+        // A/B: the L2-resident chol_wide_kernel (variant 0) against the register-resident chol_reg_kernel (1)
+        std::vector<double> hR0((size_t)LP * LP), hRi0((size_t)LP * LP);
+        rsvd::chol_variant = 0;
+        double t0 = time_us([&] { CK(launch_chol_wide(G, LP, LP, 1e-13, R, Ri, R32, cf, fl, W, nullptr, S)); });
+        CK(hipMemcpy(hR0.data(), R, hR0.size() * 8, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(hRi0.data(), Ri, hRi0.size() * 8, hipMemcpyDeviceToHost));
+        rsvd::chol_variant = 2;
         double t = time_us([&] { CK(launch_chol_wide(G, LP, LP, 1e-13, R, Ri, R32, cf, fl, W, nullptr, S)); });
+        rsvd::chol_variant = 1;
         // check R^T R = G and R Ri = I on the host
         std::vector<double> hR((size_t)LP * LP), hRi((size_t)LP * LP), hG((size_t)LP * LP);
         CK(hipMemcpy(hR.data(), R, hR.size() * 8, hipMemcpyDeviceToHost));
@@ -170,7 +178,9 @@ static void bench_chol() {
 #ifdef RSVD_CHOL_PROF
         rsvd::chol_prof_dump(LP);
 #endif
-        printf("chol LP=%d: %.1f us   |R^T R - G|/|G| = %.2e  |R Rinv - I| = %.2e\n", LP, t, sqrt(e1 / ng), sqrt(e2));
+        const bool same = !memcmp(hR0.data(), hR.data(), hR.size() * 8) && !memcmp(hRi0.data(), hRi.data(), hRi.size() * 8);
+        printf("chol LP=%d: wide %.1f us  reg %.1f us  bit-identical %d   |R^T R - G|/|G| = %.2e  |R Rinv - I| = %.2e\n", LP,
+               t0, t, (int)same, sqrt(e1 / ng), sqrt(e2));
         CK(hipFree(G)); CK(hipFree(R)); CK(hipFree(Ri)); CK(hipFree(W)); CK(hipFree(R32)); CK(hipFree(cf)); CK(hipFree(fl));
     }
 }
