@@ -703,7 +703,12 @@ __device__ __forceinline__ i32x4 read128_o(uint32_t a) {
 
 // ABL (lab ablations, results meaningless): bit 0 no barrier / DMA waits, bit 1 no DMA, bit 2 no
 // LDS fragment reads.  The product path instantiates ABL = 0 only.
-template <bool NN, int LP, bool SPLIT, int KN, int SD, int ABL = 0>
+// AR (lab only, abl 16): A staged through registers -- the LDS-DMA stream then carries only the
+// L2-resident S panels and the HBM-sourced A goes global -> VGPR -> ds_write.  Bit-identical; in the
+// isolated kernel loop it is 7 % faster (tools/wide_lab areg: NN2 3324 -> 3084 us, TN2 3383 -> 3136
+// us), but inside the 29-ms rSVD loop 2.4 % slower on the same box (C4 28.06-28.11 ms with DMA A vs
+// 28.77-28.83 ms, TN 3555 vs 3680 us; profiles/r02_v6_areg_ab.txt), so the engine keeps DMA A.
+template <bool NN, int LP, bool SPLIT, int KN, int SD, int ABL = 0, bool AR = false>
 __global__ __launch_bounds__(512) void wproj3_kernel(const bf16_t* __restrict__ A, int64_t lda, int64_t rows_out,
                                                      int64_t K, int64_t arows, const bf16_t* __restrict__ Shi,
                                                      const bf16_t* __restrict__ Slo, float* __restrict__ out,
@@ -765,23 +770,45 @@ __global__ __launch_bounds__(512) void wproj3_kernel(const bf16_t* __restrict__ 
             for (int t = 0; t < SH::SPW; ++t) glds16(S + soff[t], slot + a * SH::SIMG + (t * 8 + w) * SImg::PITCH);
         }
     };
+    auto asrc = [&](int st, int t) {
+        const int64_t k0 = kbeg + (int64_t)st * KS;
+        const bool tail = k0 + KS > K;  // (uniform) the last step of a ragged K: clamp the A reads
+        const bf16_t* src;
+        if constexpr (NN) {
+            src = A + k0 * lda + aoff[t];
+            if (tail && k0 + arow[t] >= K) src = A + (K - 1 - arow[t]) * lda + aoff[t];
+        } else {
+            src = A + k0 + aoff[t];
+            if (tail && k0 + arow[t] + 8 > arows) src = A + (arows - 8 - arow[t]) + aoff[t];
+        }
+        return src;
+    };
     auto issueA = [&](int st) {
         if constexpr ((ABL & 2) != 0) return;
         char* slot = smem_raw + (st % NA) * SH::AIMG;
-        const int64_t k0 = kbeg + (int64_t)st * KS;
-        const bool tail = k0 + KS > K;  // (uniform) the last step of a ragged K: clamp the A reads
+#pragma unroll
+        for (int t = 0; t < SH::APW; ++t) glds16<(KN & 1) ? 2 : 0>(asrc(st, t), slot + (t * 8 + w) * SH::APITCH);
+    };
+    // AR: A through registers instead of LDS-DMA -- global_load_dwordx4 four steps ahead,
+    // ds_write_b128 of the same 16 B to the same LDS address two steps ahead; S stays on the DMA.
+    // Loads and writes are inline asm: the compiler's waitcnt pass cannot count the in-flight DMA
+    // across the loop and drained vmcnt(0) before every write; the explicit wait_vm below covers them.
+    static_assert(!AR || (SD == 1 && NA >= 3), "register-staged A: SD = 1, >= 3 A slots");
+    i32x4 areg[2][SH::APW];
+    auto loadA = [&](int st, i32x4 (&dst)[SH::APW]) {
 #pragma unroll
         for (int t = 0; t < SH::APW; ++t) {
-            const bf16_t* src;
-            if constexpr (NN) {
-                src = A + k0 * lda + aoff[t];
-                if (tail && k0 + arow[t] >= K) src = A + (K - 1 - arow[t]) * lda + aoff[t];
-            } else {
-                src = A + k0 + aoff[t];
-                if (tail && k0 + arow[t] + 8 > arows) src = A + (arows - 8 - arow[t]) + aoff[t];
-            }
-            glds16<(KN & 1) ? 2 : 0>(src, slot + (t * 8 + w) * SH::APITCH);
+            if constexpr ((KN & 1) != 0)
+                asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(dst[t]) : "v"(asrc(st, t)) : "memory");
+            else
+                asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(dst[t]) : "v"(asrc(st, t)) : "memory");
         }
+    };
+    auto writeA = [&](int st, const i32x4 (&src)[SH::APW]) {
+        const uint32_t slot = lds_addr(smem_raw) + (uint32_t)((st % NA) * SH::AIMG) + 16 * lane;
+#pragma unroll
+        for (int t = 0; t < SH::APW; ++t)
+            asm volatile("ds_write_b128 %0, %1" ::"v"(slot + (uint32_t)((t * 8 + w) * SH::APITCH)), "v"(src[t]) : "memory");
     };
 
     // per-lane LDS read bases within a slot
@@ -807,22 +834,40 @@ __global__ __launch_bounds__(512) void wproj3_kernel(const bf16_t* __restrict__ 
     if ((KN & 2) && w >= 4) __builtin_amdgcn_s_setprio(1);
     // prologue: the issues of the virtual iterations -DA .. -1 (S(i + SD), A(i + DA)), so that the
     // steady-state wait below counts the same glds in every iteration
-    for (int i = -DA; i < 0; ++i) {
-        if (i + SD >= 0 && i + SD < nsteps) issueS(i + SD);
-        if (i + DA < nsteps) issueA(i + DA);
+    if constexpr (AR) {  // A(0), A(1) by DMA, S(0), then A(2), A(3) into registers
+        for (int i = 0; i < 2 && i < nsteps; ++i) issueA(i);
+        if (nsteps > 0) issueS(0);
+        if (2 < nsteps) loadA(2, areg[0]);
+        if (3 < nsteps) loadA(3, areg[1]);
+    } else {
+        for (int i = -DA; i < 0; ++i) {
+            if (i + SD >= 0 && i + SD < nsteps) issueS(i + SD);
+            if (i + DA < nsteps) issueA(i + DA);
+        }
     }
 
     const uint32_t lds0 = lds_addr(smem_raw);
-    for (int st = 0; st < nsteps; ++st) {
-        if constexpr ((ABL & 1) == 0) {
-            // S(st) and A(st) have landed once at most the glds issued after S(st) are in flight:
-            // A(st - SD + DA) and the SD - 1 full iterations since (conservatively all, at the end)
-            if (st - 1 + DA < nsteps) wait_vm<SH::APW + (SD - 1) * SH::GL>();
+    auto iter = [&](int st, i32x4 (&ar)[SH::APW]) {
+        if constexpr (AR) {
+            // S(st) (issued last iteration) and the register loads of A(st + 2) have landed once at
+            // most the APW loads of A(st + 3) are in flight
+            if (st + 3 < nsteps) wait_vm<SH::APW>();
             else wait_vm<0>();
             __builtin_amdgcn_s_barrier();
+            if (st + 2 < nsteps) writeA(st + 2, ar);
+            if (st + 1 < nsteps) issueS(st + 1);
+            if (st + 4 < nsteps) loadA(st + 4, ar);
+        } else {
+            if constexpr ((ABL & 1) == 0) {
+                // S(st) and A(st) have landed once at most the glds issued after S(st) are in flight:
+                // A(st - SD + DA) and the SD - 1 full iterations since (conservatively all, at the end)
+                if (st - 1 + DA < nsteps) wait_vm<SH::APW + (SD - 1) * SH::GL>();
+                else wait_vm<0>();
+                __builtin_amdgcn_s_barrier();
+            }
+            if (st + SD < nsteps) issueS(st + SD);
+            if (st + DA < nsteps) issueA(st + DA);
         }
-        if (st + SD < nsteps) issueS(st + SD);
-        if (st + DA < nsteps) issueA(st + DA);
         const uint32_t sS = lds0 + SH::SBASE + (uint32_t)((st % NSS) * SH::SSLOT);
         const uint32_t sA = lds0 + (uint32_t)((st % NA) * SH::AIMG);
         const uint32_t bS1 = sS + lS1, bS2 = sS + lS2, bA1 = sA + lA1, bA2 = sA + lA2;
@@ -886,6 +931,14 @@ __global__ __launch_bounds__(512) void wproj3_kernel(const bf16_t* __restrict__ 
             if constexpr (g + 1 < G) wait_b(bb[(g + 1) & 1]);
         };
         static_for<G>(gstep);
+    };
+    if constexpr (AR) {  // unrolled by two: each register buffer stays in fixed VGPRs (asm-loaded)
+        for (int st = 0; st < nsteps; st += 2) {
+            iter(st, areg[0]);
+            if (st + 1 < nsteps) iter(st + 1, areg[1]);
+        }
+    } else {
+        for (int st = 0; st < nsteps; ++st) iter(st, areg[0]);
     }
 
     float* dst = out + (int64_t)sp * slab_stride;
@@ -909,7 +962,16 @@ hipError_t wproj3_go(const void* A, int64_t lda, int64_t m, int64_t n, const bf1
     float* o = p.splits == 1 ? Out : slabs;
     const int64_t stride = rows_out * LP;
     constexpr int KN = NN ? 3 : 0;  // as v2 (profiles/r02_wide_lab_knobs.txt)
+    constexpr bool ar_ok = ABL == 0 && SD == 1 && SH::NA >= 3;  // register-staged A fits
     auto go = [&](auto knc) {
+        if constexpr (ar_ok) {
+            if (p.abl & 16) {  // abl 16 (lab only): register-staged A
+                hipLaunchKernelGGL((wproj3_kernel<NN, LP, SPLIT, decltype(knc)::value, SD, 0, true>),
+                                   dim3(p.blocks * p.splits), dim3(512), SH::LDS, s, reinterpret_cast<const bf16_t*>(A),
+                                   lda, rows_out, K, m, Shi, Slo, o, stride, p.chunk, p.blocks);
+                return;
+            }
+        }
         hipLaunchKernelGGL((wproj3_kernel<NN, LP, SPLIT, decltype(knc)::value, SD, ABL>), dim3(p.blocks * p.splits),
                            dim3(512), SH::LDS, s, reinterpret_cast<const bf16_t*>(A), lda, rows_out, K, m, Shi, Slo, o,
                            stride, p.chunk, p.blocks);
@@ -936,7 +998,7 @@ hipError_t wproj3_go(const void* A, int64_t lda, int64_t m, int64_t n, const bf1
 // S 2 x 33 KiB per hi / lo pair).  Row j's 16-B unit u (rows 8 u .. 8 u + 7 of the 64) sits at unit
 // u ^ ((j >> 1) & 7): a ds_read_b128 of 16 lanes (rows r = 0..15, one unit) covers all 16 bank
 // positions.  The S images are v3's (32-step, row placement by sigma).
-template <bool SPLIT, int KN>
+template <bool SPLIT, int KN, bool AR>
 __global__ __launch_bounds__(512) void wproj3tn2_kernel(const bf16_t* __restrict__ A, int64_t lda, int64_t rows_out,
                                                         int64_t K, int64_t arows, const bf16_t* __restrict__ Shi,
                                                         const bf16_t* __restrict__ Slo, float* __restrict__ out,
@@ -988,16 +1050,35 @@ __global__ __launch_bounds__(512) void wproj3tn2_kernel(const bf16_t* __restrict
             for (int t = 0; t < SH::SPW; ++t) glds16(S + soff[t], slot + a * SH::SIMG + (t * 8 + w) * SImg::PITCH);
         }
     };
-    auto issueA = [&](int d) {
-        char* slot = smem_raw + (d & 1) * ASLOT;
+    auto asrc = [&](int d, int t) {
         const int64_t k0 = kbeg + (int64_t)d * 2 * KS;
         const bool tail = k0 + 2 * KS > arows;
+        const bf16_t* src = A + k0 + aoff[t];
+        if (tail && k0 + arow[t] + 8 > arows) src = A + (arows - 8 - arow[t]) + aoff[t];
+        return src;
+    };
+    auto issueA = [&](int d) {
+        char* slot = smem_raw + (d & 1) * ASLOT;
+#pragma unroll
+        for (int t = 0; t < APW2; ++t) glds16<(KN & 1) ? 2 : 0>(asrc(d, t), slot + (t * 8 + w) * 1024);
+    };
+    // AR: A(d + 1) is ds_written at step 2d from registers loaded at step 2d - 2 (one A buffer: the
+    // write of A(d + 1) precedes the load of A(d + 2) in the same step); see wproj3_kernel.
+    i32x4 areg[APW2];
+    auto loadA = [&](int d) {
 #pragma unroll
         for (int t = 0; t < APW2; ++t) {
-            const bf16_t* src = A + k0 + aoff[t];
-            if (tail && k0 + arow[t] + 8 > arows) src = A + (arows - 8 - arow[t]) + aoff[t];
-            glds16<(KN & 1) ? 2 : 0>(src, slot + (t * 8 + w) * 1024);
+            if constexpr ((KN & 1) != 0)
+                asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(areg[t]) : "v"(asrc(d, t)) : "memory");
+            else
+                asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(areg[t]) : "v"(asrc(d, t)) : "memory");
         }
+    };
+    auto writeA = [&](int d) {
+        const uint32_t slot = lds_addr(smem_raw) + (uint32_t)((d & 1) * ASLOT) + 16 * lane;
+#pragma unroll
+        for (int t = 0; t < APW2; ++t)
+            asm volatile("ds_write_b128 %0, %1" ::"v"(slot + (uint32_t)((t * 8 + w) * 1024)), "v"(areg[t]) : "memory");
     };
 
     const int colS = wc * G * 16 + 4 * p;
@@ -1016,17 +1097,24 @@ __global__ __launch_bounds__(512) void wproj3tn2_kernel(const bf16_t* __restrict
     if (nsteps > 0) {
         issueS(0);
         issueA(0);
+        if (AR && 1 < nd) loadA(1);
     }
     const uint32_t lds0 = lds_addr(smem_raw);
     for (int st = 0; st < nsteps; ++st) {
         const int d = st >> 1, hs = st & 1;
-        // step 2d needs A(d) and S(2d): nothing younger is in flight; step 2d + 1 needs S(2d + 1),
-        // issued before A(d + 1) in step 2d
-        if (hs == 0 || d + 1 >= nd) wait_vm<0>();
+        // step 2d needs A(d) and S(2d) (AR: and the registers of A(d + 1)): nothing younger is in
+        // flight; step 2d + 1 needs S(2d + 1), issued before A(d + 1) (AR: A(d + 2)) in step 2d
+        if (hs == 0 || d + 1 + (AR ? 1 : 0) >= nd) wait_vm<0>();
         else wait_vm<SH::APW * 0 + APW2>();
         __builtin_amdgcn_s_barrier();
-        if (st + 1 < nsteps) issueS(st + 1);
-        if (hs == 0 && d + 1 < nd) issueA(d + 1);
+        if constexpr (AR) {
+            if (hs == 0 && d + 1 < nd) writeA(d + 1);
+            if (st + 1 < nsteps) issueS(st + 1);
+            if (hs == 0 && d + 2 < nd) loadA(d + 2);
+        } else {
+            if (st + 1 < nsteps) issueS(st + 1);
+            if (hs == 0 && d + 1 < nd) issueA(d + 1);
+        }
         const uint32_t sS = lds0 + SBASE + (uint32_t)((st & 1) * SH::SSLOT);
         const uint32_t sA = lds0 + (uint32_t)((d & 1) * ASLOT);
         const uint32_t bS1 = sS + lS1, bS2 = sS + lS2, bA = sA + (hs ? lA1 : lA0);
@@ -1099,10 +1187,15 @@ hipError_t wproj3tn2_go(const void* A, int64_t lda, int64_t m, int64_t n, const 
     const int64_t rows_out = n, K = m;
     float* o = p.splits == 1 ? Out : slabs;
     const int64_t stride = rows_out * 256;
-    auto go = [&](auto knc) {
-        hipLaunchKernelGGL((wproj3tn2_kernel<SPLIT, decltype(knc)::value>), dim3(p.blocks * p.splits), dim3(512), lds, s,
-                           reinterpret_cast<const bf16_t*>(A), lda, rows_out, K, m, Shi, Slo, o, stride, p.chunk,
-                           p.blocks);
+    auto go = [&](auto knc) {  // LDS-DMA A; register-staged A only for the lab (abl 16)
+        if (!(p.abl & 16))
+            hipLaunchKernelGGL((wproj3tn2_kernel<SPLIT, decltype(knc)::value, false>), dim3(p.blocks * p.splits),
+                               dim3(512), lds, s, reinterpret_cast<const bf16_t*>(A), lda, rows_out, K, m, Shi, Slo, o,
+                               stride, p.chunk, p.blocks);
+        else
+            hipLaunchKernelGGL((wproj3tn2_kernel<SPLIT, decltype(knc)::value, true>), dim3(p.blocks * p.splits),
+                               dim3(512), lds, s, reinterpret_cast<const bf16_t*>(A), lda, rows_out, K, m, Shi, Slo, o,
+                               stride, p.chunk, p.blocks);
     };
     switch (p.kn < 0 ? 0 : p.kn) {  // KN 0 in the engine; the others for the lab knob sweep
         case 1: go(std::integral_constant<int, 1>{}); break;

@@ -580,6 +580,7 @@ static void dma_bench() {
 }
 
 int main(int argc, char** argv) {
+    setvbuf(stdout, nullptr, _IOLBF, 0);
     const std::string what = argc > 1 ? argv[1] : "all";
     CK(hipStreamCreate(&S));
     if (what == "all" || what == "pg") bench_pg();
@@ -626,6 +627,41 @@ int main(int argc, char** argv) {
             double t2 = time_us([&] { CK(launch_wproj(0, 0, A, m, m, n, Sh, Sl, LP, pt, nullptr, Out, S)); });
             printf("abl %d (%s%s%s): NN2 %.1f us (%.0f TF)  TN2 %.1f us (%.0f TF)\n", ab, ab & 1 ? "nobar " : "",
                    ab & 2 ? "nodma " : "", ab & 4 ? "nolds" : "", t1, fl / t1 / 1e6, t2, fl / t2 / 1e6);
+        }
+    }
+    if (what == "areg") {  // v3 with A staged through registers (abl 16) against LDS-DMA A (the engine)
+        for (int cs = 0; cs < 2; ++cs) {
+            const int64_t m = cs ? 65536 : 4160, n = cs ? 65536 : 3000;  // case 0: ragged K, bit-identity
+            const int LP = 256;
+            void* A;
+            CK(hipMalloc(&A, (size_t)m * n * 2));
+            hipLaunchKernelGGL(fill_random_kernel, dim3(4096), dim3(256), 0, S, (uint16_t*)A, (size_t)m * n, 0);
+            bf16_t* Sh = dev_random<bf16_t>((size_t)(m > n ? m : n) * LP);
+            bf16_t* Sl = dev_random<bf16_t>((size_t)(m > n ? m : n) * LP);
+            float *O0, *O1;
+            CK(hipMalloc(&O0, (size_t)(m > n ? m : n) * LP * 4));
+            CK(hipMalloc(&O1, (size_t)(m > n ? m : n) * LP * 4));
+            const double fl = 4.0 * m * n * LP;
+            for (int nn = 1; nn >= 0; --nn) {
+                WProjPlan p0 = nn ? plan_wproj(m, n, LP, true) : plan_wproj(n, m, LP, true, false, false);
+                WProjPlan p1 = p0;  // p0: the engine's plan (LDS-DMA A)
+                p1.abl = 16;        // the same kernel with register-staged A
+                const int64_t ro = nn ? m : n;
+                float* slabs = nullptr;  // K-split partial products (p.splits > 1 writes them)
+                CK(hipMalloc(&slabs, (size_t)p0.splits * ro * LP * 4));
+                printf("case %ldx%ld nn %d splits %d ...\n", (long)m, (long)n, nn, p0.splits);
+                double t0 = time_us([&] { CK(launch_wproj(nn, 0, A, m, m, n, Sh, Sl, LP, p0, slabs, O0, S)); });
+                printf("  dma-A %.1f us\n", t0);
+                double t1 = time_us([&] { CK(launch_wproj(nn, 0, A, m, m, n, Sh, Sl, LP, p1, slabs, O1, S)); });
+                CK(hipFree(slabs));
+                std::vector<float> h0((size_t)ro * LP), h1((size_t)ro * LP);
+                CK(hipMemcpy(h0.data(), O0, h0.size() * 4, hipMemcpyDeviceToHost));
+                CK(hipMemcpy(h1.data(), O1, h1.size() * 4, hipMemcpyDeviceToHost));
+                const bool same = !memcmp(h0.data(), h1.data(), h0.size() * 4);
+                printf("areg %ldx%ld %s: dma-A %.1f us (%.0f TF)  reg-A %.1f us (%.0f TF)  bit-identical %d\n", (long)m,
+                       (long)n, nn ? "NN2" : (p0.tn2 ? "TN2(v3 tn2)" : "TN2(v3)"), t0, fl / t0 / 1e6, t1, fl / t1 / 1e6, (int)same);
+            }
+            CK(hipFree(A)); CK(hipFree(Sh)); CK(hipFree(Sl)); CK(hipFree(O0)); CK(hipFree(O1));
         }
     }
     if (what == "all" || what == "check") check_proj();
