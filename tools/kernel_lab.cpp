@@ -127,16 +127,16 @@ int main(int argc, char** argv) {
     unsigned t0 = 0, t1 = 0;
     double* tiles = gs + 32 * LP * LP;
     t0 += nb; t1 += NT;  // produce a valid Gram G first (mode 0)
-    CK(launch_gram_chol<float>(P, m, LP, nb, gs, tiles, ctr, t0, t1, 0, 1, G, l, R, Rinv, flag, s));
+    CK(launch_gram_chol<float>(P, m, LP, nb, gs, tiles, ctr, t0, t1, 0, 1, G, l, R, Rinv, flag, flag + 8, s));
     for (int f32 = 1; f32 >= 0; --f32) {
-        t = time_us(s, reps, [&] { t0 += nb; t1 += NT; CK(launch_gram_chol<float>(P, m, LP, nb, gs, tiles, ctr, t0, t1, 1, f32, nullptr, l, R, Rinv, flag, s)); });
+        t = time_us(s, reps, [&] { t0 += nb; t1 += NT; CK(launch_gram_chol<float>(P, m, LP, nb, gs, tiles, ctr, t0, t1, 1, f32, nullptr, l, R, Rinv, flag, flag + 8, s)); });
         printf("gram_chol fused (factor %s)    %9.2f us\n", f32 ? "fp32" : "fp64", t);
         t = time_us(s, reps, [&] { CK(launch_chol(G, l, LP, f32, R, Rinv, flag, s)); });
         printf("chol + inverse alone (%s)      %9.2f us\n", f32 ? "fp32" : "fp64", t);
     }
-    t = time_us(s, reps, [&] { t0 += nb; t1 += NT; CK(launch_gram_chol<float>(P, m, LP, nb, gs, tiles, ctr, t0, t1, 0, 1, G, l, R, Rinv, flag, s)); });
+    t = time_us(s, reps, [&] { t0 += nb; t1 += NT; CK(launch_gram_chol<float>(P, m, LP, nb, gs, tiles, ctr, t0, t1, 0, 1, G, l, R, Rinv, flag, flag + 8, s)); });
     printf("gram + tile reduce (mode 0)      %9.2f us\n", t);
-    t = time_us(s, reps, [&] { t0 += nb; t1 += NTX; CK(launch_cross_gram<float>(P, Q, m, LP, nb, gs, tiles, ctr, t0, t1, G, l, flag, s)); });
+    t = time_us(s, reps, [&] { t0 += nb; t1 += NTX; CK(launch_cross_gram<float>(P, Q, m, LP, nb, gs, tiles, ctr, t0, t1, G, l, flag + 8, s)); });
     printf("cross gram                       %9.2f us\n", t);
     t = time_us(s, reps, [&] { CK(launch_panel_small<float>(P, m, LP, Rinv, Q, 0, 0, 0, s)); });
     printf("panel_small (row-major out)      %9.2f us\n", t);
