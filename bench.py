@@ -6,6 +6,10 @@ projection, B = Q^T A, its small SVD, U = Q Utilde) on a synthetic A already res
 Synthetic A = X diag(0.9^t) Y^T / sqrt(n) + 1e-3 N, X, Y Gaussian.
 
 Configurations (BASELINE.json "configs"; --config, default c4):
+  c1  rank-10 rSVD of I_100 (the reference's input/sparse_matrix100.mtx, regenerated), fp64, q = 2,
+      Jacobi -- the reference's own CPU-runnable case (configs[0]); a latency line: the GPU call
+      next to the CPU oracle at -O3 (1 and all threads) and -O0 (the reference's build flag), with
+      the known answers S = 1, |A - U S V^T|_F = sqrt(100 - l) checked (l = 10 and 16)
   c2  dense 4096 x 4096 fp32, l = 64, q = 2                       (configs[1])
   c3  tall-skinny 1048576 x 1024 bf16, l = 128, q = 1             (configs[2])
   c4  dense 65536 x 65536 bf16, l = 256, q = 2, rows sharded      (configs[3]: the north-star
@@ -46,6 +50,7 @@ PEAK_HBM_GBS = 8000.0
 
 CONFIGS = {
     # name: (m, n, l, q, dtype, strong-scaled, cpu sample rows, label)
+    "c1": (100, 100, 10, 2, "f64", False, None, "C1: rank-10 rSVD of I_100 (input/sparse_matrix100.mtx), fp64, q=2"),
     "c2": (4096, 4096, 64, 2, "f32", False, None, "C2: dense 4096x4096 fp32 rSVD, l=64, q=2"),
     "c3": (1048576, 1024, 128, 1, "bf16", False, 16384, "C3: tall-skinny 1048576x1024 bf16 rSVD, l=128, q=1"),
     "c4": (65536, 65536, 256, 2, "bf16", True, 2048, "C4: dense 65536x65536 bf16 rSVD, l=256, q=2"),
@@ -151,6 +156,50 @@ def cpu_baseline(A_host, l, q, budget_s, threads, note):
     }
 
 
+def c1_extras(torch, R, eng, A, q, budget_s):
+    """C1 (tests/rSVD_test.cpp:60-75 on input/sparse_matrix100.mtx = I_100): known answers on the GPU
+    for l = 10 and 16, the synchronised single-call latency, and the CPU oracle at -O3 (1 thread and
+    all threads) and -O0 (the reference Makefile's flag, 1 thread)."""
+    import numpy as np
+
+    import oracle
+
+    out = {"known_answers": {}, "cpu_oracle_ms_per_rsvd": {}}
+    m = A.shape[0]
+    for l in (10, 16):
+        U, S, V = eng.rsvd(A, l, q=q, seed=0x5EED0001)
+        torch.cuda.synchronize()
+        Uh, Sh, Vh = U.cpu().numpy(), S.cpu().numpy(), V.cpu().numpy()
+        err = float(np.linalg.norm(np.eye(m) - (Uh * Sh) @ Vh.T))
+        out["known_answers"][f"l{l}"] = {"max_abs_S_minus_1": float(np.abs(Sh - 1.0).max()),
+                                         "residual_F": err, "expected_residual_F": float(np.sqrt(m - l))}
+    lat = []
+    for _ in range(20):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        eng.rsvd(A, 10, q=q, seed=0x5EED0001, check_errors=False)
+        torch.cuda.synchronize()
+        lat.append(time.perf_counter() - t0)
+    out["gpu_latency_ms_median"] = float(np.median(lat) * 1e3)
+    Ah = np.eye(m)
+    all_threads = int(os.environ.get("OMP_NUM_THREADS", str(min(16, os.cpu_count() or 1))))
+    for opt, threads in (("O3", 1), ("O3", all_threads), ("O0", 1)):
+        L = oracle.lib(opt)
+        L.orc_set_threads(threads)
+        Om = oracle.generate_omega(m, 10, 0x5EED0001)
+        Uo, So, Vo = np.zeros((m, 10), order="F"), np.zeros(10), np.zeros((m, 10), order="F")
+        ts = []
+        t_all = 0.0
+        while len(ts) < 200 and t_all < budget_s / 3:
+            t0 = time.perf_counter()
+            L.orc_rsvd(m, m, oracle._p(Ah), m, 10, q, oracle._p(Om), m, 0, oracle._p(Uo), oracle._p(So), oracle._p(Vo))
+            ts.append(time.perf_counter() - t0)
+            t_all += ts[-1]
+        out["cpu_oracle_ms_per_rsvd"][f"-{opt} {threads} thread(s)"] = float(np.median(ts) * 1e3)
+    oracle.set_threads(all_threads)
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -192,7 +241,10 @@ def main():
     else:
         m_local, row0 = m_cfg, m_cfg * rank
         m_global = m_cfg * world
-    A, a_scale = make_A(torch, m_local, n, row0, dt)
+    if args.config == "c1":  # I_100, exactly the reference's input/sparse_matrix100.mtx
+        A, a_scale = torch.eye(m_local, n, dtype=torch.float64, device="cuda").t().contiguous().t(), 1.0
+    else:
+        A, a_scale = make_A(torch, m_local, n, row0, dt)
     eng = R.Engine(local_rank)
     if world > 1:
         eng.set_comm(rank, world)
@@ -331,6 +383,8 @@ def main():
         threads = int(os.environ.get("OMP_NUM_THREADS", str(min(16, os.cpu_count() or 1))))
         cpu = cpu_baseline(Ah, l, q, args.cpu_budget, threads, note)
 
+    c1 = c1_extras(torch, R, eng, A, q, max(args.cpu_budget, 3.0)) if args.config == "c1" and rank == 0 else None
+
     if rank == 0:
         par = "single-gpu" if world == 1 else (f"row-partition x{world}" if strong else f"row-shard x{world}")
         if world > 1 and info.get("n_shard_rows"):
@@ -359,6 +413,8 @@ def main():
             "engine_info": info,
             "lowp_intermediates": fast,
         }
+        if c1 is not None:
+            line["c1"] = c1
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
