@@ -73,18 +73,6 @@ __device__ bool grid_barrier(unsigned* sync, unsigned target) {
     return ok != 0;
 }
 
-// Rotation of the pair (a = |x_p|^2, b = |x_q|^2, g = x_p.x_q): x_p' = c x_p - s x_q, x_q' = s x_p + c x_q
-// zeroes the cross term (jacobi.hip formula).
-__device__ __forceinline__ void jacobi_angle(double a, double b, double g, double& c, double& s) {
-    const double d = b - a, g2 = 2.0 * g;
-    const double sc = fmax(fabs(d), fabs(g2));
-    const double ds = fabs(d) / sc, gs = fabs(g2) / sc;
-    const double tmag = gs / (ds + sqrt(ds * ds + gs * gs));
-    const double t = ((d >= 0.0) == (g >= 0.0)) ? tmag : -tmag;
-    c = 1.0 / sqrt(1.0 + t * t);
-    s = c * t;
-}
-
 constexpr int GS = 33;       // LDS pitch of the 32 x 32 blocks
 constexpr int kInnerSweeps = 1;
 
@@ -101,7 +89,10 @@ __device__ __forceinline__ double rcp_nr(double d) {
     return y * (2.0 - d * y);
 }
 
-// jacobi_angle on the scaled operands (no overflow / underflow for any finite a, b, g)
+// Rotation of the pair (a = |x_p|^2, b = |x_q|^2, g = x_p.x_q): x_p' = c x_p - s x_q, x_q' = s x_p + c x_q
+// zeroes the cross term (jacobi.hip formula: t = sign(d g) |2g| / (|d| + sqrt(d^2 + 4 g^2)), d = b - a,
+// c = (1 + t^2)^-1/2, s = c t), evaluated on operands scaled by max(|d|, |2g|) (no overflow / underflow
+// for any finite a, b, g)
 __device__ __forceinline__ void pair_angle(const double* G, int p, int q, double tol2, double negl, double& c,
                                            double& s, bool& rot) {
     const double a = G[p * GS + p], b = G[q * GS + q], g = G[p * GS + q];
