@@ -305,7 +305,10 @@ struct WideEngine {
         ++orth_index;
         if (qr_mode == RSVD_QR_CHOLQR2 || qr_mode == RSVD_QR_GS2) passes = 2;
         if (passes <= 1) {
-            RSVD_TRY(cholqr_pass(P, rows, gp, Q, sharded, hi, lo, flag, nullptr));
+            // bf16 / e4m3 A: a power-iteration intermediate is consumed only through its bf16 hi/lo
+            // panels (the wproj kernels), so its fp32 copy is not written (-1/2 of the panel's writes)
+            T* out = (L.lowp && !repair && hi && lo) ? nullptr : Q;
+            RSVD_TRY(cholqr_pass(P, rows, gp, out, sharded, hi, lo, flag, nullptr));
         } else {
             RSVD_TRY(cholqr_pass(P, rows, gp, T1, sharded, nullptr, nullptr, flag, nullptr));
             RSVD_TRY(cholqr_pass(T1, rows, gp, Q, sharded, hi, lo, flag, nullptr));

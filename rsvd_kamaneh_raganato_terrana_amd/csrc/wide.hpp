@@ -79,7 +79,8 @@ hipError_t launch_chol_wide(const double* G, int l, int LP, double tol, double* 
 // 2: also chol_reg_kernel at LP = 256 (lab A/B only).
 extern int chol_variant;
 // Out (rows x LP) = In (rows x LP) * M (LP x LP, row-major, in the panel precision T; `upper`:
-// only k <= c of M is read).  Out layouts: row-major panel (ldo = 0) or the caller's column-major matrix (first
+// only k <= c of M is read).  Out may be null with ldo = 0 when only the hi / lo panels are wanted.
+// Out layouts: row-major panel (ldo = 0) or the caller's column-major matrix (first
 // `cols` columns, leading dimension ldo).  Optionally also writes the bf16 hi / lo panels of Out
 // (row-major, LP wide).  `pred`: as above.
 template <typename T>

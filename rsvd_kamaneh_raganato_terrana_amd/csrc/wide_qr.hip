@@ -992,7 +992,7 @@ __global__ __launch_bounds__(256) void panel_gemm_kernel(const T* __restrict__ I
                 const int c = c0 + 16 * g + r;
                 if (orow < rows && c < LP) {
                     const T v = (T)acc[g][j];
-                    Out[orow * LP + c] = v;
+                    if (Out) Out[orow * LP + c] = v;  // null: only the bf16 hi / lo panels are wanted
                     if (hi) {
                         const bf16_t bh = f2bf((float)v);
                         hi[orow * LP + c] = bh;
@@ -1203,7 +1203,7 @@ hipError_t launch_chol_wide(const double* G, int l, int LP, double tol, double* 
 template <typename T>
 hipError_t launch_panel_gemm(const T* In, int64_t rows, int LP, const T* Mm, int upper, T* Out, int64_t ldo,
                              int cols, bf16_t* hi, bf16_t* lo, const int* pred, hipStream_t s) {
-    if (!Mm || LP % 16) return hipErrorInvalidValue;
+    if (!Mm || LP % 16 || (!Out && (ldo != 0 || !hi))) return hipErrorInvalidValue;
     const int64_t rb = (rows + 63) / 64;
 #define GO(CT)                                                                                                  \
     {                                                                                                           \
