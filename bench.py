@@ -130,6 +130,31 @@ def pmc_traffic(key, kernel_prefix):
     return best
 
 
+def pmc_mfma_busy(key, kernel_prefix):
+    """MFMA pipe occupancy of the kernel from the committed rocprofv3 pass for this workload
+    (profiles/*_mfma_busy.json, tools/pmc_mfma.sh + tools/mfma_busy.py: SQ_VALU_MFMA_BUSY_CYCLES over
+    the SIMD-cycles at the clock the kernel actually ran, GRBM_GUI_ACTIVE).  Passes whose clock
+    estimate exceeds the 2.4 GHz peak are not evidence and are skipped.  None when absent."""
+    import glob
+    import re
+
+    def natural(f):
+        return [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", os.path.basename(f))]
+
+    best = None
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "*_mfma_busy.json")), key=natural):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if d.get("workload") != key:
+            continue
+        for k, v in d.get("kernels", {}).items():
+            if k.startswith(kernel_prefix) and 0 < v.get("clock_GHz_est", 9.9) <= 2.4:
+                best = {"frac": v["mfma_busy_frac"], "clock_GHz": v["clock_GHz_est"], "source": os.path.relpath(f, REPO)}
+    return best
+
+
 def cpu_baseline(A_host, l, q, budget_s, threads, note):
     import oracle
 
@@ -340,6 +365,7 @@ def main():
     else:
         kpref = "proj_tn_kernel" if kname.startswith("proj_tn") else "proj_nn_kernel"
     tr = pmc_traffic(key, kpref)
+    mb = pmc_mfma_busy(key, kpref)
     roof = {
         "bound": bound,
         "kernel": kname,
@@ -357,6 +383,8 @@ def main():
         "achieved_GBps": a_bytes / t_s / 1e9,
         "launches_timed": kn,
         "proj_share_of_step": (tm["nn_ms"] + tm["tn_ms"]) / (elapsed * 1e3) if elapsed > 0 else None,
+        # MFMA pipe occupancy of the same kernel (hi/lo work included) from the committed PMC pass
+        "mfma_busy_pmc": mb,
     }
 
     # the sketch Y = A Omega alone (single pass: Omega is exact in the storage type)
