@@ -413,13 +413,17 @@ __global__ __launch_bounds__(kBJThreads) void block_jacobi_kernel(const double* 
     }
 }
 
-// S, U_w = X / S (sorted descending, completed to orthonormal where S = 0), V_w = J.  One
-// workgroup; Uw / Vw row-major [row][col], LP x LP.
+// S, U_w = X / S (sorted descending, completed to orthonormal where S = 0), V_w = J, in three
+// launches: (1) one workgroup: column norms, descending ranks, S, and the sorted norms + inverse
+// permutation to scratch (the free half of the X double buffer); (2) a grid of 64 x 64 tiles:
+// U_w[i][k] = X[inv[k]][i] / s_k, V_w[i][k] = J[inv[k]][i] through an LDS transpose (coalesced
+// reads along i and writes along k -- one workgroup scattering 8-B values down the columns of
+// row-major U_w / V_w ran 0.7 ms at LP = 512); (3) one workgroup: completion of U_w for zero
+// singular values (returns at once when there are none).  Uw / Vw row-major [row][col], LP x LP.
 template <typename T>
 __global__ __launch_bounds__(1024) void block_jacobi_finish_kernel(const double* __restrict__ Xb,
-                                                                   const double* __restrict__ Jb, int l, int LP,
+                                                                   int l, int LP,
                                                                    const unsigned* __restrict__ sync,
-                                                                   double* __restrict__ Uw, double* __restrict__ Vw,
                                                                    T* __restrict__ S) {
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
     double* sig = reinterpret_cast<double*>(smem_raw);  // [LP]
@@ -430,21 +434,36 @@ __global__ __launch_bounds__(1024) void block_jacobi_finish_kernel(const double*
     const int64_t L2 = (int64_t)LP * LP;
     const int par = (int)sync[2];
     const double* X = Xb + (size_t)par * L2;
-    const double* J = Jb + (size_t)par * L2;
-    if (tid == 0) v[0] = 0.0;
-    __syncthreads();
-    for (int c = tid; c < LP; c += nt) {
-        double s2 = 0.0;
-        if (c < l)
-            for (int i = 0; i < LP; ++i) s2 += X[(int64_t)c * LP + i] * X[(int64_t)c * LP + i];
-        sig[c] = s2;
+    double* sigk = const_cast<double*>(Xb) + (size_t)(1 - par) * L2;  // scratch: [LP] sorted norms
+    int* inv = reinterpret_cast<int*>(sigk + LP);                     // [LP] column of rank k
+    // squared column norms: one wave per column, coalesced loads + a wave reduction, four columns
+    // per wave in flight (a column at a time left every wave waiting out one L2 round trip per column)
+    const int lane = tid & 63, wv = tid >> 6, nw = nt >> 6;
+    for (int c0 = wv; c0 < LP; c0 += 4 * nw) {
+        double s2[4] = {0.0, 0.0, 0.0, 0.0};
+        for (int i = lane; i < LP; i += 64) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int c = c0 + u * nw;
+                const double x = (c < l) ? X[(int64_t)c * LP + i] : 0.0;
+                s2[u] += x * x;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const double t = warp_sum(s2[u]);
+            if (lane == 0 && c0 + u * nw < LP) sig[c0 + u * nw] = t;
+        }
     }
     __syncthreads();
-    if (tid == 0) {
+    if (wv == 0) {
         double f = 0.0;
-        for (int c = 0; c < l; ++c) f += sig[c];
-        misc[1] = 0;
-        v[0] = f * (double)l * l * kEps * kEps;  // negligible column norm^2
+        for (int c = lane; c < l; c += 64) f += sig[c];
+        f = warp_sum(f);
+        if (lane == 0) {
+            misc[1] = 0;
+            v[0] = f * (double)l * l * kEps * kEps;  // negligible column norm^2
+        }
     }
     __syncthreads();
     const double negl = v[0];
@@ -459,26 +478,70 @@ __global__ __launch_bounds__(1024) void block_jacobi_finish_kernel(const double*
         int rk = 0;
         const double sc = sig[c];
         for (int d = 0; d < l; ++d) rk += (sig[d] > sc) || (sig[d] == sc && d < c);
-        rank[c] = rk;
+        S[rk] = (T)sc;
+        sigk[rk] = sc;
+        inv[rk] = c;
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void block_jacobi_scatter_kernel(const double* __restrict__ Xb,
+                                                                    const double* __restrict__ Jb, int l, int LP,
+                                                                    const unsigned* __restrict__ sync,
+                                                                    double* __restrict__ Uw, double* __restrict__ Vw) {
+    __shared__ double tile[64][65];
+    __shared__ double rs[64];
+    __shared__ int col[64];
+    const int tid = threadIdx.x;
+    const int nb = (LP + 63) / 64;  // LP is a multiple of 32: the last tile row / column may be half
+    const int k0 = 64 * (blockIdx.x % nb), i0 = 64 * (blockIdx.x / nb);
+    const int64_t L2 = (int64_t)LP * LP;
+    const int par = (int)sync[2];
+    const double* X = Xb + (size_t)par * L2;
+    const double* J = Jb + (size_t)par * L2;
+    const double* sigk = Xb + (size_t)(1 - par) * L2;
+    const int* inv = reinterpret_cast<const int*>(sigk + LP);
+    if (tid < 64) {
+        const int k = k0 + tid;
+        const double sc = k < l ? sigk[k] : 0.0;
+        col[tid] = k < l ? inv[k] : -1;
+        rs[tid] = sc > 0.0 ? 1.0 / sc : 0.0;
     }
     __syncthreads();
-    for (int64_t e = tid; e < L2; e += nt) {
-        Uw[e] = 0.0;
-        Vw[e] = 0.0;
-    }
-    __syncthreads();
-    for (int64_t e = tid; e < (int64_t)l * LP; e += nt) {
-        const int c = (int)(e / LP), i = (int)(e % LP);
-        if (i < l) {
-            Vw[(int64_t)i * LP + rank[c]] = J[(int64_t)c * LP + i];
-            if (sig[c] > 0.0) Uw[(int64_t)i * LP + rank[c]] = X[(int64_t)c * LP + i] / sig[c];
+    for (int pass = 0; pass < 2; ++pass) {  // 0: V_w from J, 1: U_w from X
+        const double* src = pass ? X : J;
+        for (int e = tid; e < 64 * 64; e += 256) {
+            const int kk = e >> 6, ii = e & 63;
+            const int c = col[kk], i = i0 + ii;
+            double x = 0.0;
+            if (c >= 0 && i < l) x = src[(int64_t)c * LP + i] * (pass ? rs[kk] : 1.0);
+            tile[kk][ii] = x;
         }
+        __syncthreads();
+        double* dst = pass ? Uw : Vw;
+        for (int e = tid; e < 64 * 64; e += 256) {
+            const int ii = e >> 6, kk = e & 63;
+            if (i0 + ii < LP && k0 + kk < LP) dst[(int64_t)(i0 + ii) * LP + k0 + kk] = tile[kk][ii];
+        }
+        __syncthreads();
     }
-    for (int c = tid; c < l; c += nt) S[rank[c]] = (T)sig[c];
+}
+
+template <typename T>
+__global__ __launch_bounds__(1024) void block_jacobi_complete_kernel(const T* __restrict__ S, int l, int LP,
+                                                                     double* __restrict__ Uw) {
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    double* v = reinterpret_cast<double*>(smem_raw);  // [LP]
+    int* misc = reinterpret_cast<int*>(v + LP);        // [4]
+    const int tid = threadIdx.x, nt = blockDim.x;
+    if (tid == 0) misc[1] = 0;
     __syncthreads();
+    int mine = 0;
+    for (int c = tid; c < l; c += nt) mine += (S[c] > (T)0);
+    if (mine) atomicAdd(&misc[1], mine);
+    __syncthreads();
+    const int nz = misc[1];
     // complete U_w for zero singular values (as jacobi.hip): least-covered unit vector, CGS2
-    int nz = 0;
-    for (int c = 0; c < l; ++c) nz += (sig[c] > 0.0);
     for (int k = nz; k < l; ++k) {
         for (int i = tid; i < LP; i += nt) {
             double cov = 0.0;
@@ -535,7 +598,10 @@ hipError_t launch_block_jacobi(const double* R, int l, int LP, double* X, double
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     const size_t lds = (size_t)LP * 8 * 2 + (size_t)LP * 4 + 64;
-    hipLaunchKernelGGL((block_jacobi_finish_kernel<T>), dim3(1), dim3(1024), lds, s, X, J, l, LP, sync, Uw, Vw, S);
+    hipLaunchKernelGGL((block_jacobi_finish_kernel<T>), dim3(1), dim3(1024), lds, s, X, l, LP, sync, S);
+    hipLaunchKernelGGL((block_jacobi_scatter_kernel<T>), dim3(((LP + 63) / 64) * ((LP + 63) / 64)), dim3(256), 0, s, X, J, l, LP,
+                       sync, Uw, Vw);
+    hipLaunchKernelGGL((block_jacobi_complete_kernel<T>), dim3(1), dim3(1024), (size_t)LP * 8 + 64, s, S, l, LP, Uw);
     return hipGetLastError();
 }
 
