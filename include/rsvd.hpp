@@ -84,6 +84,21 @@ inline void check(int status, const char* what) {
     throw std::runtime_error(msg);
 }
 
+// ---- multi-GPU (one process per GPU, as the reference's MPI ranks: src/rSVD.cpp:15,20-23) ----
+// The process's handle joins an RCCL communicator owned by the library (rsvd_comm_init): rank 0
+// draws the id, the caller broadcasts it (MPI_Bcast of RSVD_COMM_ID_BYTES bytes -- where the
+// reference broadcasts Omega, :52) and every rank calls distributed_init.  Afterwards
+// rsvd_local_rows runs the row-sharded rSVD on this rank's rows of A (rsvd_row_partition, the
+// :20-23 split): U comes back as this rank's rows, S and V complete on every rank.
+inline void unique_id(void* id /* RSVD_COMM_ID_BYTES */) {
+    const int st = rsvd_comm_unique_id(id);
+    if (st != RSVD_OK) throw std::runtime_error(std::string("rsvd_comm_unique_id: ") + rsvd_status_string(st));
+}
+inline void check(int status, const char* what);
+inline void distributed_init(const void* id, int rank, int world, bool shard_n = true) {
+    check(rsvd_comm_init(Context::instance().handle(), id, rank, world, shard_n ? 1 : 0), "rsvd_comm_init");
+}
+
 // rSVD(A, U, S, V, l, method) with q power iterations (the reference hard-codes q = 2).
 // rSVD with the outputs as the C ABI returns them: U m x d, S d, V n x d with the right singular
 // vectors in COLUMNS for every method (d = min(l, n)).  With Method::PowerImageCompression and
@@ -100,6 +115,14 @@ void rsvd_columns(const Mat& A, Mat& U, Vec& S, Mat& V, int l, Method method, in
     check(rsvd_run_host_f64(c.handle(), m, n, A.data(), m, l, q, static_cast<int32_t>(method), nullptr,
                             c.next_seed(), U.data(), S.data(), V.data()),
           "rSVD");
+}
+
+// The row-sharded rSVD after distributed_init: A_local = this rank's rows of the global A (the
+// partition of rsvd_row_partition), U_local its rows of U, S and V the whole of them.
+template <class Mat, class Vec>
+void rsvd_local_rows(const Mat& A_local, Mat& U_local, Vec& S, Mat& V, int l, Method method = Method::Jacobi,
+                     int q = 2) {
+    rsvd_columns(A_local, U_local, S, V, l, method, q);
 }
 
 // Method::Power returns what the reference's rSVD returns for it (src/rSVD.cpp:106-113 with

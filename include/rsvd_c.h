@@ -33,7 +33,7 @@
 extern "C" {
 #endif
 
-#define RSVD_ABI_VERSION 5
+#define RSVD_ABI_VERSION 6
 
 typedef enum {
     RSVD_OK = 0,
@@ -81,6 +81,10 @@ typedef enum { RSVD_QR_AUTO = 0, RSVD_QR_GS2 = 1, RSVD_QR_CHOLQR2 = 2 } rsvd_qr_
  * l = 256) the results stay within 1e-5 of the full-precision path, on flat ones (0.999^i) they
  * drift to ~5e-3.  Off by default. */
 #define RSVD_FLAG_LOWP_INTERMEDIATES 1
+/* Test/diagnostic flag (ABI 6): run the n-side sharded code path (reduce-scatter / all-gather
+ * through the handle's collectives) even at world 1, so a one-GPU box exercises the exact RCCL
+ * calls an N-GPU run makes.  Requires collectives (rsvd_set_collectives or rsvd_comm_init). */
+#define RSVD_FLAG_FORCE_NSHARD 2
 
 typedef struct {
     int64_t m, n;              /* A is m x n                                                   */
@@ -151,6 +155,20 @@ int rsvd_set_comm(rsvd_handle_t h, int rank, int world, rsvd_allreduce_fn fn, vo
  * n side.  SVDMethod::Power runs keep the replicated n side.  rsvd_workspace_bytes covers the
  * padded n-side panels of any world up to 64. */
 int rsvd_set_collectives(rsvd_handle_t h, rsvd_collective_fn fn, void *user);
+
+/* Library-owned RCCL (ABI 6): the handle creates and owns an RCCL communicator over the ranks'
+ * GPUs (one process per GPU, as the reference's MPI ranks, src/rSVD.cpp:15,20-23) and issues
+ * ncclAllReduce / ncclReduceScatter / ncclAllGather on its own stream -- no hooks, no Python.
+ * rsvd_comm_unique_id fills RSVD_COMM_ID_BYTES bytes (ncclGetUniqueId) on ONE rank; the caller
+ * broadcasts them (e.g. MPI_Bcast, where the reference Bcasts Omega, src/rSVD.cpp:52) and every
+ * rank calls rsvd_comm_init with its rank.  shard_n != 0 also shards the n side (as
+ * rsvd_set_collectives).  rsvd_set_comm / rsvd_set_collectives afterwards replace it;
+ * rsvd_comm_destroy (or rsvd_destroy) releases it.  librccl is loaded on first use
+ * (RSVD_ERR_UNSUPPORTED when it cannot be). */
+#define RSVD_COMM_ID_BYTES 128
+int rsvd_comm_unique_id(void *id);
+int rsvd_comm_init(rsvd_handle_t h, const void *id, int rank, int world, int shard_n);
+int rsvd_comm_destroy(rsvd_handle_t h);
 
 /* Row partition of src/rSVD.cpp:20-23 / src/PM.cpp:31-35: rows of rank `rank` out of `world`.
  * Host-only arithmetic (no device needed).  Returns the local row count, *offset = first row. */

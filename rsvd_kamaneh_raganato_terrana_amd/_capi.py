@@ -30,6 +30,8 @@ F64, F32, BF16, FP8_E4M3 = 0, 1, 2, 3
 SVD_JACOBI, SVD_POWER, SVD_PARALLEL_JACOBI, SVD_POWER_IC = 0, 1, 2, 3
 QR_AUTO, QR_GS2, QR_CHOLQR2 = 0, 1, 2
 FLAG_LOWP_INTERMEDIATES = 1
+FLAG_FORCE_NSHARD = 2  # test/diagnostic: the n-side sharded path (RCCL calls) at world 1
+COMM_ID_BYTES = 128
 
 # Every symbol include/rsvd_c.h declares (checked by tests/test_capi_exports.py).
 EXPORTS = (
@@ -39,6 +41,7 @@ EXPORTS = (
     "rsvd_generate_omega", "rsvd_run_host_f64", "rsvd_range_finder_host_f64",
     "rsvd_generate_omega_host_f64", "rsvd_qr", "rsvd_svd", "rsvd_qr_workspace_bytes",
     "rsvd_svd_workspace_bytes", "rsvd_qr_host_f64", "rsvd_svd_host_f64",
+    "rsvd_comm_unique_id", "rsvd_comm_init", "rsvd_comm_destroy",
 )
 
 
@@ -78,7 +81,7 @@ COLL_REDUCE_SCATTER, COLL_ALL_GATHER = 1, 2
 def _sources():
     """The files librsvd_hip.so is built from, in the order the Makefile hashes them."""
     hip = "util.hip proj.hip qr.hip jacobi.hip wide_proj.hip wide_qr.hip wide_svd.hip dense.hip".split()
-    cpp = "driver.cpp wide.cpp dense_api.cpp".split()
+    cpp = "driver.cpp wide.cpp dense_api.cpp comm.cpp".split()
     hdr = "common.hpp kernels.hpp wide.hpp dense.hpp handle.hpp".split()
     return ([os.path.join(CSRC, f) for f in hip + cpp + hdr] + [os.path.join(REPO, "include", "rsvd_c.h")]
             + [os.path.join(CSRC, "Makefile")])
@@ -164,6 +167,9 @@ def lib():
     L.rsvd_svd_workspace_bytes.argtypes = [i64, i64, i32, i32, szp]
     L.rsvd_qr_host_f64.argtypes = [vp, i64, i64, dp, i64, i32, dp, dp]
     L.rsvd_svd_host_f64.argtypes = [vp, i64, i64, dp, i64, i32, i32, u64, dp, dp, dp, ip]
+    L.rsvd_comm_unique_id.argtypes = [vp]
+    L.rsvd_comm_init.argtypes = [vp, vp, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    L.rsvd_comm_destroy.argtypes = [vp]
     _LIB = L
     return L
 

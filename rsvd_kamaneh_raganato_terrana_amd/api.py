@@ -102,13 +102,18 @@ def make_collective_hook(get_buffer, group=None):
     reduce-scatter of A^T Q and the all-gathers of the next skinny operand and of V that the
     n-side sharding needs.  Like the all-reduce hook it only ever touches
     slices of the handle's workspace and returns non-zero instead of raising through C.  RCCL
-    ("nccl") runs reduce_scatter_tensor / all_gather_into_tensor in place; a backend without them
-    (gloo) gets the same result from one all_reduce (reduce-scatter: sum everything, keep this
-    rank's chunk; all-gather: zero the other chunks, sum)."""
+    ("nccl") and gloo on CPU buffers run reduce_scatter_tensor / all_gather_into_tensor, in place
+    when the engine aliases recv = send + rank count (RS) or send = recv + rank count (AG) -- so the
+    CPU gloo tests run the very branch RCCL runs.  gloo on CUDA buffers (two ranks sharing one GPU
+    in the GPU tests) lacks those and gets the same result from one all_reduce (reduce-scatter: sum
+    everything, keep this rank's chunk; all-gather: zero the other chunks, sum)."""
     torch = _torch()
     import torch.distributed as dist
 
     sizes = {_capi.F64: (torch.float64, 8), _capi.F32: (torch.float32, 4), _capi.BF16: (torch.bfloat16, 2)}
+    # the tensor collectives (RCCL, and gloo on CPU tensors -- so the CPU tests run this same
+    # branch, in-place aliasing included); gloo on CUDA tensors has only all_reduce
+    legacy = {}
 
     def _hook(op, send, recv, count, dtype, stream, user):
         try:
@@ -126,9 +131,11 @@ def make_collective_hook(get_buffer, group=None):
                     raise ValueError("slice outside the workspace")
                 return ws[off: off + n * esz].view(tdt)
 
+            if "v" not in legacy:
+                legacy["v"] = dist.get_backend(group) == "gloo" and ws.is_cuda
             if op == _capi.COLL_REDUCE_SCATTER:
                 full, part = view(send, world * count), view(recv, count)
-                if dist.get_backend(group) == "nccl":
+                if not legacy["v"]:
                     dist.reduce_scatter_tensor(part, full, op=dist.ReduceOp.SUM, group=group)
                 else:
                     dist.all_reduce(full, op=dist.ReduceOp.SUM, group=group)
@@ -137,7 +144,7 @@ def make_collective_hook(get_buffer, group=None):
                 return 0
             if op == _capi.COLL_ALL_GATHER:
                 full, part = view(recv, world * count), view(send, count)
-                if dist.get_backend(group) == "nccl":
+                if not legacy["v"]:
                     dist.all_gather_into_tensor(full, part, group=group)
                 else:
                     mine = full[rank * count:(rank + 1) * count]
@@ -205,12 +212,33 @@ class Engine:
     def set_comm(self, rank: int, world: int, group=None, shard_n: bool = True):
         """Row-sharded runs: bind the exchange hooks to torch.distributed over RCCL -- the
         all-reduce (m-side Grams; A^T Q when the n side is replicated) and, with shard_n, the
-        reduce-scatter / all-gather hook that shards the n side across ranks as well."""
+        reduce-scatter / all-gather hook that shards the n side across ranks as well.  At world 1
+        the collective hook is still bound with shard_n, for runs with force_nshard=True (the
+        sharded code path and its collectives on one GPU)."""
         self._hook = make_allreduce_hook(lambda: self._ws, group)
         check(lib().rsvd_set_comm(self.h, rank, world, self._hook, None), self.h)
-        self._coll = make_collective_hook(lambda: self._ws, group) if shard_n and world > 1 else None
+        self._coll = make_collective_hook(lambda: self._ws, group) if shard_n else None
         check(lib().rsvd_set_collectives(self.h, self._coll if self._coll is not None else _capi.COLLECTIVE_FN(), None),
               self.h)
+
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        """rsvd_comm_unique_id: the RCCL id one rank draws and every rank passes to comm_init."""
+        buf = ctypes.create_string_buffer(_capi.COMM_ID_BYTES)
+        check(lib().rsvd_comm_unique_id(buf))
+        return buf.raw
+
+    def comm_init(self, uid: bytes, rank: int, world: int, shard_n: bool = True):
+        """rsvd_comm_init: the library-owned RCCL communicator (no Python hooks on the data path;
+        what a C / C++ caller uses, include/rsvd_c.h ABI 6)."""
+        if len(uid) != _capi.COMM_ID_BYTES:
+            raise ValueError("bad RCCL unique id")
+        buf = ctypes.create_string_buffer(uid, _capi.COMM_ID_BYTES)
+        self._hook = self._coll = None
+        check(lib().rsvd_comm_init(self.h, buf, rank, world, int(shard_n)), self.h)
+
+    def comm_destroy(self):
+        check(lib().rsvd_comm_destroy(self.h), self.h)
 
     def set_timing(self, enable: bool = True):
         """hipEvent timing of every projection GEMM launch (benchmarking only)."""
@@ -258,16 +286,18 @@ class Engine:
 
     def rsvd(self, A, l: int, q: int = 2, method: int = SVDMethod.Jacobi, omega=None, seed: int = 0,
              qr_mode: int = QRMode.Auto, out=None, a_scale: float = 1.0, check_errors: bool = True,
-             lowp_intermediates: bool = False):
+             lowp_intermediates: bool = False, force_nshard: bool = False):
         """Device rSVD: A (m x n, CUDA, column-major f64/f32/bf16/e4m3) -> U (m x l), S (l), V (n x l).
 
         check_errors=True synchronises and raises on the run's device-side failures (rsvd_sync);
         False leaves the run queued (asynchronous) -- call sync() later to check.
-        lowp_intermediates: RSVD_FLAG_LOWP_INTERMEDIATES (include/rsvd_c.h; bf16 / e4m3 A, q >= 2)."""
+        lowp_intermediates: RSVD_FLAG_LOWP_INTERMEDIATES (include/rsvd_c.h; bf16 / e4m3 A, q >= 2).
+        force_nshard: RSVD_FLAG_FORCE_NSHARD (tests: the n-side sharded path at world 1)."""
         torch = _torch()
         A, _ = colmajor(A)
-        d = self.desc(A, l, q, method, seed, qr_mode, a_scale,
-                      _capi.FLAG_LOWP_INTERMEDIATES if lowp_intermediates else 0)
+        flags = (_capi.FLAG_LOWP_INTERMEDIATES if lowp_intermediates else 0) | (
+            _capi.FLAG_FORCE_NSHARD if force_nshard else 0)
+        d = self.desc(A, l, q, method, seed, qr_mode, a_scale, flags)
         self.reserve(d)
         self._bind_stream()
         m, n = A.shape

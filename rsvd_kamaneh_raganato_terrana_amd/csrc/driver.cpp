@@ -74,7 +74,7 @@ int check_desc_msg(const rsvd_desc_t* d, const char** err) {
     }
     if (d->dtype < RSVD_F64 || d->dtype > RSVD_FP8_E4M3) { *err = "unsupported dtype"; return RSVD_ERR_UNSUPPORTED; }
     if (d->qr_mode < RSVD_QR_AUTO || d->qr_mode > RSVD_QR_CHOLQR2) { *err = "bad qr_mode"; return RSVD_ERR_INVALID_ARG; }
-    if (d->flags & ~RSVD_FLAG_LOWP_INTERMEDIATES) { *err = "unknown flags"; return RSVD_ERR_INVALID_ARG; }
+    if (d->flags & ~(RSVD_FLAG_LOWP_INTERMEDIATES | RSVD_FLAG_FORCE_NSHARD)) { *err = "unknown flags"; return RSVD_ERR_INVALID_ARG; }
     if (d->method != RSVD_SVD_JACOBI && d->method != RSVD_SVD_PARALLEL_JACOBI && d->method != RSVD_SVD_POWER &&
         d->method != RSVD_SVD_POWER_IC) {
         *err = "Unsupported SVD method";  // src/rSVD.cpp:123 wording
@@ -377,6 +377,7 @@ int rsvd_destroy(rsvd_handle_t h) {
     if (!h) return RSVD_OK;
     (void)hipSetDevice(h->device);
     if (h->stream) (void)hipStreamSynchronize(h->stream);
+    release_comm(h);
     if (h->ws && !h->ws_external) (void)hipFree(h->ws);
     if (h->dflags) (void)hipFree(h->dflags);
     for (auto e : h->ev_pool) (void)hipEventDestroy(e);
@@ -499,7 +500,8 @@ int rsvd_set_workspace(rsvd_handle_t h, void* ptr, size_t bytes) {
 }
 
 int rsvd_set_comm(rsvd_handle_t h, int rank, int world, rsvd_allreduce_fn fn, void* user) {
-    if (!h || world < 1 || rank < 0 || rank >= world || (world > 1 && !fn)) return RSVD_ERR_INVALID_ARG;
+    if (!h || world < 1 || world > 64 || rank < 0 || rank >= world || (world > 1 && !fn)) return RSVD_ERR_INVALID_ARG;
+    release_comm(h);  // hooks replace a library-owned communicator
     h->rank = rank;
     h->world = world;
     h->allreduce = fn;
@@ -536,7 +538,8 @@ int rsvd_run(rsvd_handle_t h, const rsvd_desc_t* d, const void* A, const void* o
         return RSVD_ERR_INVALID_ARG;
     }
     RSVD_TRY(set_device(h));
-    if (wide_path(d) || h->world > 1) return wide_run(h, d, A, omega, ldo, U, ldu, S, V, ldv, nullptr, 0);
+    if (wide_path(d) || h->world > 1 || (d->flags & RSVD_FLAG_FORCE_NSHARD))
+        return wide_run(h, d, A, omega, ldo, U, ldu, S, V, ldv, nullptr, 0);
     if (d->dtype == RSVD_F64) return run_typed<double>(h, d, A, omega, ldo, U, ldu, S, V, ldv, nullptr, 0);
     return run_typed<float>(h, d, A, omega, ldo, U, ldu, S, V, ldv, nullptr, 0);
 }

@@ -30,6 +30,7 @@ struct rsvd_handle_s {
     void* ar_user = nullptr;
     rsvd_collective_fn coll = nullptr;  // n-side sharding (wide engine), rsvd_set_collectives
     void* coll_user = nullptr;
+    void* nccl = nullptr;  // library-owned RCCL communicator (rsvd_comm_init, comm.cpp)
     // timing mode: hipEvent pairs around every projection kernel (kind 0 = A*X, 1 = A^T*Q, 2 = the
     // sketch A*Omega, which also counts as kind 0)
     bool timing = false;
@@ -64,6 +65,11 @@ inline hipError_t reset_run_flags(int* dflags, hipStream_t s) {
     if (e != hipSuccess) return e;
     return hipMemsetAsync(dflags + 4, 0, 16 * sizeof(int), s);
 }
+
+namespace rsvd {
+// comm.cpp: release the library-owned RCCL communicator (no-op without one)
+void release_comm(rsvd_handle_t h);
+}  // namespace rsvd
 
 inline int lp_of(int l) { return (l + 15) / 16 * 16; }
 inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }

@@ -64,12 +64,13 @@ struct WideLayout {
     int64_t nc = 0, nfull = 0;
     GramPlan gnc, gxc;
 
-    // a_aligned: A's base is 16-B aligned (the LDS-DMA projection kernel needs 16-B source chunks)
-    WideLayout(const rsvd_desc_t* d, bool a_aligned = true, int world = 1)
+    // a_aligned: A's base is 16-B aligned (the LDS-DMA projection kernel needs 16-B source chunks);
+    // shard: the n side is sharded over `world` ranks (world 1 only under RSVD_FLAG_FORCE_NSHARD)
+    WideLayout(const rsvd_desc_t* d, bool a_aligned = true, int world = 1, bool shard = false)
         : m(d->m), n(d->n), l(d->l), LP(wide_lp(d->l, d->dtype)) {
         lowp = lowp_dtype(d->dtype);
         mpad = rup(m, 32);
-        nsh = world > 1;
+        nsh = shard;
         nc = nsh ? rup((n + world - 1) / world, 32) : n;
         nfull = nsh ? nc * world : n;
         npad = std::max(rup(n, 32), nfull);
@@ -439,9 +440,10 @@ int wide_typed(rsvd_handle_t h, const rsvd_desc_t* d, const void* A, const void*
                int64_t ldu, void* S, void* V, int64_t ldv, void* Qout, int64_t ldq) {
     // n-side sharding: a collective hook on a sharded handle, not for SVDMethod::Power (its stage
     // runs on the whole Q_B) nor for the range-finder-only entry point (Qout)
-    const bool nshard = h->world > 1 && h->coll && !Qout && d->method != RSVD_SVD_POWER &&
-                        d->method != RSVD_SVD_POWER_IC;
-    WideLayout<T> L(d, (reinterpret_cast<uintptr_t>(A) & 15) == 0, nshard ? h->world : 1);
+    // (RSVD_FLAG_FORCE_NSHARD: the same code path at world 1, so one GPU runs the RCCL calls)
+    const bool nshard = (h->world > 1 || (d->flags & RSVD_FLAG_FORCE_NSHARD)) && h->coll && !Qout &&
+                        d->method != RSVD_SVD_POWER && d->method != RSVD_SVD_POWER_IC;
+    WideLayout<T> L(d, (reinterpret_cast<uintptr_t>(A) & 15) == 0, h->world, nshard);
     RSVD_TRY(ensure_ws(h, L.total));
     RSVD_CK(reset_run_flags(h->dflags, h->stream));
     if (L.nsh && L.nfull > L.n) {  // the zero rows past n of the sharded n-side panels (A^T Q, Q_B)
@@ -491,10 +493,12 @@ int wide_workspace_bytes(const rsvd_desc_t* d, size_t* bytes) {
     // world is not known here)
     size_t b = 0;
     for (int world = 1; world <= 64; ++world) {
+        const bool shard = world > 1 || (d->flags & RSVD_FLAG_FORCE_NSHARD);
         if (d->dtype == RSVD_F64)
-            b = std::max(b, WideLayout<double>(d, true, world).total);
+            b = std::max(b, WideLayout<double>(d, true, world, shard).total);
         else
-            b = std::max({b, WideLayout<float>(d, true, world).total, WideLayout<float>(d, false, world).total});
+            b = std::max({b, WideLayout<float>(d, true, world, shard).total,
+                          WideLayout<float>(d, false, world, shard).total});
     }
     *bytes = b;
     return RSVD_OK;

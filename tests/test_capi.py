@@ -18,7 +18,7 @@ HEADER = os.path.join(REPO, "include", "rsvd_c.h")
 
 @pytest.fixture(scope="module")
 def lib():
-    R.build()
+    R.build(force=False)
     return _capi.lib()
 
 
@@ -90,7 +90,7 @@ def test_workspace_bytes_and_argument_checks(lib):
     assert nb64.value > nb.value
     # 1 = RSVD_ERR_INVALID_ARG, 2 = RSVD_ERR_UNSUPPORTED
     for bad, code in ((dict(l=0), 1), (dict(q=-1), 1), (dict(lda=100), 1), (dict(l=513), 2), (dict(m=10, l=16), 2),
-                      (dict(dtype=7), 2), (dict(method=7), 2), (dict(flags=2), 1)):
+                      (dict(dtype=7), 2), (dict(method=7), 2), (dict(flags=4), 1)):
         assert lib.rsvd_workspace_bytes(ctypes.byref(_desc(**bad)), ctypes.byref(nb)) == code, bad
     assert lib.rsvd_workspace_bytes(ctypes.byref(_desc(flags=_capi.FLAG_LOWP_INTERMEDIATES)), ctypes.byref(nb)) == 0
     # the wide engine (l > 64, bf16 / e4m3 A): l-wide panels, bf16 hi/lo copies, slabs -- O((m + n) l)

@@ -40,7 +40,7 @@ def _matrix(case):
     return gapped_matrix(m, n, 2 * l, decay=0.93 if l < 256 else 0.985, seed=5).astype(np.float64)
 
 
-def _worker(rank, port, case, q, shard_n):
+def _worker(rank, port, case, q, shard_n, lowp=False):
     try:
         sys.path.insert(0, REPO)
         sys.path.insert(0, os.path.join(REPO, "tests"))
@@ -57,16 +57,19 @@ def _worker(rank, port, case, q, shard_n):
         m, n, l, qq, dt = case[:5]
         A = _matrix(case)
         rows, off = R.row_partition(m, WORLD, rank)
-        tdt = {"f64": torch.float64, "f32": torch.float32, "bf16": torch.bfloat16}[dt]
-        Ag = torch.from_numpy(np.ascontiguousarray(A[off:off + rows].T)).cuda().to(tdt).t()
+        tdt = {"f64": torch.float64, "f32": torch.float32, "bf16": torch.bfloat16,
+               "e4m3": torch.float8_e4m3fn}[dt]
+        # e4m3: one per-tensor scale of the GLOBAL A (every rank the same a_scale)
+        scale = float(np.abs(A).max()) / 448.0 if dt == "e4m3" else 1.0
+        Ag = torch.from_numpy(np.ascontiguousarray(A[off:off + rows].T / scale)).cuda().to(tdt).t()
         eng = R.Engine(0)
         eng.set_comm(rank, WORLD, shard_n=shard_n)
-        U, S, V = eng.rsvd(Ag, l, q=qq, seed=4242)
+        U, S, V = eng.rsvd(Ag, l, q=qq, seed=4242, a_scale=scale, lowp_intermediates=lowp)
         torch.cuda.synchronize()
         nsh = eng.info()["n_shard_rows"]
         assert (nsh == -(-(-(-n // WORLD)) // 32) * 32) if shard_n else nsh == 0, nsh
         q.put((rank, off, U.cpu().double().numpy(), S.cpu().double().numpy(), V.cpu().double().numpy(),
-               Ag.float().cpu().double().numpy()))
+               Ag.float().cpu().double().numpy() * scale))
         eng.close()
         dist.destroy_process_group()
     except Exception as e:  # pragma: no cover - reported through the queue
@@ -75,13 +78,13 @@ def _worker(rank, port, case, q, shard_n):
         q.put((rank, None, traceback.format_exc(), None, None, None))
 
 
-def _run_world2(case, shard_n=True):
+def _run_world2(case, shard_n=True, lowp=False):
     import torch.multiprocessing as mp
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, port, case, q, shard_n)) for r in range(WORLD)]
+    procs = [ctx.Process(target=_worker, args=(r, port, case, q, shard_n, lowp)) for r in range(WORLD)]
     for p in procs:
         p.start()
     res = [q.get(timeout=300) for _ in range(WORLD)]
@@ -112,15 +115,12 @@ def test_row_sharded_rank_deficient_is_orthonormal(dt, shard_n):
     assert np.all(S[2:] < (1e-9 if dt == "f64" else 1e-5) * S[0])
 
 
-@pytest.mark.parametrize("case", [(600, 300, 32, 2, "f64"), (1024, 512, 64, 2, "f32"), (2048, 1024, 128, 1, "bf16"),
-                                  (4096, 2048, 256, 2, "bf16")])
-@pytest.mark.parametrize("shard_n", [True, False])
-def test_row_sharded_world2_matches_oracle(case, shard_n):
+def _check_world2(case, shard_n, lowp=False):
     import oracle
     from conftest import rel_fro, sign_align
 
     m, n, l, qq, dt = case
-    res = _run_world2(case, shard_n)
+    res = _run_world2(case, shard_n, lowp)
     U = np.vstack([r[2] for r in res])
     A = np.vstack([r[5] for r in res])  # the values the GPU saw (bf16 / fp32 rounded)
     S0, V0 = res[0][3], res[0][4]
@@ -132,7 +132,7 @@ def test_row_sharded_world2_matches_oracle(case, shard_n):
     import rsvd_kamaneh_raganato_terrana_amd as R
 
     eng = R.Engine(0)
-    gdt = {"f64": torch.float64, "f32": torch.float32, "bf16": torch.bfloat16}[dt]
+    gdt = {"f64": torch.float64, "f32": torch.float32, "bf16": torch.bfloat16, "e4m3": torch.float8_e4m3fn}[dt]
     Om = eng.generate_omega(n, l, seed=4242, dtype=gdt).cpu().double().numpy()
     eng.close()
     Uo, So, Vo = oracle.rsvd(A, l, q=qq, Omega=Om)
@@ -143,3 +143,26 @@ def test_row_sharded_world2_matches_oracle(case, shard_n):
     assert rel_fro(sign_align(V0[:, :k], Vo[:, :k]), Vo[:, :k]) < tol_uv
     # orthonormality of the gathered U: Frobenius over l^2 entries (fp32 outputs: ~1e-6 per entry)
     assert np.linalg.norm(U.T @ U - np.eye(l)) < (1e-10 if dt == "f64" else 1e-3)
+
+
+@pytest.mark.parametrize("case", [(600, 300, 32, 2, "f64"), (1024, 512, 64, 2, "f32"), (2048, 1024, 128, 1, "bf16"),
+                                  (4096, 2048, 256, 2, "bf16")])
+@pytest.mark.parametrize("shard_n", [True, False])
+def test_row_sharded_world2_matches_oracle(case, shard_n):
+    _check_world2(case, shard_n)
+
+
+def test_row_sharded_world2_e4m3_l512_sharded_n():
+    """C5's multi-GPU path (BASELINE configs[4]): e4m3 A with one global per-tensor scale, l = 512,
+    q = 2, rows split over 2 ranks (4096 each: m and lda multiples of 16, so the sketch runs e4m3 x
+    e4m3 on the fp8 MFMA, launch_wproj_s8) with the n side sharded (A^T Q reduce-scattered, the
+    LP = 512 hi/lo panels all-gathered).  Oracle on the dequantised A and the engine's e4m3 Omega,
+    the north-star 1e-4 bar."""
+    _check_world2((8192, 2048, 512, 2, "e4m3"), True)
+
+
+def test_row_sharded_world2_lowp_intermediates_sharded_n():
+    """RSVD_FLAG_LOWP_INTERMEDIATES with the n side sharded: intermediate orthonormalisations write
+    only the bf16 hi/lo panels (no fp32 Out), which are what the all-gather moves -- the combination
+    the opt-in bench variant runs at N > 1.  0.985^i spectrum (decays across the sketch), 1e-4 bar."""
+    _check_world2((4096, 2048, 256, 2, "bf16"), True, lowp=True)

@@ -198,3 +198,17 @@ def test_image_compression_svd_recomputes_b():
 def test_unsupported_method_raises():
     with pytest.raises(ValueError):
         oracle.rsvd(np.eye(8), 4, method=7)
+
+
+@pytest.mark.skipif(not os.path.isdir("/root/reference/python"), reason="the reference is mounted only in the build container")
+def test_golden_fixtures_regenerate_byte_identical(tmp_path):
+    """tests/golden/lapack.npz is the reference's own output: make_golden.py imports
+    python/test_run_rSVD.py and python/test_run_QR.py and reads back what their process_matrix()
+    writes.  Regenerating all three fixtures must reproduce the committed bytes."""
+    import subprocess
+    import sys
+
+    subprocess.run([sys.executable, os.path.join(GOLDEN, "make_golden.py"), "/root/reference", str(tmp_path)],
+                   check=True, capture_output=True, cwd=str(tmp_path), timeout=600)
+    for f in ("inputs.npz", "lapack.npz", "philox.npz"):
+        assert (tmp_path / f).read_bytes() == open(os.path.join(GOLDEN, f), "rb").read(), f
