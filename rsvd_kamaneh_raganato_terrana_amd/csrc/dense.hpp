@@ -70,4 +70,26 @@ hipError_t launch_power_start(T* X0, int64_t rows, int l, int LP, uint64_t seed,
 // The Philox key of the power method's start vectors inside rSVD (documented in rsvd_c.h).
 uint64_t power_seed(uint64_t seed);
 
+// ---- gemm.hip: column-major building blocks of the drop-ins past 512 columns (dense_big.cpp) ----
+// C = alpha op(A) op(B) + beta C, op = transpose when ta / tb; column-major, any sizes (MFMA).
+template <typename T>
+hipError_t launch_gemm(int ta, int tb, int64_t M, int64_t N, int64_t K, T alpha, const T* A, int64_t lda, const T* B,
+                       int64_t ldb, T beta, T* C, int64_t ldc, hipStream_t s);
+// The Givens sign rule on a column-major Q (flip the leading run of untouched columns where A(j,j) < 0).
+template <typename T>
+hipError_t launch_qr_signs_cm(const T* A, int64_t lda, int64_t m, int64_t n, T* Q, int64_t ldq, hipStream_t s);
+// det(Q) > 0 for a square column-major Q (m x m): LU with partial pivoting (one launch per step,
+// W: 2 m^2 doubles, sgn: one int of workspace); flips column m - 1 when the determinant is negative.
+template <typename T>
+hipError_t launch_det_sign_cm(T* Q, int64_t ldq, int m, double* W, int* sgn, hipStream_t s);
+// Y[:, j] = e_{e0 + j} (rows x cols, column-major)
+template <typename T>
+hipError_t launch_identity_cols(T* Y, int64_t ldy, int64_t rows, int cols, int64_t e0, hipStream_t s);
+// zero the strictly lower part of a column-major rows x cols matrix
+template <typename T>
+hipError_t launch_zero_below(T* R, int64_t ldr, int64_t rows, int64_t cols, hipStream_t s);
+// D (m x n fp64, ld m) = A (column-major, ld lda)
+template <typename T>
+hipError_t launch_widen(const T* A, int64_t lda, int64_t m, int64_t n, double* D, hipStream_t s);
+
 }  // namespace rsvd

@@ -24,6 +24,9 @@
 //
 // SVD<Power> (SVD_class.hpp:183-219, src/PM.cpp:4-81): B = A^T A by the fp64 Gram kernel, then
 // the power method with deflation in one workgroup (dense.hip power_svd_kernel).
+//
+// Past 512 columns (QR with max(Q columns, n) > 512, SVD<Jacobi / ParallelJacobi> with
+// min(m, n) > 512) the blocked forms of dense_big.cpp take over.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -78,7 +81,7 @@ struct DenseWs {
         off_M32 = take(sizeof(float) * 3 * L2);
         off_S = take(sizeof(double) * LP);
         off_colflag = take(sizeof(int) * LP);
-        off_sync = take(sizeof(unsigned) * 128);
+        off_sync = take(sizeof(unsigned) * kBJSyncWords);
         total = o;
     }
 };
@@ -309,6 +312,14 @@ struct DevBuf {
 
 }  // namespace
 
+// dense_big.cpp: past the 512-column panels
+size_t qr_big_workspace(int64_t m, int64_t n, int full, int dtype);
+size_t svd_big_workspace(int64_t m, int64_t n, int dtype);
+int qr_big(rsvd_handle_t h, int64_t m, int64_t n, const void* A, int64_t lda, int dtype, int full, void* Q, int64_t ldq,
+           void* R, int64_t ldr);
+int svd_big(rsvd_handle_t h, int64_t m, int64_t n, const void* A, int64_t lda, int dtype, void* U, int64_t ldu,
+            void* S, void* V, int64_t ldv);
+
 }  // namespace rsvd
 
 using namespace rsvd;
@@ -318,7 +329,8 @@ extern "C" {
 int rsvd_qr_workspace_bytes(int64_t m, int64_t n, int32_t dtype, int32_t full, size_t* bytes) {
     if (!bytes || m < 1 || n < 1) return RSVD_ERR_INVALID_ARG;
     if (!ok_dtype(dtype)) return RSVD_ERR_UNSUPPORTED;
-    *bytes = ws_bytes(m, dense_lp(std::max(full ? m : n, n)), dtype);
+    const int64_t kq = full ? m : n;
+    *bytes = std::max(kq, n) > 512 ? qr_big_workspace(m, n, full, dtype) : ws_bytes(m, dense_lp(std::max(kq, n)), dtype);
     return RSVD_OK;
 }
 
@@ -327,6 +339,8 @@ int rsvd_svd_workspace_bytes(int64_t m, int64_t n, int32_t dtype, int32_t method
     if (!ok_dtype(dtype)) return RSVD_ERR_UNSUPPORTED;
     if (method == RSVD_SVD_POWER)
         *bytes = n > 512 ? PowerGridWs(n, std::min(m, n)).total : ws_bytes(m, (int)rup(n, 16), RSVD_F64);
+    else if (std::min(m, n) > 512)
+        *bytes = svd_big_workspace(m, n, dtype);
     else
         *bytes = ws_bytes(std::max(m, n), dense_lp(std::min(m, n)), dtype);
     return RSVD_OK;
@@ -348,14 +362,11 @@ int rsvd_qr(rsvd_handle_t h, int64_t m, int64_t n, const void* A, int64_t lda, i
         h->err = "qr_decomposition_reduced requires rows >= cols";  // Q_temp.leftCols(n), src/QR.cpp:78
         return RSVD_ERR_INVALID_ARG;
     }
-    if (std::max(kq, n) > 512) {
-        h->err = "QR is built for min(m, n) <= 512 columns (full QR: m <= 512)";
-        return RSVD_ERR_UNSUPPORTED;
-    }
     if (ldq < m || ldr < kq) {
         h->err = "bad leading dimension";
         return RSVD_ERR_INVALID_ARG;
     }
+    if (std::max(kq, n) > 512) return qr_big(h, m, n, A, lda, dtype, full, Q, ldq, R, ldr);  // dense_big.cpp
     if (dtype == RSVD_F64)
         return qr_typed<double>(h, m, n, static_cast<const double*>(A), lda, full, static_cast<double*>(Q), ldq,
                                 static_cast<double*>(R), ldr);
@@ -391,11 +402,8 @@ int rsvd_svd(rsvd_handle_t h, int64_t m, int64_t n, const void* A, int64_t lda, 
         return svd_power(h, m, n, static_cast<const double*>(A), lda, (int)dim, seed, static_cast<double*>(U), ldu,
                          static_cast<double*>(S), static_cast<double*>(V), ldv, kept);
     }
-    if (k > 512) {
-        h->err = "SVD<Jacobi> is built for min(m, n) <= 512";
-        return RSVD_ERR_UNSUPPORTED;
-    }
     *kept = (int32_t)k;
+    if (k > 512) return svd_big(h, m, n, A, lda, dtype, U, ldu, S, V, ldv);  // dense_big.cpp
     const bool ref_order = method == RSVD_SVD_PARALLEL_JACOBI;
     if (dtype == RSVD_F64)
         return svd_jacobi_typed<double>(h, m, n, static_cast<const double*>(A), lda, static_cast<double*>(U), ldu,

@@ -130,7 +130,7 @@ struct WideLayout {
         off_JJ = take(sizeof(double) * 2 * L2);
         off_M32 = take(sizeof(float) * 3 * L2);  // Rinv, Uw, Vw in fp32 (panel_gemm operand for fp32 panels)
         off_colflag = take(sizeof(int) * LP);
-        off_sync = take(sizeof(unsigned) * 128);
+        off_sync = take(sizeof(unsigned) * kBJSyncWords);
         total = o;
     }
 };
@@ -411,8 +411,10 @@ struct WideEngine {
         if (L.LP <= 64) {
             RSVD_CK(launch_small_svd<double>(R1, L.l, L.LP, Uw, Vw, Sd, h->dflags + 1, s));
         } else {
+            // fp32 results (fp32 / bf16 / e4m3 A): converged at cos <= 1e-6 -- 16 fp32 ulps, far below
+            // the 1e-4 bar -- one or two sweeps fewer than the fp64 results' 1e-12
             RSVD_CK(launch_block_jacobi<double>(R1, L.l, L.LP, JX, JJ, Uw, Vw, Sd, sync, h->dflags + 1, s,
-                                                sizeof(T) == 4 ? 1e-8 : 1e-16));  // fp32 results: one sweep fewer
+                                                sizeof(T) == 4 ? 1e-8 : 1e-16, sizeof(T) == 4 ? kBJTolF32 : kBJTolF64));
         }
         RSVD_CK(launch_convert_scale<T>(Sd, S, L.l, std::fabs(a_scale(d)), s));
         if (sizeof(T) == 4) {

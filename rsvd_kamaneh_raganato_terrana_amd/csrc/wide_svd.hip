@@ -4,22 +4,34 @@
 // As in jacobi.hip, W = R^T (R = Q_B^T B^T, so B = W Q_B^T) is diagonalised by one-sided
 // (Hestenes) Jacobi: X = W, J = I, rotate column pairs until the columns of X are orthogonal;
 // then S = column norms (descending, the reference's selection sort :164-178), U_w = X / S,
-// V_w = J.  For l > 64 the l x l problem no longer fits one workgroup, so the columns are cut
-// into NB = LP/16 blocks of 16 and paired round-robin (NB/2 disjoint block pairs per round,
-// NB - 1 rounds per sweep) over a persistent grid of NB/2 workgroups:
-//   1. Gp = X_pair^T X_pair (32 x 32, fp64 MFMA over the LP rows; exact column dot products, the
-//      same quantities the one-sided rotation angles use);
-//   2. the 32 x 32 symmetric eigenproblem of Gp by cyclic Jacobi in LDS (16 disjoint rotations
-//      per inner round, accumulated into Jp) -- each inner rotation is the one-sided rotation of
-//      the corresponding column pair of X, with the same angle formula as jacobi.hip;
-//   3. X_pair <- X_pair Jp, J_pair <- J_pair Jp (fp64 MFMA), into the other half of a double
-//      buffer (every column is owned by exactly one pair per round).
+// V_w = J.  For l > 64 the l x l problem no longer fits one workgroup: the columns are cut into
+// NB = LP/16 blocks of 16, and a sweep visits every column pair exactly once, in NB outer rounds
+// on a persistent grid of NB/2 workgroups (each owns a block pair per round):
+//   * rounds 0 .. NB-2 ("cross"): the block pairs of a round-robin tournament; inside a pair only
+//     the 16 x 16 CROSS pairs are rotated -- 16 inner rounds of 16 disjoint rotations (column k of
+//     the first block with column (k + s) % 16 of the second);
+//   * round NB-1 ("intra"): each workgroup takes two blocks and rotates the pairs INSIDE each
+//     block (15 inner rounds, round-robin per block).
+// So a sweep is the scalar cyclic Jacobi sweep with l/2 rotations in flight, l - 1 inner rounds
+// deep (the former scheme re-did every intra-block pair in every outer round: 2l inner rounds).
+// Per outer round a workgroup
+//   1. stages its 32 columns of X in LDS and forms Gp = X_pair^T X_pair (fp64 MFMA);
+//   2. runs the inner sweep on Gp: per inner round 16 lanes evaluate the angles, then 136 threads
+//      rotate the upper-triangle 2 x 2 blocks of Gp from both sides in place (Gp is symmetric:
+//      the lower half is never touched), while one wave accumulates the rotations into the 32 x 32
+//      Jp (a row per lane), one round behind, off the path between the two barriers of a round;
+//   3. X_pair <- X_pair Jp, J_pair <- J_pair Jp (fp64 MFMA) into the other half of a double buffer.
 // Rounds are separated by an agent-scope grid barrier (MI355X_MICROARCH.md "Workgroup dispatch
 // ... inter-workgroup visibility": plain stores -> vmcnt(0) -> barrier -> release fence -> relaxed
 // counter; acquire fence after the poll).  The grid (<= 16 workgroups) is always co-resident;
-// every spin is bounded and reports a timeout instead of hanging.  A sweep in which no pair has
-// an off-diagonal |g| > l eps sqrt(a b) (or only rotations already in the quadratic regime)
-// ends the iteration, as in jacobi.hip.
+// every spin is bounded and reports a timeout instead of hanging.
+// Convergence: a sweep whose rotations all had cos^2 = g^2 / (ab) <= quad2 ends the iteration (the
+// next would only square them); and when a sweep's largest pre-rotation cosine is small enough to
+// have squared below tol_chk, the whole grid checks max cos over ALL column pairs of the new X
+// (an LP x LP fp64 MFMA Gram, every workgroup a 32-column slice) and stops at <= tol_chk -- which
+// saves the confirming sweep the first rule needs.
+#include <algorithm>
+
 #include "common.hpp"
 #include "kernels.hpp"
 #include "wide.hpp"
@@ -31,9 +43,10 @@ namespace {
 typedef Mfma<double> MD;
 constexpr double kEps = 2.220446049250313e-16;
 constexpr int kMaxSweeps = 30;
-// sync layout (unsigned): [0] barrier counter, [1] abort, [2] final parity, [4 + s] sweep s rotated,
-// [36 + s] sweep s had rotations outside the quadratic regime
-constexpr int kSyncWords = 72;
+// sync layout (unsigned words): [0] barrier counter, [1] abort, [2] final parity, [4 + s] sweep s
+// rotated, [36 + s] sweep s had rotations outside the quadratic regime; u64 slots (8-B aligned):
+// [80 + 2 s] sweep s's largest pre-rotation cos^2, [144 + 2 s] the global check's max cos^2 after it
+constexpr int kSyncWords = 208;
 
 __device__ __forceinline__ void rr_pair(int round, int k, int N, int& p, int& q) {
     if (k == 0) {
@@ -73,8 +86,7 @@ __device__ bool grid_barrier(unsigned* sync, unsigned target) {
     return ok != 0;
 }
 
-constexpr int GS = 33;       // LDS pitch of the 32 x 32 blocks
-constexpr int kInnerSweeps = 1;
+constexpr int GS = 33;  // LDS pitch of the 32 x 32 blocks
 
 // Full-precision fp64 reciprocal square root / reciprocal from the hardware estimates (two
 // Newton steps each): the inner rotations need c^2 + s^2 = 1 to rounding, not IEEE division.
@@ -89,13 +101,34 @@ __device__ __forceinline__ double rcp_nr(double d) {
     return y * (2.0 - d * y);
 }
 
+// Pair k (0..15) of inner round s on the 32 local columns [block P | block Q], as (p, q) -- the
+// rotation's orientation (x_p' = c x_p - s x_q); the Gram is read through sym(), so p > q is fine:
+//   MODE 0 (cross, 16 rounds): column k of P with column (k + s) % 16 of Q;
+//   MODE 1 (intra, 15 rounds): the circle method inside each block (k < 8: block P, else block Q):
+//     pair 0 = ((s) % 15, 15), pair j = ((s + j) % 15, (s - j) % 15).
+template <int MODE>
+__device__ __forceinline__ void inner_pair(int s, int k, int& p, int& q) {
+    if (MODE == 0) {
+        p = k;
+        q = 16 + ((k + s) & 15);
+    } else {
+        const int base = k < 8 ? 0 : 16, kk = k & 7;
+        p = base + (s + kk) % 15;
+        q = base + (kk == 0 ? 15 : (s - kk + 15) % 15);
+    }
+}
+template <int MODE> constexpr int inner_rounds() { return MODE == 0 ? 16 : 15; }
+
+// (i, j) of the symmetric pair Gram, stored in its upper triangle
+__device__ __forceinline__ int sym(int i, int j) { return i < j ? i * GS + j : j * GS + i; }
+
 // Rotation of the pair (a = |x_p|^2, b = |x_q|^2, g = x_p.x_q): x_p' = c x_p - s x_q, x_q' = s x_p + c x_q
 // zeroes the cross term (jacobi.hip formula: t = sign(d g) |2g| / (|d| + sqrt(d^2 + 4 g^2)), d = b - a,
 // c = (1 + t^2)^-1/2, s = c t), evaluated on operands scaled by max(|d|, |2g|) (no overflow / underflow
 // for any finite a, b, g)
 __device__ __forceinline__ void pair_angle(const double* G, int p, int q, double tol2, double negl, double& c,
                                            double& s, bool& rot) {
-    const double a = G[p * GS + p], b = G[q * GS + q], g = G[p * GS + q];
+    const double a = G[p * GS + p], b = G[q * GS + q], g = G[sym(p, q)];
     rot = g != 0.0 && g * g > tol2 * a * b && a > negl && b > negl;
     const double d = b - a, g2 = 2.0 * g;
     const double inv = rcp_nr(fmax(fmax(fabs(d), fabs(g2)), 1e-300));
@@ -108,10 +141,95 @@ __device__ __forceinline__ void pair_angle(const double* G, int p, int q, double
     s = rot ? cc * t : 0.0;
 }
 
-size_t block_jacobi_lds(int LP) { return ((size_t)32 * (LP + 1) + 3 * 32 * GS) * sizeof(double); }
+size_t block_jacobi_lds(int MR) { return ((MR <= 512 ? (size_t)32 * (MR + 1) : 0) + 3 * 32 * GS) * sizeof(double); }
+
+constexpr int kBJThreads = 512;  // 8 waves: 2 per SIMD for the MFMA phases
+
+template <int MODE>
+__device__ __forceinline__ void jp_round(double* Jrow, const double* A, int s) {
+    // the 16 rotations of inner round s on one row of Jp (columns p, q of pair k; the pairs are
+    // disjoint), four pairs' loads in flight at a time
+#pragma unroll
+    for (int k0 = 0; k0 < 16; k0 += 4) {
+        double x[4], y[4];
+        int p[4], q[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            inner_pair<MODE>(s, k0 + u, p[u], q[u]);
+            x[u] = Jrow[p[u]];
+            y[u] = Jrow[q[u]];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const double c = A[k0 + u], sn = A[16 + k0 + u];
+            Jrow[p[u]] = c * x[u] - sn * y[u];
+            Jrow[q[u]] = sn * x[u] + c * y[u];
+        }
+    }
+}
+
+// One inner sweep of MODE on the pair Gram G (32 x 32, upper triangle, in place).  Ang: 2 x 32
+// doubles (c[16], s[16] per round, double-buffered).  bk <= bk2: this thread's 2 x 2 block (tid <
+// 136).  The Jp wave (tid 256..287, row jr = tid - 256 of Jp in LDS) applies round s - 1's
+// rotations to its row while round s's angles are evaluated (one round behind: off the critical
+// path of the two barriers per round).
+template <int MODE>
+__device__ __forceinline__ void inner_sweep(double* G, double* Jp, double* Ang, int tid, int bk, int bk2,
+                                            double tol2, double negl) {
+    constexpr int NR = inner_rounds<MODE>();
+    const bool jwave = tid >= 256 && tid < 288;
+    double* Jrow = Jp + (tid - 256) * GS;
+    if (jwave) {
+#pragma unroll
+        for (int j = 0; j < 32; ++j) Jrow[j] = (j == tid - 256) ? 1.0 : 0.0;
+    }
+    for (int s = 0; s < NR; ++s) {
+        double* A = Ang + 32 * (s & 1);
+        if (tid < 16) {
+            int p, q;
+            inner_pair<MODE>(s, tid, p, q);
+            double c, sn;
+            bool rt;
+            pair_angle(G, p, q, tol2, negl, c, sn, rt);
+            A[tid] = c;
+            A[16 + tid] = sn;
+        } else if (jwave && s > 0) {
+            jp_round<MODE>(Jrow, Ang + 32 * ((s - 1) & 1), s - 1);
+        }
+        __syncthreads();
+        if (tid < 136) {
+            int p1, q1, p2, q2;
+            inner_pair<MODE>(s, bk, p1, q1);
+            inner_pair<MODE>(s, bk2, p2, q2);
+            const double c1 = A[bk], s1 = A[16 + bk];
+            if (bk == bk2) {
+                const int ig = sym(p1, q1);
+                const double a = G[p1 * GS + p1], g = G[ig], b = G[q1 * GS + q1];
+                const double l00 = c1 * a - s1 * g, l01 = c1 * g - s1 * b;
+                const double l10 = s1 * a + c1 * g, l11 = s1 * g + c1 * b;
+                G[p1 * GS + p1] = c1 * l00 - s1 * l01;
+                G[ig] = s1 * l00 + c1 * l01;
+                G[q1 * GS + q1] = s1 * l10 + c1 * l11;
+            } else {
+                const double c2 = A[bk2], s2 = A[16 + bk2];
+                const int i00 = sym(p1, p2), i01 = sym(p1, q2), i10 = sym(q1, p2), i11 = sym(q1, q2);
+                const double b00 = G[i00], b01 = G[i01], b10 = G[i10], b11 = G[i11];
+                // left: rows (p, q) <- (c1 row_p - s1 row_q, s1 row_p + c1 row_q)
+                const double l00 = c1 * b00 - s1 * b10, l01 = c1 * b01 - s1 * b11;
+                const double l10 = s1 * b00 + c1 * b10, l11 = s1 * b01 + c1 * b11;
+                // right: cols (p2, q2) <- (c2 col_p2 - s2 col_q2, s2 col_p2 + c2 col_q2)
+                G[i00] = c2 * l00 - s2 * l01;
+                G[i01] = s2 * l00 + c2 * l01;
+                G[i10] = c2 * l10 - s2 * l11;
+                G[i11] = s2 * l10 + c2 * l11;
+            }
+        }
+        __syncthreads();
+    }
+    if (jwave) jp_round<MODE>(Jrow, Ang + 32 * ((NR - 1) & 1), NR - 1);
+}
 
 // Stage the 32 columns col(0..31) of a column-major LP x LP matrix into LDS rows of pitch LP + 1.
-constexpr int kBJThreads = 512;  // 8 waves: 2 per SIMD for the MFMA phases
 
 // 32 LP / 2 double2: each thread keeps up to 4 loads in flight.
 template <typename F>
@@ -163,22 +281,6 @@ __device__ __forceinline__ void apply_pair(const double* Xs, const double* Jp, d
     }
 }
 
-#ifdef RSVD_BJ_PROF
-__device__ long long g_bj_prof[8];
-#define BJ_T(k)                                                \
-    do {                                                       \
-        if (wg == 0 && tid == 0) {                             \
-            const long long now_ = wall_clock64();             \
-            bj_acc[(k)] += now_ - bj_last;                     \
-            bj_last = now_;                                    \
-        }                                                      \
-    } while (0)
-#else
-#define BJ_T(k) \
-    do {        \
-    } while (0)
-#endif
-
 // The same product with the pair's columns read straight from global memory (column-major source:
 // the 16 lanes of an MFMA row read 128 contiguous bytes of one column), all 8 k-steps in flight.
 template <typename F>
@@ -203,26 +305,130 @@ __device__ __forceinline__ void apply_pair_global(const double* __restrict__ Src
     }
 }
 
-__global__ __launch_bounds__(kBJThreads) void block_jacobi_kernel(const double* __restrict__ R, int l, int LP,
+#ifdef RSVD_BJ_PROF
+__device__ long long g_bj_prof[8];
+#define BJ_T(k)                                                \
+    do {                                                       \
+        if (wg == 0 && tid == 0) {                             \
+            const long long now_ = wall_clock64();             \
+            bj_acc[(k)] += now_ - bj_last;                     \
+            bj_last = now_;                                    \
+        }                                                      \
+    } while (0)
+#else
+#define BJ_T(k) \
+    do {        \
+    } while (0)
+#endif
+
+// Gp = X_pair^T X_pair with the pair's columns read from global memory (MR > 512 rows: no LDS
+// image), wave w -> tile ((w >> 1) & 1, w & 1) over row half w >> 2; the halves land in Ga / Gb.
+template <typename F>
+__device__ __forceinline__ void pair_gram_global(const double* __restrict__ X, int MR, F col, int w, int r, int h,
+                                                 double* Ga, double* Gb) {
+    const int ta = (w >> 1) & 1, tb = w & 1, half = w >> 2;
+    const double* xa = X + (int64_t)col(16 * ta + r) * MR + 4 * h;
+    const double* xb = X + (int64_t)col(16 * tb + r) * MR + 4 * h;
+    f64x4 acc[2] = {MD::zero(), MD::zero()};
+    const int ibeg = half * (MR / 2), iend = ibeg + MR / 2;
+    for (int i0 = ibeg; i0 < iend; i0 += 16) {
+        const double2 a01 = *reinterpret_cast<const double2*>(xa + i0);
+        const double2 a23 = *reinterpret_cast<const double2*>(xa + i0 + 2);
+        const double2 b01 = *reinterpret_cast<const double2*>(xb + i0);
+        const double2 b23 = *reinterpret_cast<const double2*>(xb + i0 + 2);
+        acc[0] = MD::mma(a01.x, b01.x, acc[0]);
+        acc[1] = MD::mma(a01.y, b01.y, acc[1]);
+        acc[0] = MD::mma(a23.x, b23.x, acc[0]);
+        acc[1] = MD::mma(a23.y, b23.y, acc[1]);
+    }
+    double* Gd = half ? Gb : Ga;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) Gd[(16 * ta + MD::row(h, j)) * GS + 16 * tb + r] = acc[0][j] + acc[1][j];
+}
+
+__device__ __forceinline__ double u64_as_double(unsigned long long v) { return __longlong_as_double((long long)v); }
+
+// max cos^2 over the column pairs (a, b), a in this workgroup's 32 columns [32 wg, 32 wg + 32), b any,
+// of the MR x LP column-major X (global, after an acquire): 16 x 16 Gram tiles on the fp64 MFMA,
+// the column norms accumulated from the same operand loads.  Columns with norm^2 <= negl (and the
+// zero padding) are excluded, as the rotations exclude them.
+__device__ double slice_max_cos2(const double* __restrict__ X, int MR, int LP, int wg, int w, int lane, double negl) {
+    const int r = lane & 15, h = lane >> 4;
+    double mx = 0.0;
+    const int ntile = 2 * (LP / 16);
+    for (int t = w; t < ntile; t += kBJThreads / 64) {
+        const int a0 = 32 * wg + 16 * (t & 1), b0 = 16 * (t >> 1);
+        const double* xa = X + (int64_t)(a0 + r) * MR + 4 * h;
+        const double* xb = X + (int64_t)(b0 + r) * MR + 4 * h;
+        f64x4 acc = MD::zero();
+        double na = 0.0, nb = 0.0;
+        for (int i0 = 0; i0 < MR; i0 += 16) {
+            const double2 a01 = *reinterpret_cast<const double2*>(xa + i0);
+            const double2 a23 = *reinterpret_cast<const double2*>(xa + i0 + 2);
+            const double2 b01 = *reinterpret_cast<const double2*>(xb + i0);
+            const double2 b23 = *reinterpret_cast<const double2*>(xb + i0 + 2);
+            // k order inside the 16-row chunk is 4h + j for both operands (the sum is order-free)
+            acc = MD::mma(a01.x, b01.x, acc);
+            acc = MD::mma(a01.y, b01.y, acc);
+            acc = MD::mma(a23.x, b23.x, acc);
+            acc = MD::mma(a23.y, b23.y, acc);
+            na += a01.x * a01.x + a01.y * a01.y + a23.x * a23.x + a23.y * a23.y;
+            nb += b01.x * b01.x + b01.y * b01.y + b23.x * b23.x + b23.y * b23.y;
+        }
+        na += __shfl_xor(na, 16, 64);
+        na += __shfl_xor(na, 32, 64);
+        nb += __shfl_xor(nb, 16, 64);
+        nb += __shfl_xor(nb, 32, 64);
+        // C/D (f64): col = lane & 15 (b0 + col), row = h + 4 reg (a0 + row)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int row = MD::row(h, j);
+            const double nar = __shfl(na, row, 64);
+            const double g = acc[j];
+            if (a0 + row != b0 + r && nar > negl && nb > negl) mx = fmax(mx, (g * g) / (nar * nb));
+        }
+    }
+    return mx;
+}
+
+// X = the mrv x l source (column-major with ld lds, or row-major when src_rowmajor: X = src^T),
+// zero-padded to MR x LP (MR, LP multiples of 32); J = I (LP x LP).  MR <= 512: the pair's columns
+// are staged in LDS; beyond, the pair Gram and the X product read them from global memory.
+__global__ __launch_bounds__(kBJThreads) void block_jacobi_kernel(const double* __restrict__ R, int64_t lds,
+                                                           int src_rowmajor, int mrv, int l, int MR, int LP,
                                                            double* __restrict__ Xb, double* __restrict__ Jb,
                                                            double* __restrict__ scratch, unsigned* __restrict__ sync,
-                                                           int* __restrict__ info, double quad2) {
+                                                           int* __restrict__ info, double quad2, double tol_chk2) {
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-    const int XP = LP + 1;
-    double* Xs = reinterpret_cast<double*>(smem_raw);  // [32][LP + 1]: the pair's columns
-    double* Ga = Xs + 32 * XP;                         // [32][GS] x 2: the pair Gram, double-buffered
+    const bool staged = MR <= 512;
+    const int XP = MR + 1;
+    double* Xs = reinterpret_cast<double*>(smem_raw);  // [32][MR + 1]: the pair's columns (staged)
+    double* Ga = Xs + (staged ? 32 * XP : 0);          // [32][GS] x 2: the pair Gram (Gb: the MFMA half)
     double* Gb = Ga + 32 * GS;
     double* Jp = Gb + 32 * GS;                         // [32][GS] accumulated inner rotation
     __shared__ int flags[8];
     __shared__ double fro;
-    __shared__ double Ang[32];  // c, s of the 16 pairs of an inner round
-    __shared__ int Rot[16];
+    __shared__ double Ang[64];  // c, s of the 16 pairs of an inner round, double-buffered
+    __shared__ unsigned long long lmax;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int r = lane & 15, h = lane >> 4;
     const int nwg = gridDim.x, wg = blockIdx.x;
     const int NB = LP / 16;
-    const int64_t L2 = (int64_t)LP * LP;
+    const int64_t L2 = (int64_t)LP * LP, L2X = (int64_t)MR * LP;
     const double tol = (double)l * kEps, tol2 = tol * tol;
+    unsigned long long* smax = reinterpret_cast<unsigned long long*>(sync + 80);
+    unsigned long long* cmax = reinterpret_cast<unsigned long long*>(sync + 144);
+    // this thread's upper-triangle 2 x 2 block (bk <= bk2) of the inner update, tid < 136
+    int bk = 0, bk2 = 0;
+    {
+        int t = tid < 136 ? tid : 0, k = 0;
+        while (t >= 16 - k) {
+            t -= 16 - k;
+            ++k;
+        }
+        bk = k;
+        bk2 = k + t;
+    }
 #ifdef RSVD_BJ_PROF
     long long bj_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     long long bj_last = wall_clock64();
@@ -233,13 +439,12 @@ __global__ __launch_bounds__(kBJThreads) void block_jacobi_kernel(const double* 
     {
         double part = 0.0;
         for (int c = wg; c < LP; c += nwg) {
-            const int64_t o = (int64_t)c * LP;
-            for (int i = tid; i < LP; i += kBJThreads) {
-                const double v = (c < l && i < l) ? R[o + i] : 0.0;
-                Xb[o + i] = v;
-                Jb[o + i] = (c == i && c < l) ? 1.0 : 0.0;
+            for (int i = tid; i < MR; i += kBJThreads) {
+                const double v = (c < l && i < mrv) ? (src_rowmajor ? R[(int64_t)i * lds + c] : R[(int64_t)c * lds + i]) : 0.0;
+                Xb[(int64_t)c * MR + i] = v;
                 part += v * v;
             }
+            for (int i = tid; i < LP; i += kBJThreads) Jb[(int64_t)c * LP + i] = (c == i && c < l) ? 1.0 : 0.0;
         }
         if (tid == 0) fro = 0.0;
         __syncthreads();
@@ -261,28 +466,36 @@ __global__ __launch_bounds__(kBJThreads) void block_jacobi_kernel(const double* 
     BJ_T(0);
     int par = 0, sweeps = 0;
     for (int sweep = 0; sweep < kMaxSweeps; ++sweep) {
-        for (int round = 0; round < NB - 1; ++round) {
+        for (int round = 0; round < NB; ++round) {
+            const bool intra = round == NB - 1;
             int P, Q;
-            rr_pair(round, wg, NB, P, Q);
-            const double* Xsrc = Xb + (size_t)par * L2;
+            if (intra) {
+                P = 2 * wg;
+                Q = 2 * wg + 1;
+            } else {
+                rr_pair(round, wg, NB, P, Q);
+            }
+            const double* Xsrc = Xb + (size_t)par * L2X;
             const double* Jsrc = Jb + (size_t)par * L2;
-            double* Xd = Xb + (size_t)(1 - par) * L2;
+            double* Xd = Xb + (size_t)(1 - par) * L2X;
             double* Jd = Jb + (size_t)(1 - par) * L2;
             auto col = [&](int k) { return k < 16 ? 16 * P + k : 16 * Q + k - 16; };
             // 1. the pair's columns of X into LDS
-            stage_pair(Xs, Xsrc, LP, col);
+            if (staged) stage_pair(Xs, Xsrc, MR, col);
             if (tid < 8) flags[tid] = 0;
-            for (int e = tid; e < 32 * 32; e += kBJThreads) Jp[(e / 32) * GS + e % 32] = (e / 32 == e % 32) ? 1.0 : 0.0;
+            if (tid == 0) lmax = 0ull;
             __syncthreads();
             BJ_T(1);
             // 2. Gp = X_pair^T X_pair: wave w -> tile ((w >> 1) & 1, w & 1) over row half w >> 2 (four
             //    independent MFMA chains); the halves meet in Ga (half 0) + Gb (half 1)
-            {
+            if (!staged) {
+                pair_gram_global(Xsrc, MR, col, w, r, h, Ga, Gb);
+            } else {
                 const int ta = (w >> 1) & 1, tb = w & 1, half = w >> 2;
                 const double* xa = Xs + (16 * ta + r) * XP + h;
                 const double* xb = Xs + (16 * tb + r) * XP + h;
                 f64x4 acc[4] = {MD::zero(), MD::zero(), MD::zero(), MD::zero()};
-                const int ibeg = half * (LP / 2), iend = ibeg + LP / 2;
+                const int ibeg = half * (MR / 2), iend = ibeg + MR / 2;
                 for (int i0 = ibeg; i0 < iend; i0 += 16) {
 #pragma unroll
                     for (int u = 0; u < 4; ++u) acc[u] = MD::mma(xa[i0 + 4 * u], xb[i0 + 4 * u], acc[u]);
@@ -299,95 +512,53 @@ __global__ __launch_bounds__(kBJThreads) void block_jacobi_kernel(const double* 
             }
             __syncthreads();
             BJ_T(2);
-            // 3. convergence test on the fresh Gram
+            // 3. convergence test on the fresh Gram, over the pairs this round rotates
             for (int e = tid; e < 32 * 32; e += kBJThreads) {
                 const int i = e / 32, j = e % 32;
-                if (i < j) {
+                const bool mine = intra ? (i < j && (i < 16) == (j < 16)) : (i < 16 && j >= 16);
+                if (mine) {
                     const double a = Ga[i * GS + i], b = Ga[j * GS + j], g = Ga[i * GS + j];
-                    if (g != 0.0 && g * g > tol2 * a * b && a > negl && b > negl) {
-                        flags[0] = 1;
-                        if (g * g > quad2 * a * b) flags[1] = 1;
+                    if (a > negl && b > negl) {
+                        const double c2 = (g * g) / (a * b);
+                        atomicMax(&lmax, (unsigned long long)__double_as_longlong(c2));
+                        if (g != 0.0 && g * g > tol2 * a * b) {
+                            flags[0] = 1;
+                            if (g * g > quad2 * a * b) flags[1] = 1;
+                        }
                     }
                 }
             }
             __syncthreads();
+            if (tid == 0 && lmax) atomicMax(smax + sweep, lmax);
             if (flags[0]) {
                 if (tid == 0) {
                     __hip_atomic_store(sync + 4 + sweep, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     if (flags[1]) __hip_atomic_store(sync + 36 + sweep, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
-                // 4. inner cyclic Jacobi on Gp, two phases per inner round: (a) lanes 0..15 compute the
-                //    angles of the 16 disjoint pairs into LDS; (b) thread (k, k2) < 256 rotates the 2x2 block
-                //    (pair k rows, pair k2 columns) from both sides into the other G buffer, while threads
-                //    256.. rotate the columns of Jp (Jp <- Jp J)
-                const int k = (tid >> 4) & 15, k2 = tid & 15;
-                double* cur = Ga;
-                double* nxt = Gb;
-                for (int isw = 0; isw < kInnerSweeps; ++isw) {
-                    bool any = false;
-                    for (int ir = 0; ir < 31; ++ir) {
-                        if (tid < 16) {
-                            int p, q;
-                            rr_pair(ir, tid, 32, p, q);
-                            double c, sn;
-                            bool rt;
-                            pair_angle(cur, p, q, tol2, negl, c, sn, rt);
-                            Ang[tid] = c;
-                            Ang[16 + tid] = sn;
-                            Rot[tid] = rt;
-                            if (rt) any = true;
-                        }
-                        __syncthreads();
-                        int p2, q2;
-                        rr_pair(ir, k2, 32, p2, q2);
-                        const double c2 = Ang[k2], s2 = Ang[16 + k2];
-                        if (tid < 256) {
-                            int p, q;
-                            rr_pair(ir, k, 32, p, q);
-                            const double c1 = Ang[k], s1 = Ang[16 + k];
-                            const double b00 = cur[p * GS + p2], b01 = cur[p * GS + q2];
-                            const double b10 = cur[q * GS + p2], b11 = cur[q * GS + q2];
-                            // left: rows (p, q) <- (c1 row_p - s1 row_q, s1 row_p + c1 row_q)
-                            const double l00 = c1 * b00 - s1 * b10, l01 = c1 * b01 - s1 * b11;
-                            const double l10 = s1 * b00 + c1 * b10, l11 = s1 * b01 + c1 * b11;
-                            // right: cols (p2, q2) <- (c2 col_p2 - s2 col_q2, s2 col_p2 + c2 col_q2)
-                            nxt[p * GS + p2] = c2 * l00 - s2 * l01;
-                            nxt[p * GS + q2] = s2 * l00 + c2 * l01;
-                            nxt[q * GS + p2] = c2 * l10 - s2 * l11;
-                            nxt[q * GS + q2] = s2 * l10 + c2 * l11;
-                        } else if (Rot[k2]) {
-                            // Jp columns (p2, q2) of pair k2, rows k and k + 16 (disjoint per thread)
-#pragma unroll
-                            for (int rr = 0; rr < 2; ++rr) {
-                                const int row = k + 16 * rr;
-                                const double jp = Jp[row * GS + p2], jq = Jp[row * GS + q2];
-                                Jp[row * GS + p2] = c2 * jp - s2 * jq;
-                                Jp[row * GS + q2] = s2 * jp + c2 * jq;
-                            }
-                        }
-                        __syncthreads();
-                        double* t = cur;
-                        cur = nxt;
-                        nxt = t;
-                    }
-                    if (any) flags[2 + (isw & 1)] = 1;
-                    __syncthreads();
-                    const bool more = flags[2 + (isw & 1)] != 0;
-                    if (tid == 0) flags[2 + ((isw + 1) & 1)] = 0;
-                    __syncthreads();
-                    if (!more) break;
-                }
+                // 4. the inner sweep on Gp (in place; Jp from the register wave)
+                if (intra)
+                    inner_sweep<1>(Ga, Jp, Ang, tid, bk, bk2, tol2, negl);
+                else
+                    inner_sweep<0>(Ga, Jp, Ang, tid, bk, bk2, tol2, negl);
+                __syncthreads();
                 BJ_T(3);
                 // 5. X_pair Jp and J_pair Jp -> destination buffer
-                apply_pair(Xs, Jp, Xd, LP, col, w, r, h);
+                if (staged)
+                    apply_pair(Xs, Jp, Xd, MR, col, w, r, h);
+                else
+                    apply_pair_global(Xsrc, Jp, Xd, MR, col, w, r, h);
                 BJ_T(4);
                 apply_pair_global(Jsrc, Jp, Jd, LP, col, w, r, h);
                 BJ_T(5);
             } else {
+                for (int e = tid; e < 32 * (MR / 2); e += kBJThreads) {
+                    const int kk = e / (MR / 2), i = 2 * (e % (MR / 2));
+                    const int64_t o = (int64_t)col(kk) * MR + i;
+                    *reinterpret_cast<double2*>(Xd + o) = *reinterpret_cast<const double2*>(Xsrc + o);
+                }
                 for (int e = tid; e < 32 * (LP / 2); e += kBJThreads) {
                     const int kk = e / (LP / 2), i = 2 * (e % (LP / 2));
                     const int64_t o = (int64_t)col(kk) * LP + i;
-                    *reinterpret_cast<double2*>(Xd + o) = *reinterpret_cast<const double2*>(Xsrc + o);
                     *reinterpret_cast<double2*>(Jd + o) = *reinterpret_cast<const double2*>(Jsrc + o);
                 }
             }
@@ -403,6 +574,22 @@ __global__ __launch_bounds__(kBJThreads) void block_jacobi_kernel(const double* 
         const unsigned rot = __hip_atomic_load(sync + 4 + sweep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const unsigned big = __hip_atomic_load(sync + 36 + sweep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (rot == 0 || big == 0) break;
+        // the global check, once the sweep's rotations were small enough to have squared below tol_chk2
+        const double pre = u64_as_double(__hip_atomic_load(smax + sweep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        if (tol_chk2 > 0.0 && pre <= 1e3 * tol_chk2) {
+            const double mx = slice_max_cos2(Xb + (size_t)par * L2X, MR, LP, wg, w, lane, negl);
+            if (tid == 0) lmax = 0ull;
+            __syncthreads();
+            atomicMax(&lmax, (unsigned long long)__double_as_longlong(mx));
+            __syncthreads();
+            if (tid == 0) atomicMax(cmax + sweep, lmax);
+            if (!grid_barrier(sync, (unsigned)nwg * ++bar)) {
+                if (tid == 0) info[2] = 1;
+                return;
+            }
+            const double post = u64_as_double(__hip_atomic_load(cmax + sweep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            if (post <= tol_chk2) break;
+        }
     }
     if (wg == 0 && tid == 0) {
         sync[2] = (unsigned)par;
@@ -413,17 +600,17 @@ __global__ __launch_bounds__(kBJThreads) void block_jacobi_kernel(const double* 
     }
 }
 
-// S, U_w = X / S (sorted descending, completed to orthonormal where S = 0), V_w = J, in three
+// S, U_w = X / S (sorted descending, completed to orthonormal where S = 0), V_w = J, in four
 // launches: (1) one workgroup: column norms, descending ranks, S, and the sorted norms + inverse
-// permutation to scratch (the free half of the X double buffer); (2) a grid of 64 x 64 tiles:
-// U_w[i][k] = X[inv[k]][i] / s_k, V_w[i][k] = J[inv[k]][i] through an LDS transpose (coalesced
-// reads along i and writes along k -- one workgroup scattering 8-B values down the columns of
-// row-major U_w / V_w ran 0.7 ms at LP = 512); (3) one workgroup: completion of U_w for zero
-// singular values (returns at once when there are none).  Uw / Vw row-major [row][col], LP x LP.
+// permutation to scratch (the free half of the X double buffer); (2, 3) grids of 64 x 64 tiles:
+// U_w[i][k] = X[inv[k]][i] / s_k (MR rows), V_w[i][k] = J[inv[k]][i] (LP rows), through an LDS
+// transpose (coalesced reads along i and writes along k -- one workgroup scattering 8-B values down
+// the columns of row-major U_w / V_w ran 0.7 ms at LP = 512); (4) one workgroup: completion of U_w
+// for zero singular values (returns at once when there are none).  U_w row-major [row][col], MR x LP;
+// V_w LP x LP.
 template <typename T>
-__global__ __launch_bounds__(1024) void block_jacobi_finish_kernel(const double* __restrict__ Xb,
-                                                                   int l, int LP,
-                                                                   const unsigned* __restrict__ sync,
+__global__ __launch_bounds__(1024) void block_jacobi_finish_kernel(const double* __restrict__ Xb, int l, int MR,
+                                                                   int LP, const unsigned* __restrict__ sync,
                                                                    T* __restrict__ S) {
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
     double* sig = reinterpret_cast<double*>(smem_raw);  // [LP]
@@ -431,21 +618,21 @@ __global__ __launch_bounds__(1024) void block_jacobi_finish_kernel(const double*
     int* rank = reinterpret_cast<int*>(v + LP);         // [LP]
     int* misc = rank + LP;                              // [4]
     const int tid = threadIdx.x, nt = blockDim.x;
-    const int64_t L2 = (int64_t)LP * LP;
+    const int64_t L2X = (int64_t)MR * LP;
     const int par = (int)sync[2];
-    const double* X = Xb + (size_t)par * L2;
-    double* sigk = const_cast<double*>(Xb) + (size_t)(1 - par) * L2;  // scratch: [LP] sorted norms
-    int* inv = reinterpret_cast<int*>(sigk + LP);                     // [LP] column of rank k
+    const double* X = Xb + (size_t)par * L2X;
+    double* sigk = const_cast<double*>(Xb) + (size_t)(1 - par) * L2X;  // scratch: [LP] sorted norms
+    int* inv = reinterpret_cast<int*>(sigk + LP);                      // [LP] column of rank k
     // squared column norms: one wave per column, coalesced loads + a wave reduction, four columns
     // per wave in flight (a column at a time left every wave waiting out one L2 round trip per column)
     const int lane = tid & 63, wv = tid >> 6, nw = nt >> 6;
     for (int c0 = wv; c0 < LP; c0 += 4 * nw) {
         double s2[4] = {0.0, 0.0, 0.0, 0.0};
-        for (int i = lane; i < LP; i += 64) {
+        for (int i = lane; i < MR; i += 64) {
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
                 const int c = c0 + u * nw;
-                const double x = (c < l) ? X[(int64_t)c * LP + i] : 0.0;
+                const double x = (c < l) ? X[(int64_t)c * MR + i] : 0.0;
                 s2[u] += x * x;
             }
         }
@@ -484,55 +671,49 @@ __global__ __launch_bounds__(1024) void block_jacobi_finish_kernel(const double*
     }
 }
 
-template <typename T>
-__global__ __launch_bounds__(256) void block_jacobi_scatter_kernel(const double* __restrict__ Xb,
-                                                                    const double* __restrict__ Jb, int l, int LP,
-                                                                    const unsigned* __restrict__ sync,
-                                                                    double* __restrict__ Uw, double* __restrict__ Vw) {
+// Dst[i][k] = Src[inv[k]][i] (/ s_k when scale), i < rows (rows >= rows_valid are zero), k < LP
+__global__ __launch_bounds__(256) void block_jacobi_scatter_kernel(const double* __restrict__ base, int64_t buf_stride,
+                                                                   const double* __restrict__ Xb, int64_t x_stride,
+                                                                   int rows_valid, int rows, int l, int LP,
+                                                                   const unsigned* __restrict__ sync, int scale,
+                                                                   double* __restrict__ Dst) {
     __shared__ double tile[64][65];
     __shared__ double rs[64];
     __shared__ int col[64];
     const int tid = threadIdx.x;
-    const int nb = (LP + 63) / 64;  // LP is a multiple of 32: the last tile row / column may be half
-    const int k0 = 64 * (blockIdx.x % nb), i0 = 64 * (blockIdx.x / nb);
-    const int64_t L2 = (int64_t)LP * LP;
+    const int nbk = (LP + 63) / 64;  // LP is a multiple of 32: the last tile column may be half
+    const int k0 = 64 * (blockIdx.x % nbk), i0 = 64 * (blockIdx.x / nbk);
     const int par = (int)sync[2];
-    const double* X = Xb + (size_t)par * L2;
-    const double* J = Jb + (size_t)par * L2;
-    const double* sigk = Xb + (size_t)(1 - par) * L2;
+    const double* src = base + (size_t)par * buf_stride;
+    const double* sigk = Xb + (size_t)(1 - par) * x_stride;
     const int* inv = reinterpret_cast<const int*>(sigk + LP);
     if (tid < 64) {
         const int k = k0 + tid;
         const double sc = k < l ? sigk[k] : 0.0;
         col[tid] = k < l ? inv[k] : -1;
-        rs[tid] = sc > 0.0 ? 1.0 / sc : 0.0;
+        rs[tid] = !scale ? 1.0 : (sc > 0.0 ? 1.0 / sc : 0.0);
     }
     __syncthreads();
-    for (int pass = 0; pass < 2; ++pass) {  // 0: V_w from J, 1: U_w from X
-        const double* src = pass ? X : J;
-        for (int e = tid; e < 64 * 64; e += 256) {
-            const int kk = e >> 6, ii = e & 63;
-            const int c = col[kk], i = i0 + ii;
-            double x = 0.0;
-            if (c >= 0 && i < l) x = src[(int64_t)c * LP + i] * (pass ? rs[kk] : 1.0);
-            tile[kk][ii] = x;
-        }
-        __syncthreads();
-        double* dst = pass ? Uw : Vw;
-        for (int e = tid; e < 64 * 64; e += 256) {
-            const int ii = e >> 6, kk = e & 63;
-            if (i0 + ii < LP && k0 + kk < LP) dst[(int64_t)(i0 + ii) * LP + k0 + kk] = tile[kk][ii];
-        }
-        __syncthreads();
+    for (int e = tid; e < 64 * 64; e += 256) {
+        const int kk = e >> 6, ii = e & 63;
+        const int c = col[kk], i = i0 + ii;
+        double x = 0.0;
+        if (c >= 0 && i < rows_valid) x = src[(int64_t)c * rows + i] * rs[kk];
+        tile[kk][ii] = x;
+    }
+    __syncthreads();
+    for (int e = tid; e < 64 * 64; e += 256) {
+        const int ii = e >> 6, kk = e & 63;
+        if (i0 + ii < rows && k0 + kk < LP) Dst[(int64_t)(i0 + ii) * LP + k0 + kk] = tile[kk][ii];
     }
 }
 
 template <typename T>
-__global__ __launch_bounds__(1024) void block_jacobi_complete_kernel(const T* __restrict__ S, int l, int LP,
-                                                                     double* __restrict__ Uw) {
+__global__ __launch_bounds__(1024) void block_jacobi_complete_kernel(const T* __restrict__ S, int l, int rows_valid,
+                                                                     int LP, double* __restrict__ Uw) {
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-    double* v = reinterpret_cast<double*>(smem_raw);  // [LP]
-    int* misc = reinterpret_cast<int*>(v + LP);        // [4]
+    double* v = reinterpret_cast<double*>(smem_raw);  // [max(rows_valid, LP)]
+    __shared__ int misc[2];
     const int tid = threadIdx.x, nt = blockDim.x;
     if (tid == 0) misc[1] = 0;
     __syncthreads();
@@ -543,30 +724,30 @@ __global__ __launch_bounds__(1024) void block_jacobi_complete_kernel(const T* __
     const int nz = misc[1];
     // complete U_w for zero singular values (as jacobi.hip): least-covered unit vector, CGS2
     for (int k = nz; k < l; ++k) {
-        for (int i = tid; i < LP; i += nt) {
+        for (int i = tid; i < rows_valid; i += nt) {
             double cov = 0.0;
             for (int j = 0; j < k; ++j) cov += Uw[(int64_t)i * LP + j] * Uw[(int64_t)i * LP + j];
-            v[i] = (i < l) ? cov : 1e300;
+            v[i] = cov;
         }
         __syncthreads();
         if (tid == 0) {
             int best = 0;
-            for (int i = 1; i < l; ++i)
+            for (int i = 1; i < rows_valid; ++i)
                 if (v[i] < v[best]) best = i;
             misc[0] = best;
         }
         __syncthreads();
         const int cand = misc[0];
-        for (int i = tid; i < LP; i += nt) Uw[(int64_t)i * LP + k] = (i == cand) ? 1.0 : 0.0;
+        for (int i = tid; i < rows_valid; i += nt) Uw[(int64_t)i * LP + k] = (i == cand) ? 1.0 : 0.0;
         __syncthreads();
         for (int pass = 0; pass < 2; ++pass) {
             for (int j = tid; j < k; j += nt) {
                 double d = 0.0;
-                for (int i = 0; i < l; ++i) d += Uw[(int64_t)i * LP + j] * Uw[(int64_t)i * LP + k];
+                for (int i = 0; i < rows_valid; ++i) d += Uw[(int64_t)i * LP + j] * Uw[(int64_t)i * LP + k];
                 v[j] = d;
             }
             __syncthreads();
-            for (int i = tid; i < l; i += nt) {
+            for (int i = tid; i < rows_valid; i += nt) {
                 double x = Uw[(int64_t)i * LP + k];
                 for (int j = 0; j < k; ++j) x -= v[j] * Uw[(int64_t)i * LP + j];
                 Uw[(int64_t)i * LP + k] = x;
@@ -575,12 +756,12 @@ __global__ __launch_bounds__(1024) void block_jacobi_complete_kernel(const T* __
         }
         if (tid == 0) {
             double nv = 0.0;
-            for (int i = 0; i < l; ++i) nv += Uw[(int64_t)i * LP + k] * Uw[(int64_t)i * LP + k];
+            for (int i = 0; i < rows_valid; ++i) nv += Uw[(int64_t)i * LP + k] * Uw[(int64_t)i * LP + k];
             v[0] = 1.0 / sqrt(nv);
         }
         __syncthreads();
         const double sc = v[0];
-        for (int i = tid; i < l; i += nt) Uw[(int64_t)i * LP + k] *= sc;
+        for (int i = tid; i < rows_valid; i += nt) Uw[(int64_t)i * LP + k] *= sc;
         __syncthreads();
     }
 }
@@ -588,27 +769,45 @@ __global__ __launch_bounds__(1024) void block_jacobi_complete_kernel(const T* __
 }  // namespace
 
 template <typename T>
-hipError_t launch_block_jacobi(const double* R, int l, int LP, double* X, double* J, double* Uw, double* Vw, T* S,
-                               unsigned* sync, int* info, hipStream_t s, double quad2) {
-    if (LP % 32 || LP < 64 || LP > 512) return hipErrorInvalidValue;
+hipError_t launch_block_jacobi_ex(const double* src, int64_t lds, int src_rowmajor, int mrv, int l, int MR, int LP,
+                                  double* X, double* J, double* Uw, double* Vw, T* S, unsigned* sync, int* info,
+                                  hipStream_t s, double quad2, double tol_chk) {
+    if (LP % 32 || LP < 64 || LP > 4096 || MR % 32 || MR < 32 || l > LP || mrv > MR) return hipErrorInvalidValue;
     hipError_t e = hipMemsetAsync(sync, 0, kSyncWords * sizeof(unsigned), s);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(block_jacobi_kernel, dim3(LP / 32), dim3(kBJThreads), block_jacobi_lds(LP), s, R, l, LP, X, J, Uw,
-                       sync, info, quad2);
+    hipLaunchKernelGGL(block_jacobi_kernel, dim3(LP / 32), dim3(kBJThreads), block_jacobi_lds(MR), s, src, lds,
+                       src_rowmajor, mrv, l, MR, LP, X, J, Uw, sync, info, quad2, tol_chk * tol_chk);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
-    const size_t lds = (size_t)LP * 8 * 2 + (size_t)LP * 4 + 64;
-    hipLaunchKernelGGL((block_jacobi_finish_kernel<T>), dim3(1), dim3(1024), lds, s, X, l, LP, sync, S);
-    hipLaunchKernelGGL((block_jacobi_scatter_kernel<T>), dim3(((LP + 63) / 64) * ((LP + 63) / 64)), dim3(256), 0, s, X, J, l, LP,
-                       sync, Uw, Vw);
-    hipLaunchKernelGGL((block_jacobi_complete_kernel<T>), dim3(1), dim3(1024), (size_t)LP * 8 + 64, s, S, l, LP, Uw);
+    const size_t lds_fin = (size_t)LP * 8 * 2 + (size_t)LP * 4 + 64;
+    hipLaunchKernelGGL((block_jacobi_finish_kernel<T>), dim3(1), dim3(1024), lds_fin, s, X, l, MR, LP, sync, S);
+    const int64_t sx = (int64_t)MR * LP, sj = (int64_t)LP * LP;
+    const int nbk = (LP + 63) / 64;
+    hipLaunchKernelGGL(block_jacobi_scatter_kernel, dim3(nbk * ((LP + 63) / 64)), dim3(256), 0, s, J, sj, X, sx, l, LP,
+                       l, LP, sync, 0, Vw);
+    hipLaunchKernelGGL(block_jacobi_scatter_kernel, dim3(nbk * ((MR + 63) / 64)), dim3(256), 0, s, X, sx, X, sx, mrv, MR,
+                       l, LP, sync, 1, Uw);
+    hipLaunchKernelGGL((block_jacobi_complete_kernel<T>), dim3(1), dim3(1024), (size_t)std::max(mrv, LP) * 8 + 64, s, S, l,
+                       mrv, LP, Uw);
     return hipGetLastError();
 }
 
+template <typename T>
+hipError_t launch_block_jacobi(const double* R, int l, int LP, double* X, double* J, double* Uw, double* Vw, T* S,
+                               unsigned* sync, int* info, hipStream_t s, double quad2, double tol_chk) {
+    if (LP > 512) return hipErrorInvalidValue;
+    return launch_block_jacobi_ex<T>(R, LP, 0, l, l, LP, LP, X, J, Uw, Vw, S, sync, info, s, quad2, tol_chk);
+}
+
 template hipError_t launch_block_jacobi<float>(const double*, int, int, double*, double*, double*, double*, float*,
-                                               unsigned*, int*, hipStream_t, double);
+                                               unsigned*, int*, hipStream_t, double, double);
 template hipError_t launch_block_jacobi<double>(const double*, int, int, double*, double*, double*, double*, double*,
-                                                unsigned*, int*, hipStream_t, double);
+                                                unsigned*, int*, hipStream_t, double, double);
+template hipError_t launch_block_jacobi_ex<float>(const double*, int64_t, int, int, int, int, int, double*, double*,
+                                                  double*, double*, float*, unsigned*, int*, hipStream_t, double, double);
+template hipError_t launch_block_jacobi_ex<double>(const double*, int64_t, int, int, int, int, int, double*, double*,
+                                                   double*, double*, double*, unsigned*, int*, hipStream_t, double,
+                                                   double);
 
 #ifdef RSVD_BJ_PROF
 void bj_prof_dump() {

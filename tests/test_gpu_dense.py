@@ -332,3 +332,68 @@ def test_qr_free_functions_and_svd_class_jacobi(engine):
     s.compute()
     Uo, So, Vo, _ = oracle.jacobi_svd(A)
     assert rel_fro(s.getS(), So) < 1e-12
+
+
+# ---- past the 512-column panels (dense_big.cpp: blocked CGS2 QR, block Jacobi on P directly) ----
+@pytest.mark.parametrize("m,n,full", [(1500, 300, True), (1100, 600, False), (600, 600, False), (530, 700, True)])
+def test_qr_big_matches_givens(engine, m, n, full):
+    """qr_decomposition_full / _reduced (src/QR.cpp:22-80) with more than 512 columns of Q: Q is built
+    in 512-column blocks by block CGS2 + CholeskyQR3.  The unique part (Q[:, :n] and R for full-rank A;
+    all of Q when it is square with m <= n -- the Givens product has det +1) matches the oracle's
+    Givens restatement; a tall full Q's complement is an orthonormal completion with det +1 too."""
+    A = np.asfortranarray(_rng(m * 3 + n).standard_normal((m, n)))
+    Q, R = engine.qr_host(A, full=full)
+    Qo, Ro = (oracle.givens_qr_full if full else oracle.givens_qr_reduced)(A)
+    kq = m if full else n
+    assert Q.shape == (m, kq) and R.shape == (kq, n)
+    assert _orth_err(Q) < 1e-12
+    assert np.all(np.tril(R, -1) == 0)
+    assert rel_fro(Q @ R, A) < 1e-13
+    assert rel_fro(R, Ro) < 1e-11
+    kk = min(m, n)
+    assert rel_fro(Q[:, :kk], Qo[:, :kk]) < 1e-11
+    if kq == m:  # a square Q: the reference's product of rotations has det +1
+        assert np.linalg.slogdet(Q)[0] == 1.0
+        if m <= n:
+            assert rel_fro(Q, Qo) < 1e-11
+
+
+@pytest.mark.parametrize("m,n", [(1200, 900), (900, 1200)])
+def test_svd_jacobi_big_f64(engine, m, n):
+    """SVD<Jacobi> past 512 (SVD_class.hpp:100-180 has no size limit): the block Jacobi runs on P = A
+    or A^T directly (MR = max(m, n) rows read from global memory).  Golden: numpy's LAPACK SVD, the
+    reference's own Python recipe (python/test_run_rSVD.py:47) -- the C oracle's two-sided Jacobi on a
+    900 x 900 triangle takes minutes.  Gapped spectrum 0.99^i: S to 1e-12, vectors to 1e-9."""
+    k = min(m, n)
+    sig = 0.99 ** np.arange(k)
+    A = _spectrum_matrix(m, n, sig, seed=m + 2 * n)
+    U, S, V = engine.svd_host(A, 0)
+    Ul, Sl, Vlt = np.linalg.svd(A, full_matrices=False)
+    assert U.shape == (m, k) and S.shape == (k,) and V.shape == (n, k)
+    assert np.all(np.diff(S) <= 0)
+    assert rel_fro(S, Sl) < 1e-12
+    assert rel_fro(sign_align(U, Ul), Ul) < 1e-9
+    assert rel_fro(sign_align(V, Vlt.T), Vlt.T) < 1e-9
+    assert _orth_err(U) < 1e-12 and _orth_err(V) < 1e-12
+    assert rel_fro((U * S) @ V.T, A) < 1e-12
+
+
+def test_svd_big_parallel_jacobi_and_f32(engine):
+    """ParallelJacobi past 512 returns the converged SVD (its weight-ordered iteration stops at an
+    absolute 1e-12 weight); the fp32 device path widens A once and returns fp32 factors."""
+    import torch
+
+    m, n = 1100, 600
+    A = _spectrum_matrix(m, n, 0.99 ** np.arange(n) + 0.01, seed=21)
+    Ul, Sl, Vlt = np.linalg.svd(A, full_matrices=False)
+    U, S, V = engine.svd_host(A, 2)
+    assert rel_fro(S, Sl) < 1e-12
+    assert rel_fro(sign_align(U, Ul), Ul) < 1e-9
+    U32, S32, V32 = engine.svd(torch.from_numpy(A.astype(np.float32)).cuda(), 0)
+    U32, S32, V32 = (x.cpu().double().numpy() for x in (U32, S32, V32))
+    A32 = A.astype(np.float32).astype(np.float64)
+    Ul, Sl, Vlt = np.linalg.svd(A32, full_matrices=False)
+    assert rel_fro(S32, Sl) < 1e-5
+    h = n // 2
+    assert rel_fro(sign_align(U32[:, :h], Ul[:, :h]), Ul[:, :h]) < 1e-4
+    assert rel_fro(sign_align(V32[:, :h], Vlt.T[:, :h]), Vlt.T[:, :h]) < 1e-4

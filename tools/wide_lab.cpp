@@ -188,56 +188,119 @@ static void bench_chol() {
 #ifdef RSVD_BJ_PROF
 namespace rsvd { void bj_prof_dump(); }
 #endif
-static void bench_jac() {
-    for (int LP : {64, 128, 256, 512}) {
-        // R: upper triangular with a 0.97^i graded diagonal + noise (like a QR-preconditioned B^T)
-        std::vector<double> hR((size_t)LP * LP, 0.0);
-        std::mt19937 g(5);
-        std::normal_distribution<double> d;
-        for (int i = 0; i < LP; ++i)
-            for (int j = i; j < LP; ++j) hR[(size_t)i * LP + j] = (i == j ? 1.0 : 0.05 * d(g)) * pow(0.97, i);
-        double* R;
-        CK(hipMalloc(&R, hR.size() * 8));
-        CK(hipMemcpy(R, hR.data(), hR.size() * 8, hipMemcpyHostToDevice));
-        double *X, *J, *Uw, *Vw, *Sd;
-        unsigned* sync;
-        int* info;
-        CK(hipMalloc(&X, (size_t)2 * LP * LP * 8));
-        CK(hipMalloc(&J, (size_t)2 * LP * LP * 8));
-        CK(hipMalloc(&Uw, (size_t)LP * LP * 8));
-        CK(hipMalloc(&Vw, (size_t)LP * LP * 8));
-        CK(hipMalloc(&Sd, LP * 8));
-        CK(hipMalloc(&sync, 128 * 4));
-        CK(hipMalloc(&info, 16 * 4));
-        CK(hipMemset(info, 0, 64));
-        double t = time_us([&] { CK(launch_block_jacobi<double>(R, LP, LP, X, J, Uw, Vw, Sd, sync, info, S)); }, 3);
-        int hinfo[4];
-        CK(hipMemcpy(hinfo, info, 16, hipMemcpyDeviceToHost));
-        std::vector<double> hS(LP);
-        CK(hipMemcpy(hS.data(), Sd, LP * 8, hipMemcpyDeviceToHost));
-#ifdef RSVD_BJ_PROF
-        rsvd::bj_prof_dump();
-#endif
-        std::vector<double> hU((size_t)LP * LP), hV((size_t)LP * LP);
-        CK(hipMemcpy(hU.data(), Uw, hU.size() * 8, hipMemcpyDeviceToHost));
-        CK(hipMemcpy(hV.data(), Vw, hV.size() * 8, hipMemcpyDeviceToHost));
-        double rec = 0, wn = 0, orth = 0;  // W = R^T = Uw diag(S) Vw^T (row-major [row][col]); Vw^T Vw = I
-        for (int i = 0; i < LP; ++i)
-            for (int j = 0; j < LP; ++j) {
-                double a = 0, o = 0;
-                for (int k = 0; k < LP; ++k) {
-                    a += hU[(size_t)i * LP + k] * hS[k] * hV[(size_t)j * LP + k];
-                    o += hV[(size_t)k * LP + i] * hV[(size_t)k * LP + j];
-                }
-                const double w = hR[(size_t)j * LP + i];
-                rec += (a - w) * (a - w);
-                wn += w * w;
-                orth += (o - (i == j)) * (o - (i == j));
+// Householder-free modified Gram-Schmidt QR of an n x n column-major matrix (host, for inputs)
+static void mgs(std::vector<double>& A, int n, std::vector<double>* Rout) {
+    if (Rout) Rout->assign((size_t)n * n, 0.0);
+    for (int j = 0; j < n; ++j) {
+        for (int pass = 0; pass < 2; ++pass)
+            for (int i = 0; i < j; ++i) {
+                double d = 0;
+                for (int t = 0; t < n; ++t) d += A[(size_t)i * n + t] * A[(size_t)j * n + t];
+                for (int t = 0; t < n; ++t) A[(size_t)j * n + t] -= d * A[(size_t)i * n + t];
+                if (Rout) (*Rout)[(size_t)j * n + i] += d;  // R[i][j] column-major
             }
-        printf("block_jacobi LP=%d: %.1f us  sweeps=%d timeout=%d  S[0]=%.6f S[last]=%.3e  |W-USV'|/|W|=%.2e  |V'V-I|=%.2e\n",
-               LP, t, hinfo[0], hinfo[2], hS[0], hS[LP - 1], sqrt(rec / wn), sqrt(orth));
-        CK(hipFree(R)); CK(hipFree(X)); CK(hipFree(J)); CK(hipFree(Uw)); CK(hipFree(Vw)); CK(hipFree(Sd));
-        CK(hipFree(sync)); CK(hipFree(info));
+        double nn = 0;
+        for (int t = 0; t < n; ++t) nn += A[(size_t)j * n + t] * A[(size_t)j * n + t];
+        nn = sqrt(nn);
+        for (int t = 0; t < n; ++t) A[(size_t)j * n + t] /= nn;
+        if (Rout) (*Rout)[(size_t)j * n + j] = nn;
+    }
+}
+
+// R (upper triangular, stored [c][i] = R(i, c) as the kernel reads it) of W^T where W has the
+// singular values s: W = U diag(s) V^T with random orthogonal U, V, R = qr(W^T).R
+static std::vector<double> make_R(int LP, const std::vector<double>& sv, unsigned seed) {
+    std::mt19937 g(seed);
+    std::normal_distribution<double> d;
+    std::vector<double> U((size_t)LP * LP), V((size_t)LP * LP);
+    for (auto& x : U) x = d(g);
+    for (auto& x : V) x = d(g);
+    mgs(U, LP, nullptr);
+    mgs(V, LP, nullptr);
+    std::vector<double> Wt((size_t)LP * LP, 0.0);  // W^T (column-major): W^T = V diag(s) U^T
+    for (int j = 0; j < LP; ++j)        // column j of W^T = sum_k V[:,k] s_k U[j,k]
+        for (int k = 0; k < LP; ++k) {
+            const double f = sv[k] * U[(size_t)k * LP + j];
+            for (int i = 0; i < LP; ++i) Wt[(size_t)j * LP + i] += V[(size_t)k * LP + i] * f;
+        }
+    std::vector<double> R;
+    mgs(Wt, LP, &R);
+    // kernel layout: hR[c * LP + i] = R(c, i)?  the kernel reads X[c][i] = W[i][c] = R[c][i] with R
+    // row-major [c][i] = R(c, i) (upper: i >= c)
+    std::vector<double> hR((size_t)LP * LP, 0.0);
+    for (int c = 0; c < LP; ++c)
+        for (int i = c; i < LP; ++i) hR[(size_t)c * LP + i] = R[(size_t)i * LP + c];
+    return hR;
+}
+
+static void bench_jac() {
+    for (int LP : {128, 256, 512}) {
+        for (int kind = 0; kind < 2; ++kind) {
+            std::vector<double> hR((size_t)LP * LP, 0.0);
+            if (kind == 0) {
+                // R: upper triangular with a 0.97^i graded diagonal + noise (like a QR-preconditioned B^T)
+                std::mt19937 g(5);
+                std::normal_distribution<double> d;
+                for (int i = 0; i < LP; ++i)
+                    for (int j = i; j < LP; ++j) hR[(size_t)i * LP + j] = (i == j ? 1.0 : 0.05 * d(g)) * pow(0.97, i);
+            } else {
+                // the C4 / C5 small SVD: 90 * 0.9^t down to a noise floor, then a tight cluster (0.146 .. 0.2)
+                std::vector<double> sv(LP);
+                std::mt19937 g(7);
+                std::uniform_real_distribution<double> u(0.146, 0.2);
+                for (int t = 0; t < LP; ++t) sv[t] = std::max(90.0 * pow(0.9, t), u(g));
+                hR = make_R(LP, sv, 11);
+            }
+            double* R;
+            CK(hipMalloc(&R, hR.size() * 8));
+            CK(hipMemcpy(R, hR.data(), hR.size() * 8, hipMemcpyHostToDevice));
+            double *X, *J, *Uw, *Vw, *Sd;
+            unsigned* sync;
+            int* info;
+            CK(hipMalloc(&X, (size_t)2 * LP * LP * 8));
+            CK(hipMalloc(&J, (size_t)2 * LP * LP * 8));
+            CK(hipMalloc(&Uw, (size_t)LP * LP * 8));
+            CK(hipMalloc(&Vw, (size_t)LP * LP * 8));
+            CK(hipMalloc(&Sd, LP * 8));
+            CK(hipMalloc(&sync, kBJSyncWords * 4));
+            CK(hipMalloc(&info, 16 * 4));
+            for (int prec = 0; prec < 2; ++prec) {  // 0: fp64 results, 1: fp32 results
+                CK(hipMemset(info, 0, 64));
+                const double q2 = prec ? 1e-8 : 1e-16, tc = prec ? kBJTolF32 : kBJTolF64;
+                double t = time_us([&] { CK(launch_block_jacobi<double>(R, LP, LP, X, J, Uw, Vw, Sd, sync, info, S, q2, tc)); }, 3);
+                int hinfo[4];
+                CK(hipMemcpy(hinfo, info, 16, hipMemcpyDeviceToHost));
+                std::vector<double> hS(LP);
+                CK(hipMemcpy(hS.data(), Sd, LP * 8, hipMemcpyDeviceToHost));
+#ifdef RSVD_BJ_PROF
+                rsvd::bj_prof_dump();
+#endif
+                std::vector<double> hU((size_t)LP * LP), hV((size_t)LP * LP);
+                CK(hipMemcpy(hU.data(), Uw, hU.size() * 8, hipMemcpyDeviceToHost));
+                CK(hipMemcpy(hV.data(), Vw, hV.size() * 8, hipMemcpyDeviceToHost));
+                double rec = 0, wn = 0, orth = 0, uorth = 0;  // W = R^T = Uw diag(S) Vw^T (row-major [row][col])
+                for (int i = 0; i < LP; ++i)
+                    for (int j = 0; j < LP; ++j) {
+                        double a = 0, o = 0, uo = 0;
+                        for (int k = 0; k < LP; ++k) {
+                            a += hU[(size_t)i * LP + k] * hS[k] * hV[(size_t)j * LP + k];
+                            o += hV[(size_t)k * LP + i] * hV[(size_t)k * LP + j];
+                            uo += hU[(size_t)k * LP + i] * hU[(size_t)k * LP + j];
+                        }
+                        const double w = hR[(size_t)j * LP + i];
+                        rec += (a - w) * (a - w);
+                        wn += w * w;
+                        orth += (o - (i == j)) * (o - (i == j));
+                        uorth += (uo - (i == j)) * (uo - (i == j));
+                    }
+                printf("block_jacobi LP=%d %s %s: %.1f us  sweeps=%d timeout=%d  S[0]=%.6f S[last]=%.3e  |W-USV'|/|W|=%.2e  "
+                       "|V'V-I|=%.2e |U'U-I|=%.2e\n",
+                       LP, kind ? "c4-cluster" : "graded", prec ? "f32-out" : "f64-out", t, hinfo[0], hinfo[2], hS[0],
+                       hS[LP - 1], sqrt(rec / wn), sqrt(orth), sqrt(uorth));
+            }
+            CK(hipFree(R)); CK(hipFree(X)); CK(hipFree(J)); CK(hipFree(Uw)); CK(hipFree(Vw)); CK(hipFree(Sd));
+            CK(hipFree(sync)); CK(hipFree(info));
+        }
     }
 }
 
