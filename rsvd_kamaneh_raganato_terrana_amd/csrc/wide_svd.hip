@@ -4,30 +4,27 @@
 // As in jacobi.hip, W = R^T (R = Q_B^T B^T, so B = W Q_B^T) is diagonalised by one-sided
 // (Hestenes) Jacobi: X = W, J = I, rotate column pairs until the columns of X are orthogonal;
 // then S = column norms (descending, the reference's selection sort :164-178), U_w = X / S,
-// V_w = J.  For l > 64 the l x l problem no longer fits one workgroup: the columns are cut into
-// NB = LP/16 blocks of 16, and a sweep visits every column pair exactly once, in NB outer rounds
-// on a persistent grid of NB/2 workgroups (each owns a block pair per round):
-//   * rounds 0 .. NB-2 ("cross"): the block pairs of a round-robin tournament; inside a pair only
-//     the 16 x 16 CROSS pairs are rotated -- 16 inner rounds of 16 disjoint rotations (column k of
-//     the first block with column (k + s) % 16 of the second);
-//   * round NB-1 ("intra"): each workgroup takes two blocks and rotates the pairs INSIDE each
-//     block (15 inner rounds, round-robin per block).
-// So a sweep is the scalar cyclic Jacobi sweep with l/2 rotations in flight, l - 1 inner rounds
-// deep (the former scheme re-did every intra-block pair in every outer round: 2l inner rounds).
-// Per outer round a workgroup
-//   1. stages its 32 columns of X in LDS and forms Gp = X_pair^T X_pair (fp64 MFMA);
-//   2. runs the inner sweep on Gp: per inner round 16 lanes evaluate the angles, then 136 threads
-//      rotate the upper-triangle 2 x 2 blocks of Gp from both sides in place (Gp is symmetric:
-//      the lower half is never touched), while one wave accumulates the rotations into the 32 x 32
-//      Jp (a row per lane), one round behind, off the path between the two barriers of a round;
-//   3. X_pair <- X_pair Jp, J_pair <- J_pair Jp (fp64 MFMA) into the other half of a double buffer.
+// V_w = J.  For l > 64 the l x l problem no longer fits one workgroup, so the columns are cut
+// into NB = LP/16 blocks of 16 and paired round-robin (NB/2 disjoint block pairs per round,
+// NB - 1 rounds per sweep) over a persistent grid of NB/2 workgroups:
+//   1. Gp = X_pair^T X_pair (32 x 32, fp64 MFMA over the MR rows; exact column dot products, the
+//      same quantities the one-sided rotation angles use);
+//   2. the 32 x 32 symmetric eigenproblem of Gp by one cyclic Jacobi sweep in LDS (16 disjoint
+//      rotations per inner round, accumulated into Jp) -- each inner rotation is the one-sided
+//      rotation of the corresponding column pair of X, with the same angle formula as jacobi.hip;
+//   3. X_pair <- X_pair Jp, J_pair <- J_pair Jp (fp64 MFMA), into the other half of a double
+//      buffer (every column is owned by exactly one pair per round).
+// (Measured and reverted, profiles/r03_bj_cross_deadend.txt: rotating only the 16 x 16 cross pairs
+// per outer round plus one intra-block round per sweep -- half the inner rounds -- needs 1-2 sweeps
+// more on clustered spectra and its inner round was no faster.)
 // Rounds are separated by an agent-scope grid barrier (MI355X_MICROARCH.md "Workgroup dispatch
 // ... inter-workgroup visibility": plain stores -> vmcnt(0) -> barrier -> release fence -> relaxed
 // counter; acquire fence after the poll).  The grid (<= 16 workgroups) is always co-resident;
 // every spin is bounded and reports a timeout instead of hanging.
 // Convergence: a sweep whose rotations all had cos^2 = g^2 / (ab) <= quad2 ends the iteration (the
-// next would only square them); and when a sweep's largest pre-rotation cosine is small enough to
-// have squared below tol_chk, the whole grid checks max cos over ALL column pairs of the new X
+// next would only square them); and when a sweep's largest pre-rotation cosine is <= sqrt(tol_chk)
+// (quadratic convergence: small enough to have squared below tol_chk), the whole grid checks max cos
+// over ALL column pairs of the new X
 // (an LP x LP fp64 MFMA Gram, every workgroup a 32-column slice) and stops at <= tol_chk -- which
 // saves the confirming sweep the first rule needs.
 #include <algorithm>
@@ -101,34 +98,13 @@ __device__ __forceinline__ double rcp_nr(double d) {
     return y * (2.0 - d * y);
 }
 
-// Pair k (0..15) of inner round s on the 32 local columns [block P | block Q], as (p, q) -- the
-// rotation's orientation (x_p' = c x_p - s x_q); the Gram is read through sym(), so p > q is fine:
-//   MODE 0 (cross, 16 rounds): column k of P with column (k + s) % 16 of Q;
-//   MODE 1 (intra, 15 rounds): the circle method inside each block (k < 8: block P, else block Q):
-//     pair 0 = ((s) % 15, 15), pair j = ((s + j) % 15, (s - j) % 15).
-template <int MODE>
-__device__ __forceinline__ void inner_pair(int s, int k, int& p, int& q) {
-    if (MODE == 0) {
-        p = k;
-        q = 16 + ((k + s) & 15);
-    } else {
-        const int base = k < 8 ? 0 : 16, kk = k & 7;
-        p = base + (s + kk) % 15;
-        q = base + (kk == 0 ? 15 : (s - kk + 15) % 15);
-    }
-}
-template <int MODE> constexpr int inner_rounds() { return MODE == 0 ? 16 : 15; }
-
-// (i, j) of the symmetric pair Gram, stored in its upper triangle
-__device__ __forceinline__ int sym(int i, int j) { return i < j ? i * GS + j : j * GS + i; }
-
 // Rotation of the pair (a = |x_p|^2, b = |x_q|^2, g = x_p.x_q): x_p' = c x_p - s x_q, x_q' = s x_p + c x_q
 // zeroes the cross term (jacobi.hip formula: t = sign(d g) |2g| / (|d| + sqrt(d^2 + 4 g^2)), d = b - a,
 // c = (1 + t^2)^-1/2, s = c t), evaluated on operands scaled by max(|d|, |2g|) (no overflow / underflow
 // for any finite a, b, g)
 __device__ __forceinline__ void pair_angle(const double* G, int p, int q, double tol2, double negl, double& c,
                                            double& s, bool& rot) {
-    const double a = G[p * GS + p], b = G[q * GS + q], g = G[sym(p, q)];
+    const double a = G[p * GS + p], b = G[q * GS + q], g = G[p * GS + q];
     rot = g != 0.0 && g * g > tol2 * a * b && a > negl && b > negl;
     const double d = b - a, g2 = 2.0 * g;
     const double inv = rcp_nr(fmax(fmax(fabs(d), fabs(g2)), 1e-300));
@@ -145,88 +121,63 @@ size_t block_jacobi_lds(int MR) { return ((MR <= 512 ? (size_t)32 * (MR + 1) : 0
 
 constexpr int kBJThreads = 512;  // 8 waves: 2 per SIMD for the MFMA phases
 
-template <int MODE>
-__device__ __forceinline__ void jp_round(double* Jrow, const double* A, int s) {
-    // the 16 rotations of inner round s on one row of Jp (columns p, q of pair k; the pairs are
-    // disjoint), four pairs' loads in flight at a time
-#pragma unroll
-    for (int k0 = 0; k0 < 16; k0 += 4) {
-        double x[4], y[4];
-        int p[4], q[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            inner_pair<MODE>(s, k0 + u, p[u], q[u]);
-            x[u] = Jrow[p[u]];
-            y[u] = Jrow[q[u]];
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const double c = A[k0 + u], sn = A[16 + k0 + u];
-            Jrow[p[u]] = c * x[u] - sn * y[u];
-            Jrow[q[u]] = sn * x[u] + c * y[u];
-        }
-    }
-}
-
-// One inner sweep of MODE on the pair Gram G (32 x 32, upper triangle, in place).  Ang: 2 x 32
-// doubles (c[16], s[16] per round, double-buffered).  bk <= bk2: this thread's 2 x 2 block (tid <
-// 136).  The Jp wave (tid 256..287, row jr = tid - 256 of Jp in LDS) applies round s - 1's
-// rotations to its row while round s's angles are evaluated (one round behind: off the critical
-// path of the two barriers per round).
-template <int MODE>
-__device__ __forceinline__ void inner_sweep(double* G, double* Jp, double* Ang, int tid, int bk, int bk2,
-                                            double tol2, double negl) {
-    constexpr int NR = inner_rounds<MODE>();
-    const bool jwave = tid >= 256 && tid < 288;
-    double* Jrow = Jp + (tid - 256) * GS;
-    if (jwave) {
-#pragma unroll
-        for (int j = 0; j < 32; ++j) Jrow[j] = (j == tid - 256) ? 1.0 : 0.0;
-    }
-    for (int s = 0; s < NR; ++s) {
-        double* A = Ang + 32 * (s & 1);
+// One cyclic sweep of the 32 x 32 pair Gram (round-robin: 16 disjoint rotations per inner round,
+// 31 rounds), two phases per inner round: (a) lanes 0..15 compute the angles of the 16 pairs into
+// LDS; (b) thread (k, k2) < 256 rotates the 2 x 2 block (pair k rows, pair k2 columns) from both
+// sides into the other G buffer, while threads 256.. rotate the columns of Jp (Jp <- Jp J).
+// Returns the buffer holding the final Gram.
+__device__ __forceinline__ double* inner_sweep(double* Ga, double* Gb, double* Jp, double* Ang, int* Rot, int tid,
+                                               double tol2, double negl) {
+    for (int e = tid; e < 32 * 32; e += kBJThreads) Jp[(e / 32) * GS + e % 32] = (e / 32 == e % 32) ? 1.0 : 0.0;
+    __syncthreads();
+    const int k = (tid >> 4) & 15, k2 = tid & 15;
+    double* cur = Ga;
+    double* nxt = Gb;
+    for (int ir = 0; ir < 31; ++ir) {
         if (tid < 16) {
             int p, q;
-            inner_pair<MODE>(s, tid, p, q);
+            rr_pair(ir, tid, 32, p, q);
             double c, sn;
             bool rt;
-            pair_angle(G, p, q, tol2, negl, c, sn, rt);
-            A[tid] = c;
-            A[16 + tid] = sn;
-        } else if (jwave && s > 0) {
-            jp_round<MODE>(Jrow, Ang + 32 * ((s - 1) & 1), s - 1);
+            pair_angle(cur, p, q, tol2, negl, c, sn, rt);
+            Ang[tid] = c;
+            Ang[16 + tid] = sn;
+            Rot[tid] = rt;
         }
         __syncthreads();
-        if (tid < 136) {
-            int p1, q1, p2, q2;
-            inner_pair<MODE>(s, bk, p1, q1);
-            inner_pair<MODE>(s, bk2, p2, q2);
-            const double c1 = A[bk], s1 = A[16 + bk];
-            if (bk == bk2) {
-                const int ig = sym(p1, q1);
-                const double a = G[p1 * GS + p1], g = G[ig], b = G[q1 * GS + q1];
-                const double l00 = c1 * a - s1 * g, l01 = c1 * g - s1 * b;
-                const double l10 = s1 * a + c1 * g, l11 = s1 * g + c1 * b;
-                G[p1 * GS + p1] = c1 * l00 - s1 * l01;
-                G[ig] = s1 * l00 + c1 * l01;
-                G[q1 * GS + q1] = s1 * l10 + c1 * l11;
-            } else {
-                const double c2 = A[bk2], s2 = A[16 + bk2];
-                const int i00 = sym(p1, p2), i01 = sym(p1, q2), i10 = sym(q1, p2), i11 = sym(q1, q2);
-                const double b00 = G[i00], b01 = G[i01], b10 = G[i10], b11 = G[i11];
-                // left: rows (p, q) <- (c1 row_p - s1 row_q, s1 row_p + c1 row_q)
-                const double l00 = c1 * b00 - s1 * b10, l01 = c1 * b01 - s1 * b11;
-                const double l10 = s1 * b00 + c1 * b10, l11 = s1 * b01 + c1 * b11;
-                // right: cols (p2, q2) <- (c2 col_p2 - s2 col_q2, s2 col_p2 + c2 col_q2)
-                G[i00] = c2 * l00 - s2 * l01;
-                G[i01] = s2 * l00 + c2 * l01;
-                G[i10] = c2 * l10 - s2 * l11;
-                G[i11] = s2 * l10 + c2 * l11;
+        int p2, q2;
+        rr_pair(ir, k2, 32, p2, q2);
+        const double c2 = Ang[k2], s2 = Ang[16 + k2];
+        if (tid < 256) {
+            int p, q;
+            rr_pair(ir, k, 32, p, q);
+            const double c1 = Ang[k], s1 = Ang[16 + k];
+            const double b00 = cur[p * GS + p2], b01 = cur[p * GS + q2];
+            const double b10 = cur[q * GS + p2], b11 = cur[q * GS + q2];
+            // left: rows (p, q) <- (c1 row_p - s1 row_q, s1 row_p + c1 row_q)
+            const double l00 = c1 * b00 - s1 * b10, l01 = c1 * b01 - s1 * b11;
+            const double l10 = s1 * b00 + c1 * b10, l11 = s1 * b01 + c1 * b11;
+            // right: cols (p2, q2) <- (c2 col_p2 - s2 col_q2, s2 col_p2 + c2 col_q2)
+            nxt[p * GS + p2] = c2 * l00 - s2 * l01;
+            nxt[p * GS + q2] = s2 * l00 + c2 * l01;
+            nxt[q * GS + p2] = c2 * l10 - s2 * l11;
+            nxt[q * GS + q2] = s2 * l10 + c2 * l11;
+        } else if (Rot[k2]) {
+            // Jp columns (p2, q2) of pair k2, rows k and k + 16 (disjoint per thread)
+#pragma unroll
+            for (int rr = 0; rr < 2; ++rr) {
+                const int row = k + 16 * rr;
+                const double jp = Jp[row * GS + p2], jq = Jp[row * GS + q2];
+                Jp[row * GS + p2] = c2 * jp - s2 * jq;
+                Jp[row * GS + q2] = s2 * jp + c2 * jq;
             }
         }
         __syncthreads();
+        double* t = cur;
+        cur = nxt;
+        nxt = t;
     }
-    if (jwave) jp_round<MODE>(Jrow, Ang + 32 * ((NR - 1) & 1), NR - 1);
+    return cur;
 }
 
 // Stage the 32 columns col(0..31) of a column-major LP x LP matrix into LDS rows of pitch LP + 1.
@@ -408,7 +359,8 @@ __global__ __launch_bounds__(kBJThreads) void block_jacobi_kernel(const double* 
     double* Jp = Gb + 32 * GS;                         // [32][GS] accumulated inner rotation
     __shared__ int flags[8];
     __shared__ double fro;
-    __shared__ double Ang[64];  // c, s of the 16 pairs of an inner round, double-buffered
+    __shared__ double Ang[32];  // c, s of the 16 pairs of an inner round
+    __shared__ int Rot[16];
     __shared__ unsigned long long lmax;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int r = lane & 15, h = lane >> 4;
@@ -418,17 +370,6 @@ __global__ __launch_bounds__(kBJThreads) void block_jacobi_kernel(const double* 
     const double tol = (double)l * kEps, tol2 = tol * tol;
     unsigned long long* smax = reinterpret_cast<unsigned long long*>(sync + 80);
     unsigned long long* cmax = reinterpret_cast<unsigned long long*>(sync + 144);
-    // this thread's upper-triangle 2 x 2 block (bk <= bk2) of the inner update, tid < 136
-    int bk = 0, bk2 = 0;
-    {
-        int t = tid < 136 ? tid : 0, k = 0;
-        while (t >= 16 - k) {
-            t -= 16 - k;
-            ++k;
-        }
-        bk = k;
-        bk2 = k + t;
-    }
 #ifdef RSVD_BJ_PROF
     long long bj_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     long long bj_last = wall_clock64();
@@ -466,15 +407,9 @@ __global__ __launch_bounds__(kBJThreads) void block_jacobi_kernel(const double* 
     BJ_T(0);
     int par = 0, sweeps = 0;
     for (int sweep = 0; sweep < kMaxSweeps; ++sweep) {
-        for (int round = 0; round < NB; ++round) {
-            const bool intra = round == NB - 1;
+        for (int round = 0; round < NB - 1; ++round) {
             int P, Q;
-            if (intra) {
-                P = 2 * wg;
-                Q = 2 * wg + 1;
-            } else {
-                rr_pair(round, wg, NB, P, Q);
-            }
+            rr_pair(round, wg, NB, P, Q);
             const double* Xsrc = Xb + (size_t)par * L2X;
             const double* Jsrc = Jb + (size_t)par * L2;
             double* Xd = Xb + (size_t)(1 - par) * L2X;
@@ -512,21 +447,25 @@ __global__ __launch_bounds__(kBJThreads) void block_jacobi_kernel(const double* 
             }
             __syncthreads();
             BJ_T(2);
-            // 3. convergence test on the fresh Gram, over the pairs this round rotates
-            for (int e = tid; e < 32 * 32; e += kBJThreads) {
-                const int i = e / 32, j = e % 32;
-                const bool mine = intra ? (i < j && (i < 16) == (j < 16)) : (i < 16 && j >= 16);
-                if (mine) {
-                    const double a = Ga[i * GS + i], b = Ga[j * GS + j], g = Ga[i * GS + j];
-                    if (a > negl && b > negl) {
-                        const double c2 = (g * g) / (a * b);
-                        atomicMax(&lmax, (unsigned long long)__double_as_longlong(c2));
-                        if (g != 0.0 && g * g > tol2 * a * b) {
-                            flags[0] = 1;
-                            if (g * g > quad2 * a * b) flags[1] = 1;
+            // 3. convergence test on the fresh Gram (and this round's largest cos^2, one LDS atomic per wave)
+            {
+                double cm = 0.0;
+                for (int e = tid; e < 32 * 32; e += kBJThreads) {
+                    const int i = e / 32, j = e % 32;
+                    if (i < j) {
+                        const double a = Ga[i * GS + i], b = Ga[j * GS + j], g = Ga[i * GS + j];
+                        if (a > negl && b > negl) {
+                            cm = fmax(cm, (g * g) / (a * b));
+                            if (g != 0.0 && g * g > tol2 * a * b) {
+                                flags[0] = 1;
+                                if (g * g > quad2 * a * b) flags[1] = 1;
+                            }
                         }
                     }
                 }
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) cm = fmax(cm, __shfl_xor(cm, o, 64));
+                if (lane == 0 && cm > 0.0) atomicMax(&lmax, (unsigned long long)__double_as_longlong(cm));
             }
             __syncthreads();
             if (tid == 0 && lmax) atomicMax(smax + sweep, lmax);
@@ -536,11 +475,7 @@ __global__ __launch_bounds__(kBJThreads) void block_jacobi_kernel(const double* 
                     if (flags[1]) __hip_atomic_store(sync + 36 + sweep, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
                 // 4. the inner sweep on Gp (in place; Jp from the register wave)
-                if (intra)
-                    inner_sweep<1>(Ga, Jp, Ang, tid, bk, bk2, tol2, negl);
-                else
-                    inner_sweep<0>(Ga, Jp, Ang, tid, bk, bk2, tol2, negl);
-                __syncthreads();
+                inner_sweep(Ga, Gb, Jp, Ang, Rot, tid, tol2, negl);
                 BJ_T(3);
                 // 5. X_pair Jp and J_pair Jp -> destination buffer
                 if (staged)
@@ -576,7 +511,7 @@ __global__ __launch_bounds__(kBJThreads) void block_jacobi_kernel(const double* 
         if (rot == 0 || big == 0) break;
         // the global check, once the sweep's rotations were small enough to have squared below tol_chk2
         const double pre = u64_as_double(__hip_atomic_load(smax + sweep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-        if (tol_chk2 > 0.0 && pre <= 1e3 * tol_chk2) {
+        if (tol_chk2 > 0.0 && pre <= sqrt(tol_chk2)) {  // pre-rotation cos <= sqrt(tol): squared below ~tol
             const double mx = slice_max_cos2(Xb + (size_t)par * L2X, MR, LP, wg, w, lane, negl);
             if (tid == 0) lmax = 0ull;
             __syncthreads();
