@@ -8,7 +8,7 @@
 // Givens sign convention: R(j,j) >= 0 except where the reference's sweep never rotates (leading
 // columns whose sub-diagonal is already zero keep the sign of A(j,j); a square Q has det +1).  The
 // reduced form requires rows >= cols (std::invalid_argument otherwise, where the reference's Eigen
-// block would assert).  Built for n <= 512 (reduced) and m, n <= 512 (full).
+// block would assert).  Any size (past 512 columns: blocked CGS2 + CholeskyQR3, dense_big.cpp).
 // The reference header also declares `Mat_m givens_rotation(double, double)` without defining it
 // (QR.hpp:14 vs src/QR.cpp:12); the defined overload is provided here.
 #ifndef QR_HPP

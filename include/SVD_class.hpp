@@ -4,11 +4,11 @@
 // engine (rsvd_svd, dense_api.cpp) through include/rsvd.hpp.
 //
 //   Jacobi / ParallelJacobi (SVD_class.hpp:100-180, :223-333): U m x k, S k (descending), V n x k,
-//     k = min(m, n) <= 512.  Both reference methods converge to the same SVD (up to signs of
+//     k = min(m, n) <= 4096.  Both reference methods converge to the same SVD (up to signs of
 //     singular-vector pairs); the GPU runs one-sided Jacobi on the QR-preconditioned triangle.
 //   Power (SVD_class.hpp:183-219, src/PM.cpp): the reference's layouts -- U m x m and V n x n
 //     identity-initialised with u_i in column i of U and v_i in ROW i of V, S of length min(m, n),
-//     cut to the first i columns on an early stop (sigma < 1e-12).  n <= 512.  Start vectors come
+//     cut to the first i columns on an early stop (sigma < 1e-12).  Any n.  Start vectors come
 //     from the Philox stream (RSVD_SEED) instead of std::random_device.
 // compute() prints nothing (the reference writes progress lines to stdout, :80-95).
 #ifndef SVD_CLASS_HPP

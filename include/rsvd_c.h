@@ -219,14 +219,16 @@ int rsvd_generate_omega(rsvd_handle_t h, int64_t n, int32_t l, uint64_t seed, in
  * and A = Q R; R(j,j) >= 0 except on the leading columns of A whose sub-diagonal is already zero,
  * where R(j,j) = A(j,j) as the Givens sweep leaves them.  For full-rank A this is the unique QR,
  * i.e. the reference's; the complement Q[:, n:] of a full QR is an orthonormal completion
- * (identity columns for an A with trailing zero rows).  Built for n <= 512 (reduced) and
- * m, n <= 512 (full); larger sizes return RSVD_ERR_UNSUPPORTED. */
+ * (identity columns for an A with trailing zero rows).  Up to 512 columns (of A, or of Q for the
+ * full form) one shifted-CholeskyQR3 pass; past that, 512-column blocks by block CGS2 + CholeskyQR3
+ * (dense_big.cpp), bounded only by device memory. */
 int rsvd_qr(rsvd_handle_t h, int64_t m, int64_t n, const void *A, int64_t lda, int32_t dtype, int32_t full, void *Q,
             int64_t ldq, void *R, int64_t ldr);
 
 /* SVD<method>::compute() boundary (include/SVD_class.hpp:35-97).  Jacobi / ParallelJacobi
  * (:100-180, :223-333): U m x k (ldu), S k (descending, >= 0), V n x k (ldv), k = min(m, n)
- * <= 512; dtype F64 / F32.  Power (:183-219 with PM, src/PM.cpp): dtype F64, n <= 512,
+ * <= 4096 (past 512: block Jacobi directly on the columns of A or A^T, RSVD_ERR_UNSUPPORTED
+ * above 4096); dtype F64 / F32.  Power (:183-219 with PM, src/PM.cpp): dtype F64, any n,
  * dim = r ? r : min(m, n) deflation steps, start vectors Philox(seed + i); stops at the first
  * sigma < 1e-12 (:198-208); *kept = triplets written (U, S, V columns 0..kept-1; V's columns are
  * the right singular vectors -- the reference's row layout is rebuilt by include/SVD_class.hpp).

@@ -80,7 +80,7 @@ struct WideLayout {
             // where the clamped read lands on zero S rows / unstored output rows)
             const bool v2 = a_aligned && ((d->dtype == RSVD_BF16 && d->lda % 8 == 0 && m % 8 == 0 && m >= 8) ||
                                           (d->dtype == RSVD_FP8_E4M3 && d->lda % 16 == 0 && m % 16 == 0 && m >= 16));
-            wnn = plan_wproj(m, n, LP, v2);
+            wnn = plan_wproj(m, n, LP, v2, true, d->dtype == RSVD_FP8_E4M3);
             wtn = plan_wproj(n, m, LP, v2, false, d->dtype == RSVD_FP8_E4M3);
             pslab = std::max<int64_t>(wnn.splits > 1 ? wnn.splits * m : 0, wtn.splits > 1 ? wtn.splits * n : 0);
         } else {

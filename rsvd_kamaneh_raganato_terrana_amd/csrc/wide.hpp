@@ -33,6 +33,7 @@ struct WProjPlan {
     bool v3 = false; // v2 with launch-constant LDS read bases (bf16 A, LP 256 / 512; wide_proj.hip)
     int sd = 1;       // v3: S-panel prefetch distance in k-steps (1 or 2; A runs as far ahead as LDS allows)
     bool tn2 = false; // v3 TN at LP = 256 with two k-steps per A slot (128-B A lines)
+    bool half = false; // e4m3 A at LP = 512: two LP = 256 column-half launches (256-row tiles)
     int abl = 0;      // lab-only ablations of the v3 kernel (tools/wide_lab.cpp), never set by the engine
     int kn = -1;      // lab-only knob override of the LP = 256 v3 kernels (-1: the engine's choice)
 };

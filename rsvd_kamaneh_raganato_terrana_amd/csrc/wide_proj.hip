@@ -382,7 +382,8 @@ template <bool FP8, bool NN, int LP, bool SPLIT, bool DS = false, int KN = 0, bo
 __global__ __launch_bounds__(512) void wproj2_kernel(const void* __restrict__ Av, int64_t lda, int64_t rows_out,
                                                      int64_t K, int64_t arows, const bf16_t* __restrict__ Shi,
                                                      const bf16_t* __restrict__ Slo, float* __restrict__ out,
-                                                     int64_t slab_stride, int64_t kchunk, int nrowblk) {
+                                                     int64_t slab_stride, int64_t kchunk, int nrowblk, int s_pitch,
+                                                     int o_pitch) {
     typedef W2Shape<LP, SPLIT, FP8, DS, S8> SH;
     static_assert(!DS || (!NN && !FP8), "double-step stages: bf16 TN only");
     static_assert(!S8 || (FP8 && NN && !SPLIT && LP >= 256), "e4m3 S: single-pass e4m3 NN at LP >= 256");
@@ -413,7 +414,7 @@ __global__ __launch_bounds__(512) void wproj2_kernel(const void* __restrict__ Av
                 const int u = gi * 64 + lane;
                 constexpr int CPR = LP / 16;
                 const int k = u / CPR, cp = u % CPR;
-                glds16(S + (k0 + k) * LP + 16 * (cp ^ swz8<LP>(k)), slot + gi * 1024);
+                glds16(S + (k0 + k) * s_pitch + 16 * (cp ^ swz8<LP>(k)), slot + gi * 1024);
             }
         } else {
 #pragma unroll
@@ -424,7 +425,7 @@ __global__ __launch_bounds__(512) void wproj2_kernel(const void* __restrict__ Av
                 const int gi = t * 8 + w;             // wave instruction index within the tile
                 const int u = gi * 64 + lane;         // 16-B chunk of the LDS image
                 const int row = u / (LP / 8), cc = u % (LP / 8);
-                glds16(S + (k0 + row) * LP + 8 * (cc ^ swz(row)), slot + a * SH::SBYTES + gi * 1024);
+                glds16(S + (k0 + row) * s_pitch + 8 * (cc ^ swz(row)), slot + a * SH::SBYTES + gi * 1024);
             }
         }
         }
@@ -614,7 +615,7 @@ __global__ __launch_bounds__(512) void wproj2_kernel(const void* __restrict__ Av
             const int64_t row = row0 + wr * 64 + 16 * t + 4 * h + j;
             if (row < rows_out) {
 #pragma unroll
-                for (int g = 0; g < G; ++g) dst[row * LP + wc * G * 16 + 16 * g + r] = acc[t][g][j];
+                for (int g = 0; g < G; ++g) dst[row * o_pitch + wc * G * 16 + 16 * g + r] = acc[t][g][j];
             }
         }
 }
@@ -1223,9 +1224,39 @@ hipError_t wproj2_go(const void* A, int64_t lda, int64_t m, int64_t n, const bf1
     // (profiles/r02_wide_lab_knobs.txt).
     constexpr int KN = NN ? 3 : 0;
     hipLaunchKernelGGL((wproj2_kernel<FP8, NN, LP, SPLIT, DS, KN, S8>), dim3(p.blocks * p.splits), dim3(512), SH::LDS, s,
-                       A, lda, rows_out, K, m, Shi, Slo, o, stride, p.chunk, p.blocks);
+                       A, lda, rows_out, K, m, Shi, Slo, o, stride, p.chunk, p.blocks, LP, LP);
     hipError_t e = hipGetLastError();
     if (e == hipSuccess && done) e = hipEventRecord(done, s);
+    if (e != hipSuccess || p.splits == 1) return e;
+    return launch_sum_slabs<float>(slabs, stride, p.splits, stride, Out, s);
+}
+
+// LP = 512 as two LP = 256 column halves (WProjPlan::half).  At LP = 512 the v2 tile is 128 output
+// rows x 512 columns, so every workgroup re-reads 16x (NN) / 16x (TN) more S bytes from L2 than A
+// bytes (C5 TN: 16 GB of S per launch against 1.07 GB of A, and the L2 pressure evicted A's line
+// halves before the next k-step used them: 4x A traffic from HBM).  Each half runs the LP = 256
+// tile (256 rows x 256 columns: S 2x A per k-step) on its 256 columns of S (pitch 512) into its
+// 256 columns of the output / slabs (pitch 512).  Same per-element arithmetic: bit-identical.
+template <bool FP8, bool NN, bool SPLIT, bool S8 = false>
+hipError_t wproj2_half_go(const void* A, int64_t lda, int64_t m, int64_t n, const bf16_t* Shi, const bf16_t* Slo,
+                          const WProjPlan& p, float* slabs, float* Out, hipStream_t s, hipEvent_t done) {
+    typedef W2Shape<256, SPLIT, FP8, false, S8> SH;
+    const int64_t rows_out = NN ? m : n, K = NN ? n : m;
+    float* o = p.splits == 1 ? Out : slabs;
+    const int64_t stride = rows_out * 512;
+    constexpr int KN = NN ? 3 : 0;
+    for (int hf = 0; hf < 2; ++hf) {
+        // S column offset: 256 bf16 elements, or 256 bytes of an e4m3 panel (S8)
+        const bf16_t* sh = S8 ? reinterpret_cast<const bf16_t*>(reinterpret_cast<const uint8_t*>(Shi) + 256 * hf)
+                              : Shi + 256 * hf;
+        const bf16_t* sl = Slo ? Slo + 256 * hf : nullptr;
+        hipLaunchKernelGGL((wproj2_kernel<FP8, NN, 256, SPLIT, false, KN, S8>), dim3(p.blocks * p.splits), dim3(512),
+                           SH::LDS, s, A, lda, rows_out, K, m, sh, sl, o + 256 * hf, stride, p.chunk, p.blocks, 512, 512);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    hipError_t e = hipSuccess;
+    if (done) e = hipEventRecord(done, s);
     if (e != hipSuccess || p.splits == 1) return e;
     return launch_sum_slabs<float>(slabs, stride, p.splits, stride, Out, s);
 }
@@ -1284,6 +1315,14 @@ hipError_t wproj_lp(int nn, int fp8, const void* A, int64_t lda, int64_t m, int6
 #undef GO3
         }
     }
+    if constexpr (LP == 512) {
+        if (p.v2 && p.half && fp8) {
+            if (nn) return split ? wproj2_half_go<true, true, true>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d)
+                                 : wproj2_half_go<true, true, false>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d);
+            return split ? wproj2_half_go<true, false, true>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d)
+                         : wproj2_half_go<true, false, false>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d);
+        }
+    }
     if constexpr (LP >= 128) {
         if (p.v2) {
 #define GO2(F)                                                                                   \
@@ -1324,7 +1363,9 @@ WProjPlan plan_wproj(int64_t rows_out, int64_t K, int LP, bool v2, bool nn, bool
     p.v3 = p.v2 && !fp8 && (LP == 256 || LP == 512);
     p.tn2 = p.v3 && !nn && LP == 256;  // two k-steps per A slot: K chunks of whole 64-row pairs
     p.ds = p.v2 && LP == 128 && !nn && !fp8 && K % 64 == 0;  // double-step TN stages (whole 64-row K chunks)
-    const int WI = p.v2 ? (LP == 128 ? (p.ds ? 256 : 512) : (LP == 256 ? 256 : 128)) : wproj_rows_per_block(LP);
+    p.half = p.v2 && fp8 && LP == 512;  // two LP = 256 column halves (wproj2_half_go)
+    const int WI = p.v2 ? (LP == 128 ? (p.ds ? 256 : 512) : ((LP == 256 || p.half) ? 256 : 128))
+                        : wproj_rows_per_block(LP);
     p.blocks = (int)((rows_out + WI - 1) / WI);
     const int target = (p.v2 || LP >= 512) ? 256 : 512;  // one workgroup per CU (LDS ring / registers)
     int64_t splits = (target + p.blocks - 1) / p.blocks;
@@ -1347,6 +1388,7 @@ hipError_t launch_wproj_s8(const void* A, int64_t lda, int64_t m, int64_t n, con
     if (!wproj_s8_supported(p, LP)) return hipErrorInvalidValue;
     const bf16_t* S = reinterpret_cast<const bf16_t*>(S8);
     if (LP == 256) return wproj2_go<true, true, 256, false, false, true>(A, lda, m, n, S, nullptr, p, slabs, Out, s, done);
+    if (p.half) return wproj2_half_go<true, true, false, true>(A, lda, m, n, S, nullptr, p, slabs, Out, s, done);
     return wproj2_go<true, true, 512, false, false, true>(A, lda, m, n, S, nullptr, p, slabs, Out, s, done);
 }
 

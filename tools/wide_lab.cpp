@@ -334,7 +334,7 @@ static void bench_proj(bool c4only = false) {
         float* Out;
         CK(hipMalloc(&Out, (size_t)mx * c.LP * 4));
         for (int v2 = c4only ? 1 : 0; v2 < 4; ++v2) {
-            WProjPlan pnn = plan_wproj(c.m, c.n, c.LP, v2 > 0), ptn = plan_wproj(c.n, c.m, c.LP, v2 > 0, false, c.fp8);
+            WProjPlan pnn = plan_wproj(c.m, c.n, c.LP, v2 > 0, true, c.fp8), ptn = plan_wproj(c.n, c.m, c.LP, v2 > 0, false, c.fp8);
             if (v2 == 1) pnn.v3 = ptn.v3 = false;
             if (v2 >= 2 && !pnn.v3 && !ptn.v3) continue;
             if (v2 == 3) ptn.tn2 = false;  // v3 TN with single-step A slots
