@@ -119,19 +119,22 @@ hipError_t launch_omega_lowp_from(const float* om, int64_t ld, int64_t n, int l,
 // only square them): 1e-16 for fp64 results, 1e-8 for results delivered in fp32 (as jacobi.hip's fp32 path).
 // tol_chk: after a sweep whose rotations were small enough, the largest cosine over ALL column pairs
 // is measured and the iteration ends when it is <= tol_chk (0 disables the check).
-constexpr int kBJSyncWords = 256;
+constexpr int kBJSyncWords = 512;
 constexpr double kBJTolF64 = 1e-12, kBJTolF32 = 1e-6;
 template <typename T>
 hipError_t launch_block_jacobi(const double* R, int l, int LP, double* X, double* J, double* Uw, double* Vw, T* S,
                                unsigned* sync, int* info, hipStream_t s, double quad2 = 1e-16,
-                               double tol_chk = kBJTolF64);
+                               double tol_chk = kBJTolF64, int G = 0);
 // The general form: X = the mrv x l source (column-major with ld lds, or row-major: X = src^T when
 // src_rowmajor), zero-padded to MR x LP (multiples of 32, LP <= 4096); X: 2 MR LP, J: 2 LP^2 doubles;
-// U_w: MR x LP, V_w: LP x LP (row-major).  MR > 512 reads the pair columns from global memory.
+// U_w: MR x LP, V_w: LP x LP (row-major).  G: workgroups per block pair (row groups; 0 = the largest
+// of 4, 2, 1 that block_jacobi_groups accepts).  MR / G > 512 reads the pair columns from global memory.
 template <typename T>
 hipError_t launch_block_jacobi_ex(const double* src, int64_t lds, int src_rowmajor, int mrv, int l, int MR, int LP,
                                   double* X, double* J, double* Uw, double* Vw, T* S, unsigned* sync, int* info,
-                                  hipStream_t s, double quad2 = 1e-16, double tol_chk = kBJTolF64);
+                                  hipStream_t s, double quad2 = 1e-16, double tol_chk = kBJTolF64, int G = 0);
+// The row-group count launch_block_jacobi_ex uses for G (0: auto), or 0 when G does not fit.
+int block_jacobi_groups(int MR, int LP, int G);
 
 // ---- wide.cpp: the host pipeline ------------------------------------------------------------------
 // True when `d` runs on the wide engine (bf16 / fp8 A, or l > 64).

@@ -16,7 +16,16 @@
 //      buffer (every column is owned by exactly one pair per round).
 // (Measured and reverted, profiles/r03_bj_cross_deadend.txt: rotating only the 16 x 16 cross pairs
 // per outer round plus one intra-block round per sweep -- half the inner rounds -- needs 1-2 sweeps
-// more on clustered spectra and its inner round was no faster.)
+// more on clustered spectra and its inner round was no faster.  Also reverted, profiles/r03_bj_rowgroups.txt:
+// one barrier per inner round with wave 7 deriving the next round's angles from the current Gram
+// while the others rotate -- the look-ahead's 12 extra LDS reads and three 2 x 2 products made it
+// the longer path, 0.93 vs 0.67 us per inner round.)
+// Row groups: each block pair is served by G workgroups (G = 1, 2, 4), member g owning rows
+// [g MR / G, (g + 1) MR / G) of X and [g LP / G, (g + 1) LP / G) of J.  The members publish their
+// partial pair Grams, meet at a group barrier, sum the G partials in a fixed order and then run the
+// SAME inner sweep on the same Gram (bit-identical Jp, no broadcast), each applying it to its own
+// rows.  The staging, Gram and rotation traffic per workgroup shrink by G; the inner sweep is
+// replicated.
 // Rounds are separated by an agent-scope grid barrier (MI355X_MICROARCH.md "Workgroup dispatch
 // ... inter-workgroup visibility": plain stores -> vmcnt(0) -> barrier -> release fence -> relaxed
 // counter; acquire fence after the poll).  The grid (<= 16 workgroups) is always co-resident;
@@ -42,8 +51,11 @@ constexpr double kEps = 2.220446049250313e-16;
 constexpr int kMaxSweeps = 30;
 // sync layout (unsigned words): [0] barrier counter, [1] abort, [2] final parity, [4 + s] sweep s
 // rotated, [36 + s] sweep s had rotations outside the quadratic regime; u64 slots (8-B aligned):
-// [80 + 2 s] sweep s's largest pre-rotation cos^2, [144 + 2 s] the global check's max cos^2 after it
-constexpr int kSyncWords = 208;
+// [80 + 2 s] sweep s's largest pre-rotation cos^2, [144 + 2 s] the global check's max cos^2 after it,
+// [kGroupWord + pair] the row-group barrier counters (one per block pair, up to 128 pairs)
+constexpr int kGroupWord = 256;
+constexpr int kSyncWords = 384;
+static_assert(kSyncWords <= kBJSyncWords, "block Jacobi sync words");
 
 __device__ __forceinline__ void rr_pair(int round, int k, int N, int& p, int& q) {
     if (k == 0) {
@@ -55,18 +67,20 @@ __device__ __forceinline__ void rr_pair(int round, int k, int N, int& p, int& q)
     }
 }
 
-// Returns false on timeout (then every workgroup bails out through the abort word).
-__device__ bool grid_barrier(unsigned* sync, unsigned target) {
+// Returns false on timeout (then every workgroup bails out through the abort word sync[1]).
+// ctr: the arrival counter (sync[0] for the grid, a group word for a row group).
+__device__ bool grid_barrier(unsigned* sync, unsigned target, unsigned* ctr = nullptr) {
+    if (!ctr) ctr = sync;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     __shared__ int ok;
     if (threadIdx.x == 0) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_fetch_add(sync, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         int good = 1;
         long spins = 0;
-        while (__hip_atomic_load(sync, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+        while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
             __builtin_amdgcn_s_sleep(2);
             if ((++spins & 1023) == 0 &&
                 (__hip_atomic_load(sync + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0 || spins > (1l << 26))) {
@@ -83,7 +97,45 @@ __device__ bool grid_barrier(unsigned* sync, unsigned target) {
     return ok != 0;
 }
 
+// The row-group hand-off of the partial pair Grams, fence-free (MI355X_MICROARCH.md, "Hand-offs
+// measured with sc1 loads", first row): every byte stored `sc1` (st_wt) and loaded `sc1`
+// (ld_wt), every storing wave's vmcnt(0) before the workgroup barrier, one lane's agent-scope add
+// to the group counter, an `sc1` poll, then a workgroup barrier before any load.  No release /
+// acquire fence: each costs ~1.7 us, and the group meets once per round.
+__device__ bool group_barrier(unsigned* sync, unsigned* ctr, unsigned target) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    __shared__ int ok;
+    if (threadIdx.x == 0) {
+        __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        int good = 1;
+        long spins = 0;
+        while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+            __builtin_amdgcn_s_sleep(1);
+            if ((++spins & 1023) == 0 &&
+                (__hip_atomic_load(sync + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0 || spins > (1l << 26))) {
+                __hip_atomic_store(sync + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                good = 0;
+                break;
+            }
+        }
+        ok = good;
+    }
+    __syncthreads();
+    return ok != 0;
+}
+
 constexpr int GS = 33;  // LDS pitch of the 32 x 32 blocks
+
+// Stores of the round's X / J columns and partial Grams: `sc1` (write-through; the line leaves the
+// XCD's L2 clean).  The next reader of a column is almost always a workgroup on another XCD, so
+// keeping the line in this L2 buys nothing, while a dirty line makes the agent release of the next
+// barrier write it back on the critical path (MI355X_MICROARCH.md: 1.7 us clean vs 6.5 us with
+// 16 KB dirty per block; a round dirtied 64 KB per workgroup at LP = 512).
+__device__ __forceinline__ void st_wt(double* p, double v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ double ld_wt(double* p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 
 // Full-precision fp64 reciprocal square root / reciprocal from the hardware estimates (two
 // Newton steps each): the inner rotations need c^2 + s^2 = 1 to rounding, not IEEE division.
@@ -117,7 +169,8 @@ __device__ __forceinline__ void pair_angle(const double* G, int p, int q, double
     s = rot ? cc * t : 0.0;
 }
 
-size_t block_jacobi_lds(int MR) { return ((MR <= 512 ? (size_t)32 * (MR + 1) : 0) + 3 * 32 * GS) * sizeof(double); }
+// rows: the rows one workgroup stages (MR / G)
+size_t block_jacobi_lds(int rows) { return ((rows <= 512 ? (size_t)32 * (rows + 1) : 0) + 3 * 32 * GS) * sizeof(double); }
 
 constexpr int kBJThreads = 512;  // 8 waves: 2 per SIMD for the MFMA phases
 
@@ -180,13 +233,12 @@ __device__ __forceinline__ double* inner_sweep(double* Ga, double* Gb, double* J
     return cur;
 }
 
-// Stage the 32 columns col(0..31) of a column-major LP x LP matrix into LDS rows of pitch LP + 1.
-
-// 32 LP / 2 double2: each thread keeps up to 4 loads in flight.
+// Stage rows [row0, row0 + nr) of the 32 columns col(0..31) of a column-major matrix (ld rows per
+// column) into LDS rows of pitch nr + 1; 32 nr / 2 double2, each thread keeping up to 4 loads in flight.
 template <typename F>
-__device__ __forceinline__ void stage_pair(double* Xs, const double* __restrict__ S, int LP, F col) {
-    const int XP = LP + 1;
-    const int per = LP / 2;  // double2 per column
+__device__ __forceinline__ void stage_pair(double* Xs, const double* __restrict__ S, int ld, int row0, int nr, F col) {
+    const int XP = nr + 1;
+    const int per = nr / 2;  // double2 per column
     const int tot = 32 * per;
     for (int e0 = threadIdx.x; e0 < tot; e0 += 4 * kBJThreads) {
         double2 v[4];
@@ -195,7 +247,7 @@ __device__ __forceinline__ void stage_pair(double* Xs, const double* __restrict_
             const int e = e0 + kBJThreads * u;
             if (e < tot) {
                 const int k = e / per, i = 2 * (e % per);
-                v[u] = *reinterpret_cast<const double2*>(S + (int64_t)col(k) * LP + i);
+                v[u] = *reinterpret_cast<const double2*>(S + (int64_t)col(k) * ld + row0 + i);
             }
         }
 #pragma unroll
@@ -210,12 +262,13 @@ __device__ __forceinline__ void stage_pair(double* Xs, const double* __restrict_
     }
 }
 
-// D[:, col(j)] = sum_k Xs[k][:] Jp[k][j] for the 32 pair columns (fp64 MFMA), wave w -> row tiles w, w+4, ...
+// D[row0 + i, col(j)] = sum_k Xs[k][i] Jp[k][j], i < nr, for the 32 pair columns (fp64 MFMA; D has
+// ld rows per column), wave w -> row tiles w, w + 8, ...
 template <typename F>
-__device__ __forceinline__ void apply_pair(const double* Xs, const double* Jp, double* __restrict__ D, int LP, F col,
-                                           int w, int r, int h) {
-    const int XP = LP + 1;
-    for (int it = w; it < LP / 16; it += kBJThreads / 64) {
+__device__ __forceinline__ void apply_pair(const double* Xs, const double* Jp, double* __restrict__ D, int ld, int row0,
+                                           int nr, F col, int w, int r, int h) {
+    const int XP = nr + 1;
+    for (int it = w; it < nr / 16; it += kBJThreads / 64) {
         const int i0 = 16 * it;
         f64x4 acc0 = MD::zero(), acc1 = MD::zero();
 #pragma unroll
@@ -226,8 +279,8 @@ __device__ __forceinline__ void apply_pair(const double* Xs, const double* Jp, d
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            D[(int64_t)col(r) * LP + i0 + MD::row(h, j)] = acc0[j];
-            D[(int64_t)col(16 + r) * LP + i0 + MD::row(h, j)] = acc1[j];
+            st_wt(D + (int64_t)col(r) * ld + row0 + i0 + MD::row(h, j), acc0[j]);
+            st_wt(D + (int64_t)col(16 + r) * ld + row0 + i0 + MD::row(h, j), acc1[j]);
         }
     }
 }
@@ -236,12 +289,13 @@ __device__ __forceinline__ void apply_pair(const double* Xs, const double* Jp, d
 // the 16 lanes of an MFMA row read 128 contiguous bytes of one column), all 8 k-steps in flight.
 template <typename F>
 __device__ __forceinline__ void apply_pair_global(const double* __restrict__ Src, const double* Jp,
-                                                  double* __restrict__ D, int LP, F col, int w, int r, int h) {
-    for (int it = w; it < LP / 16; it += kBJThreads / 64) {
-        const int i0 = 16 * it;
+                                                  double* __restrict__ D, int ld, int row0, int nr, F col, int w, int r,
+                                                  int h) {
+    for (int it = w; it < nr / 16; it += kBJThreads / 64) {
+        const int i0 = row0 + 16 * it;
         double a[8];
 #pragma unroll
-        for (int kk = 0; kk < 8; ++kk) a[kk] = Src[(int64_t)col(4 * kk + h) * LP + i0 + r];
+        for (int kk = 0; kk < 8; ++kk) a[kk] = Src[(int64_t)col(4 * kk + h) * ld + i0 + r];
         f64x4 acc0 = MD::zero(), acc1 = MD::zero();
 #pragma unroll
         for (int kk = 0; kk < 8; ++kk) {
@@ -250,8 +304,8 @@ __device__ __forceinline__ void apply_pair_global(const double* __restrict__ Src
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            D[(int64_t)col(r) * LP + i0 + MD::row(h, j)] = acc0[j];
-            D[(int64_t)col(16 + r) * LP + i0 + MD::row(h, j)] = acc1[j];
+            st_wt(D + (int64_t)col(r) * ld + i0 + MD::row(h, j), acc0[j]);
+            st_wt(D + (int64_t)col(16 + r) * ld + i0 + MD::row(h, j), acc1[j]);
         }
     }
 }
@@ -275,13 +329,13 @@ __device__ long long g_bj_prof[8];
 // Gp = X_pair^T X_pair with the pair's columns read from global memory (MR > 512 rows: no LDS
 // image), wave w -> tile ((w >> 1) & 1, w & 1) over row half w >> 2; the halves land in Ga / Gb.
 template <typename F>
-__device__ __forceinline__ void pair_gram_global(const double* __restrict__ X, int MR, F col, int w, int r, int h,
-                                                 double* Ga, double* Gb) {
+__device__ __forceinline__ void pair_gram_global(const double* __restrict__ X, int MR, int row0, int nr, F col, int w,
+                                                 int r, int h, double* Ga, double* Gb) {
     const int ta = (w >> 1) & 1, tb = w & 1, half = w >> 2;
     const double* xa = X + (int64_t)col(16 * ta + r) * MR + 4 * h;
     const double* xb = X + (int64_t)col(16 * tb + r) * MR + 4 * h;
     f64x4 acc[2] = {MD::zero(), MD::zero()};
-    const int ibeg = half * (MR / 2), iend = ibeg + MR / 2;
+    const int ibeg = row0 + half * (nr / 2), iend = ibeg + nr / 2;
     for (int i0 = ibeg; i0 < iend; i0 += 16) {
         const double2 a01 = *reinterpret_cast<const double2*>(xa + i0);
         const double2 a23 = *reinterpret_cast<const double2*>(xa + i0 + 2);
@@ -303,12 +357,13 @@ __device__ __forceinline__ double u64_as_double(unsigned long long v) { return _
 // of the MR x LP column-major X (global, after an acquire): 16 x 16 Gram tiles on the fp64 MFMA,
 // the column norms accumulated from the same operand loads.  Columns with norm^2 <= negl (and the
 // zero padding) are excluded, as the rotations exclude them.
-__device__ double slice_max_cos2(const double* __restrict__ X, int MR, int LP, int wg, int w, int lane, double negl) {
+__device__ double slice_max_cos2(const double* __restrict__ X, int MR, int LP, int slice, int g, int G, int w, int lane,
+                                 double negl) {
     const int r = lane & 15, h = lane >> 4;
     double mx = 0.0;
     const int ntile = 2 * (LP / 16);
-    for (int t = w; t < ntile; t += kBJThreads / 64) {
-        const int a0 = 32 * wg + 16 * (t & 1), b0 = 16 * (t >> 1);
+    for (int t = w + (kBJThreads / 64) * g; t < ntile; t += (kBJThreads / 64) * G) {
+        const int a0 = 32 * slice + 16 * (t & 1), b0 = 16 * (t >> 1);
         const double* xa = X + (int64_t)(a0 + r) * MR + 4 * h;
         const double* xb = X + (int64_t)(b0 + r) * MR + 4 * h;
         f64x4 acc = MD::zero();
@@ -343,16 +398,19 @@ __device__ double slice_max_cos2(const double* __restrict__ X, int MR, int LP, i
 }
 
 // X = the mrv x l source (column-major with ld lds, or row-major when src_rowmajor: X = src^T),
-// zero-padded to MR x LP (MR, LP multiples of 32); J = I (LP x LP).  MR <= 512: the pair's columns
-// are staged in LDS; beyond, the pair Gram and the X product read them from global memory.
+// zero-padded to MR x LP (MR, LP multiples of 32); J = I (LP x LP).  Grid: (LP / 32) pairs x G
+// row-group members (MR % 32 G == 0, LP % 16 G == 0).  MR / G <= 512: the member's rows of the pair
+// columns are staged in LDS; beyond, the pair Gram and the X product read them from global memory.
+// scratch: nwg + 1024 nwg doubles (||W||_F partials, then the partial pair Grams when G > 1).
 __global__ __launch_bounds__(kBJThreads) void block_jacobi_kernel(const double* __restrict__ R, int64_t lds,
-                                                           int src_rowmajor, int mrv, int l, int MR, int LP,
+                                                           int src_rowmajor, int mrv, int l, int MR, int LP, int G,
                                                            double* __restrict__ Xb, double* __restrict__ Jb,
                                                            double* __restrict__ scratch, unsigned* __restrict__ sync,
                                                            int* __restrict__ info, double quad2, double tol_chk2) {
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-    const bool staged = MR <= 512;
-    const int XP = MR + 1;
+    const int rpg = MR / G, jpg = LP / G;  // rows of X / J per group member
+    const bool staged = rpg <= 512;
+    const int XP = rpg + 1;
     double* Xs = reinterpret_cast<double*>(smem_raw);  // [32][MR + 1]: the pair's columns (staged)
     double* Ga = Xs + (staged ? 32 * XP : 0);          // [32][GS] x 2: the pair Gram (Gb: the MFMA half)
     double* Gb = Ga + 32 * GS;
@@ -365,6 +423,10 @@ __global__ __launch_bounds__(kBJThreads) void block_jacobi_kernel(const double* 
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int r = lane & 15, h = lane >> 4;
     const int nwg = gridDim.x, wg = blockIdx.x;
+    const int pr = wg / G, g = wg - pr * G;  // block pair (round-robin slot), row-group member
+    const int xr0 = g * rpg, jr0 = g * jpg;
+    unsigned* gctr = sync + kGroupWord + pr;
+    double* gpart = scratch + ((nwg + 31) & ~31);  // [pair][member] 32 x 32 partial Grams
     const int NB = LP / 16;
     const int64_t L2 = (int64_t)LP * LP, L2X = (int64_t)MR * LP;
     const double tol = (double)l * kEps, tol2 = tol * tol;
@@ -409,14 +471,14 @@ __global__ __launch_bounds__(kBJThreads) void block_jacobi_kernel(const double* 
     for (int sweep = 0; sweep < kMaxSweeps; ++sweep) {
         for (int round = 0; round < NB - 1; ++round) {
             int P, Q;
-            rr_pair(round, wg, NB, P, Q);
+            rr_pair(round, pr, NB, P, Q);
             const double* Xsrc = Xb + (size_t)par * L2X;
             const double* Jsrc = Jb + (size_t)par * L2;
             double* Xd = Xb + (size_t)(1 - par) * L2X;
             double* Jd = Jb + (size_t)(1 - par) * L2;
             auto col = [&](int k) { return k < 16 ? 16 * P + k : 16 * Q + k - 16; };
             // 1. the pair's columns of X into LDS
-            if (staged) stage_pair(Xs, Xsrc, MR, col);
+            if (staged) stage_pair(Xs, Xsrc, MR, xr0, rpg, col);
             if (tid < 8) flags[tid] = 0;
             if (tid == 0) lmax = 0ull;
             __syncthreads();
@@ -424,13 +486,13 @@ __global__ __launch_bounds__(kBJThreads) void block_jacobi_kernel(const double* 
             // 2. Gp = X_pair^T X_pair: wave w -> tile ((w >> 1) & 1, w & 1) over row half w >> 2 (four
             //    independent MFMA chains); the halves meet in Ga (half 0) + Gb (half 1)
             if (!staged) {
-                pair_gram_global(Xsrc, MR, col, w, r, h, Ga, Gb);
+                pair_gram_global(Xsrc, MR, xr0, rpg, col, w, r, h, Ga, Gb);
             } else {
                 const int ta = (w >> 1) & 1, tb = w & 1, half = w >> 2;
                 const double* xa = Xs + (16 * ta + r) * XP + h;
                 const double* xb = Xs + (16 * tb + r) * XP + h;
                 f64x4 acc[4] = {MD::zero(), MD::zero(), MD::zero(), MD::zero()};
-                const int ibeg = half * (MR / 2), iend = ibeg + MR / 2;
+                const int ibeg = half * (rpg / 2), iend = ibeg + rpg / 2;
                 for (int i0 = ibeg; i0 < iend; i0 += 16) {
 #pragma unroll
                     for (int u = 0; u < 4; ++u) acc[u] = MD::mma(xa[i0 + 4 * u], xb[i0 + 4 * u], acc[u]);
@@ -441,9 +503,29 @@ __global__ __launch_bounds__(kBJThreads) void block_jacobi_kernel(const double* 
                     Gd[(16 * ta + MD::row(h, j)) * GS + 16 * tb + r] = (acc[0][j] + acc[1][j]) + (acc[2][j] + acc[3][j]);
             }
             __syncthreads();
-            for (int e = tid; e < 32 * 32; e += kBJThreads) {
-                const int i = e / 32, j = e % 32;
-                Ga[i * GS + j] += Gb[i * GS + j];
+            if (G == 1) {
+                for (int e = tid; e < 32 * 32; e += kBJThreads) {
+                    const int i = e / 32, j = e % 32;
+                    Ga[i * GS + j] += Gb[i * GS + j];
+                }
+            } else {
+                // publish this member's rows' Gram, meet the group, sum the G partials in member order
+                double* mine = gpart + (int64_t)wg * 1024;
+                for (int e = tid; e < 32 * 32; e += kBJThreads) {
+                    const int i = e / 32, j = e % 32;
+                    st_wt(mine + e, Ga[i * GS + j] + Gb[i * GS + j]);
+                }
+                if (!group_barrier(sync, gctr, (unsigned)G * (unsigned)(sweep * (NB - 1) + round + 1))) {
+                    if (tid == 0) info[2] = 1;
+                    return;
+                }
+                double* grp = gpart + (int64_t)pr * G * 1024;
+                for (int e = tid; e < 32 * 32; e += kBJThreads) {
+                    const int i = e / 32, j = e % 32;
+                    double v = ld_wt(grp + e);
+                    for (int m = 1; m < G; ++m) v += ld_wt(grp + (int64_t)m * 1024 + e);
+                    Ga[i * GS + j] = v;
+                }
             }
             __syncthreads();
             BJ_T(2);
@@ -479,22 +561,26 @@ __global__ __launch_bounds__(kBJThreads) void block_jacobi_kernel(const double* 
                 BJ_T(3);
                 // 5. X_pair Jp and J_pair Jp -> destination buffer
                 if (staged)
-                    apply_pair(Xs, Jp, Xd, MR, col, w, r, h);
+                    apply_pair(Xs, Jp, Xd, MR, xr0, rpg, col, w, r, h);
                 else
-                    apply_pair_global(Xsrc, Jp, Xd, MR, col, w, r, h);
+                    apply_pair_global(Xsrc, Jp, Xd, MR, xr0, rpg, col, w, r, h);
                 BJ_T(4);
-                apply_pair_global(Jsrc, Jp, Jd, LP, col, w, r, h);
+                apply_pair_global(Jsrc, Jp, Jd, LP, jr0, jpg, col, w, r, h);
                 BJ_T(5);
             } else {
-                for (int e = tid; e < 32 * (MR / 2); e += kBJThreads) {
-                    const int kk = e / (MR / 2), i = 2 * (e % (MR / 2));
-                    const int64_t o = (int64_t)col(kk) * MR + i;
-                    *reinterpret_cast<double2*>(Xd + o) = *reinterpret_cast<const double2*>(Xsrc + o);
+                for (int e = tid; e < 32 * (rpg / 2); e += kBJThreads) {
+                    const int kk = e / (rpg / 2), i = 2 * (e % (rpg / 2));
+                    const int64_t o = (int64_t)col(kk) * MR + xr0 + i;
+                    const double2 v = *reinterpret_cast<const double2*>(Xsrc + o);
+                    st_wt(Xd + o, v.x);
+                    st_wt(Xd + o + 1, v.y);
                 }
-                for (int e = tid; e < 32 * (LP / 2); e += kBJThreads) {
-                    const int kk = e / (LP / 2), i = 2 * (e % (LP / 2));
-                    const int64_t o = (int64_t)col(kk) * LP + i;
-                    *reinterpret_cast<double2*>(Jd + o) = *reinterpret_cast<const double2*>(Jsrc + o);
+                for (int e = tid; e < 32 * (jpg / 2); e += kBJThreads) {
+                    const int kk = e / (jpg / 2), i = 2 * (e % (jpg / 2));
+                    const int64_t o = (int64_t)col(kk) * LP + jr0 + i;
+                    const double2 v = *reinterpret_cast<const double2*>(Jsrc + o);
+                    st_wt(Jd + o, v.x);
+                    st_wt(Jd + o + 1, v.y);
                 }
             }
             par = 1 - par;
@@ -512,7 +598,7 @@ __global__ __launch_bounds__(kBJThreads) void block_jacobi_kernel(const double* 
         // the global check, once the sweep's rotations were small enough to have squared below tol_chk2
         const double pre = u64_as_double(__hip_atomic_load(smax + sweep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
         if (tol_chk2 > 0.0 && pre <= sqrt(tol_chk2)) {  // pre-rotation cos <= sqrt(tol): squared below ~tol
-            const double mx = slice_max_cos2(Xb + (size_t)par * L2X, MR, LP, wg, w, lane, negl);
+            const double mx = slice_max_cos2(Xb + (size_t)par * L2X, MR, LP, pr, g, G, w, lane, negl);
             if (tid == 0) lmax = 0ull;
             __syncthreads();
             atomicMax(&lmax, (unsigned long long)__double_as_longlong(mx));
@@ -703,15 +789,31 @@ __global__ __launch_bounds__(1024) void block_jacobi_complete_kernel(const T* __
 
 }  // namespace
 
+int block_jacobi_groups(int MR, int LP, int G) {
+    // scratch (U_w, MR x LP doubles) must hold nwg + 1024 nwg doubles; members split MR and LP rows
+    // into whole 32- / 16-row tiles
+    auto ok = [&](int g) {
+        const int64_t nwg = (int64_t)(LP / 32) * g;
+        return MR % (32 * g) == 0 && LP % (16 * g) == 0 && ((nwg + 31) & ~31) + 1024 * nwg <= (int64_t)MR * LP;
+    };
+    if (G > 0) return ok(G) ? G : 0;
+    for (int g : {4, 2}) {
+        if (ok(g)) return g;
+    }
+    return 1;
+}
+
 template <typename T>
 hipError_t launch_block_jacobi_ex(const double* src, int64_t lds, int src_rowmajor, int mrv, int l, int MR, int LP,
                                   double* X, double* J, double* Uw, double* Vw, T* S, unsigned* sync, int* info,
-                                  hipStream_t s, double quad2, double tol_chk) {
+                                  hipStream_t s, double quad2, double tol_chk, int G) {
     if (LP % 32 || LP < 64 || LP > 4096 || MR % 32 || MR < 32 || l > LP || mrv > MR) return hipErrorInvalidValue;
+    G = block_jacobi_groups(MR, LP, G);
+    if (G < 1) return hipErrorInvalidValue;
     hipError_t e = hipMemsetAsync(sync, 0, kSyncWords * sizeof(unsigned), s);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(block_jacobi_kernel, dim3(LP / 32), dim3(kBJThreads), block_jacobi_lds(MR), s, src, lds,
-                       src_rowmajor, mrv, l, MR, LP, X, J, Uw, sync, info, quad2, tol_chk * tol_chk);
+    hipLaunchKernelGGL(block_jacobi_kernel, dim3(LP / 32 * G), dim3(kBJThreads), block_jacobi_lds(MR / G), s, src, lds,
+                       src_rowmajor, mrv, l, MR, LP, G, X, J, Uw, sync, info, quad2, tol_chk * tol_chk);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     const size_t lds_fin = (size_t)LP * 8 * 2 + (size_t)LP * 4 + 64;
@@ -729,20 +831,21 @@ hipError_t launch_block_jacobi_ex(const double* src, int64_t lds, int src_rowmaj
 
 template <typename T>
 hipError_t launch_block_jacobi(const double* R, int l, int LP, double* X, double* J, double* Uw, double* Vw, T* S,
-                               unsigned* sync, int* info, hipStream_t s, double quad2, double tol_chk) {
+                               unsigned* sync, int* info, hipStream_t s, double quad2, double tol_chk, int G) {
     if (LP > 512) return hipErrorInvalidValue;
-    return launch_block_jacobi_ex<T>(R, LP, 0, l, l, LP, LP, X, J, Uw, Vw, S, sync, info, s, quad2, tol_chk);
+    return launch_block_jacobi_ex<T>(R, LP, 0, l, l, LP, LP, X, J, Uw, Vw, S, sync, info, s, quad2, tol_chk, G);
 }
 
 template hipError_t launch_block_jacobi<float>(const double*, int, int, double*, double*, double*, double*, float*,
-                                               unsigned*, int*, hipStream_t, double, double);
+                                               unsigned*, int*, hipStream_t, double, double, int);
 template hipError_t launch_block_jacobi<double>(const double*, int, int, double*, double*, double*, double*, double*,
-                                                unsigned*, int*, hipStream_t, double, double);
+                                                unsigned*, int*, hipStream_t, double, double, int);
 template hipError_t launch_block_jacobi_ex<float>(const double*, int64_t, int, int, int, int, int, double*, double*,
-                                                  double*, double*, float*, unsigned*, int*, hipStream_t, double, double);
+                                                  double*, double*, float*, unsigned*, int*, hipStream_t, double, double,
+                                                  int);
 template hipError_t launch_block_jacobi_ex<double>(const double*, int64_t, int, int, int, int, int, double*, double*,
                                                    double*, double*, double*, unsigned*, int*, hipStream_t, double,
-                                                   double);
+                                                   double, int);
 
 #ifdef RSVD_BJ_PROF
 void bj_prof_dump() {

@@ -264,10 +264,12 @@ static void bench_jac() {
             CK(hipMalloc(&Sd, LP * 8));
             CK(hipMalloc(&sync, kBJSyncWords * 4));
             CK(hipMalloc(&info, 16 * 4));
-            for (int prec = 0; prec < 2; ++prec) {  // 0: fp64 results, 1: fp32 results
+            for (int pg = 0; pg < 6; ++pg) {  // prec 0: fp64 results, 1: fp32 results; G = 1, 2, 4 row groups
+                const int prec = pg & 1, G = 1 << (pg >> 1);
+                if (block_jacobi_groups(LP, LP, G) != G) continue;
                 CK(hipMemset(info, 0, 64));
                 const double q2 = prec ? 1e-8 : 1e-16, tc = prec ? kBJTolF32 : kBJTolF64;
-                double t = time_us([&] { CK(launch_block_jacobi<double>(R, LP, LP, X, J, Uw, Vw, Sd, sync, info, S, q2, tc)); }, 3);
+                double t = time_us([&] { CK(launch_block_jacobi<double>(R, LP, LP, X, J, Uw, Vw, Sd, sync, info, S, q2, tc, G)); }, 3);
                 int hinfo[4];
                 CK(hipMemcpy(hinfo, info, 16, hipMemcpyDeviceToHost));
                 std::vector<double> hS(LP);
@@ -293,9 +295,9 @@ static void bench_jac() {
                         orth += (o - (i == j)) * (o - (i == j));
                         uorth += (uo - (i == j)) * (uo - (i == j));
                     }
-                printf("block_jacobi LP=%d %s %s: %.1f us  sweeps=%d timeout=%d  S[0]=%.6f S[last]=%.3e  |W-USV'|/|W|=%.2e  "
+                printf("block_jacobi LP=%d G=%d %s %s: %.1f us  sweeps=%d timeout=%d  S[0]=%.6f S[last]=%.3e  |W-USV'|/|W|=%.2e  "
                        "|V'V-I|=%.2e |U'U-I|=%.2e\n",
-                       LP, kind ? "c4-cluster" : "graded", prec ? "f32-out" : "f64-out", t, hinfo[0], hinfo[2], hS[0],
+                       LP, G, kind ? "c4-cluster" : "graded", prec ? "f32-out" : "f64-out", t, hinfo[0], hinfo[2], hS[0],
                        hS[LP - 1], sqrt(rec / wn), sqrt(orth), sqrt(uorth));
             }
             CK(hipFree(R)); CK(hipFree(X)); CK(hipFree(J)); CK(hipFree(Uw)); CK(hipFree(Vw)); CK(hipFree(Sd));
