@@ -388,6 +388,7 @@ def main():
         bound, achieved, peak, unit = "mfma", flop_launch / t_s / 1e12, PEAK_TFLOPS[dt], "TFLOP/s"
     key = f"{args.config}_{dt}_{m_local}x{n}_l{l}_q{q}"
     lowp = dt in ("bf16", "fp8")
+    per_op = 1  # kernel dispatches per timed projection (the HIP events bracket the whole product)
     if lowp:  # the LDS-DMA kernels (hi/lo split skinny operand): wproj3 (bf16, LP 256 / 512; TN at
         # LP 256 with two-step A slots: wproj3tn2), wproj2<FP8, NN, LP, SPLIT> otherwise
         nn = kname.startswith("proj_nn")
@@ -396,11 +397,16 @@ def main():
             kpref = "wproj3tn2_kernel<true"
         elif dt == "bf16" and LPk in (256, 512):
             kpref = f"wproj3_kernel<{'true' if nn else 'false'}, {LPk}, true"
+        elif dt == "fp8" and LPk == 512:  # two 256-column half launches per product (WProjPlan::half)
+            kpref = f"wproj2_kernel<true, {'true' if nn else 'false'}, 256, true"
+            per_op = 2
         else:
             kpref = f"wproj2_kernel<{'true' if dt == 'fp8' else 'false'}, {'true' if nn else 'false'}, {LPk}, true"
     else:
         kpref = "proj_tn_kernel" if kname.startswith("proj_tn") else "proj_nn_kernel"
     tr = pmc_traffic(key, kpref)
+    if tr:
+        tr = (tr[0] * per_op, tr[1])
     mb = pmc_mfma_busy(key, kpref)
     roof = {
         "bound": bound,
@@ -411,6 +417,7 @@ def main():
         "frac": achieved / peak,
         "traffic": tr[0] if tr else None,
         "traffic_unit": "bytes per launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE)",
+        "kernel_dispatches_per_launch": per_op,
         "traffic_source": tr[1] if tr else None,
         "avg_launch_us": avg_ms * 1e3,
         "algorithmic_flop_per_launch": flop_launch,
