@@ -176,7 +176,9 @@ static void bench_chol() {
                 e2 += (s2 - (i == j)) * (s2 - (i == j));
             }
 #ifdef RSVD_CHOL_PROF
+        rsvd::chol_variant = LP == 512 ? 0 : 1;  // LP = 512 ran chol_wide_kernel
         rsvd::chol_prof_dump(LP);
+        rsvd::chol_variant = 1;
 #endif
         const bool same = !memcmp(hR0.data(), hR.data(), hR.size() * 8) && !memcmp(hRi0.data(), hRi.data(), hRi.size() * 8);
         printf("chol LP=%d: wide %.1f us  reg %.1f us  bit-identical %d   |R^T R - G|/|G| = %.2e  |R Rinv - I| = %.2e\n", LP,
@@ -353,6 +355,31 @@ static void bench_proj(bool c4only = false) {
             CK(hipFree(slabs));
         }
         CK(hipFree(A)); CK(hipFree(Sh)); CK(hipFree(Sl)); CK(hipFree(Out));
+    }
+}
+
+// C5 e4m3 TN / NN at LP = 512 with a power-of-two column stride (lda = m) against a padded one:
+// the L2-set hypothesis for the TN A over-fetch (32-B column runs per k-step, 2^17-B stride)
+static void bench_c5_stride() {
+    const int64_t m = 131072, n = 8192;
+    const int LP = 512;
+    for (int64_t pad : {0, 256, 4096 + 256}) {
+        const int64_t lda = m + pad;
+        void* A;
+        CK(hipMalloc(&A, (size_t)lda * n));
+        hipLaunchKernelGGL(fill_random_kernel, dim3(4096), dim3(256), 0, S, (uint16_t*)A, (size_t)lda * n / 2, 1);
+        bf16_t* Sh = dev_random<bf16_t>((size_t)m * LP);
+        bf16_t* Sl = dev_random<bf16_t>((size_t)m * LP);
+        float* Out;
+        CK(hipMalloc(&Out, (size_t)m * LP * 4));
+        WProjPlan pnn = plan_wproj(m, n, LP, true, true, true), ptn = plan_wproj(n, m, LP, true, false, true);
+        float* slabs;
+        CK(hipMalloc(&slabs, (size_t)std::max<int64_t>(pnn.splits * m, ptn.splits * n) * LP * 4));
+        double t2 = time_us([&] { CK(launch_wproj(1, 1, A, lda, m, n, Sh, Sl, LP, pnn, slabs, Out, S)); });
+        double t3 = time_us([&] { CK(launch_wproj(0, 1, A, lda, m, n, Sh, Sl, LP, ptn, slabs, Out, S)); });
+        printf("C5 e4m3 LP=512 lda=m+%ld: NN2 %.1f us  TN2 %.1f us (half=%d, splits nn=%d tn=%d)\n", (long)pad, t2, t3,
+               (int)ptn.half, pnn.splits, ptn.splits);
+        CK(hipFree(slabs)); CK(hipFree(A)); CK(hipFree(Sh)); CK(hipFree(Sl)); CK(hipFree(Out));
     }
 }
 
@@ -654,6 +681,7 @@ int main(int argc, char** argv) {
     if (what == "all" || what == "jac") bench_jac();
     if (what == "all" || what == "proj") bench_proj();
     if (what == "proj4") bench_proj(true);
+    if (what == "c5stride") bench_c5_stride();
     if (what == "kn") {  // v3 knob sweep at C4: bit 0 non-temporal A, bit 1 s_setprio on waves 4-7
         const int64_t m = 65536, n = 65536;
         const int LP = 256;
