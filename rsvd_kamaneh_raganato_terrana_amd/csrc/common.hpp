@@ -12,6 +12,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <tuple>
+
 namespace rsvd {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -60,6 +62,21 @@ template <> struct Vec16<double> {
     typedef double2 type;
     static __device__ __forceinline__ double get(const double2& v, int t) { return t == 0 ? v.x : v.y; }
 };
+
+// Launch of a persistent grid whose workgroups wait on each other (grid barriers, spin hand-offs):
+// a cooperative launch, so co-residency is the runtime's guarantee -- the launch fails when the
+// grid cannot be resident at once (e.g. CUs held by another process's kernels) -- instead of an
+// assumption the kernel's bounded spins can only report after the fact.
+template <typename... P, typename... A>
+hipError_t launch_coresident(void (*kernel)(P...), dim3 grid, dim3 block, size_t lds, hipStream_t s, A&&... a) {
+    std::tuple<P...> args(static_cast<P>(a)...);
+    void* argv[sizeof...(P) > 0 ? sizeof...(P) : 1];
+    std::apply([&](auto&... x) {
+        int i = 0;
+        ((argv[i++] = static_cast<void*>(&x)), ...);
+    }, args);
+    return hipLaunchCooperativeKernel(reinterpret_cast<const void*>(kernel), grid, block, argv, (unsigned)lds, s);
+}
 
 // XCD-aware bijective block remap (cdna_hip_programming.md §5 "XCD swizzle must be bijective"):
 // blocks that the dispatcher deals to the same XCD (b % 8) get consecutive logical ids, so

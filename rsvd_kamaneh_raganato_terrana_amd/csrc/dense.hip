@@ -945,9 +945,8 @@ hipError_t launch_power_grid(const double* A, int64_t lda, int64_t m, int64_t n,
                              double* part, unsigned* sync, int* kept, int* tmo, hipStream_t s) {
     hipError_t e = hipMemsetAsync(sync, 0, 8 * sizeof(unsigned), s);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(power_grid_kernel, dim3(power_grid_size(n)), dim3(kPgThreads), 0, s, A, lda, m, n, B, dim, seed,
-                       iters, U, ldu, V, ldv, S, Y, part, sync, kept, tmo);
-    return hipGetLastError();
+    return launch_coresident(power_grid_kernel, dim3(power_grid_size(n)), dim3(kPgThreads), 0, s, A, lda, m, n, B, dim,
+                             seed, iters, U, ldu, V, ldv, S, Y, part, sync, kept, tmo);
 }
 
 int power_iterations(int64_t n) {

@@ -439,7 +439,8 @@ __device__ __forceinline__ double* wtile(double* W, int np, int ib, int jb, int 
     return W + ((int64_t)ib * np + jb) * 256 + lane * 4;
 }
 
-__global__ __launch_bounds__(kCholThreads) void chol_wide_kernel(const double* __restrict__ G, int l, int LP,
+template <int NT, int B>
+__global__ __launch_bounds__(NT) void chol_wide_kernel(const double* __restrict__ G, int l, int LP,
                                                                  double tol, double* __restrict__ W,
                                                                  double* __restrict__ R, double* __restrict__ Rinv,
                                                                  int* __restrict__ colflag, int* __restrict__ flag,
@@ -448,8 +449,7 @@ __global__ __launch_bounds__(kCholThreads) void chol_wide_kernel(const double* _
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
     const int np = LP / 16;
     const int ldr = LP + kCholPad;
-    constexpr int nw = kCholThreads / 64;
-    constexpr int B = kCholBatch;
+    constexpr int nw = NT / 64;
     double* Dd = reinterpret_cast<double*>(smem_raw);  // [2][16][16] D^-1 of blocks p, p+1
     double* d0 = Dd + 512;                             // [LP] original diagonal of G
     double* Rs = d0 + LP;                              // [16][ldr] current R row strip
@@ -488,7 +488,7 @@ __global__ __launch_bounds__(kCholThreads) void chol_wide_kernel(const double* _
                 }
         }
     }
-    for (int i = tid; i < LP; i += kCholThreads) {
+    for (int i = tid; i < LP; i += NT) {
         d0[i] = (i < l) ? G[(int64_t)i * LP + i] : 0.0;
         colflag[i] = 0;
     }
@@ -1192,8 +1192,8 @@ hipError_t launch_chol_wide(const double* G, int l, int LP, double tol, double* 
         hipLaunchKernelGGL(chol_reg_kernel<16>, dim3(1), dim3(64 * kCholRegWaves), CholReg<16>::lds_bytes, s, G, l,
                            tol, R, Rinv, colflag, flag, pred);
     else
-        hipLaunchKernelGGL(chol_wide_kernel, dim3(1), dim3(kCholThreads), chol_lds_bytes(LP), s, G, l, LP, tol, work,
-                           R, Rinv, colflag, flag, pred);
+        hipLaunchKernelGGL((chol_wide_kernel<kCholThreads, kCholBatch>), dim3(1), dim3(kCholThreads), chol_lds_bytes(LP),
+                           s, G, l, LP, tol, work, R, Rinv, colflag, flag, pred);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(rinv_wide_kernel, dim3(LP / 16), dim3(256), 0, s, LP, R, Rinv, Rinv32, pred);

@@ -28,8 +28,9 @@
 // replicated.
 // Rounds are separated by an agent-scope grid barrier (MI355X_MICROARCH.md "Workgroup dispatch
 // ... inter-workgroup visibility": plain stores -> vmcnt(0) -> barrier -> release fence -> relaxed
-// counter; acquire fence after the poll).  The grid (<= 16 workgroups) is always co-resident;
-// every spin is bounded and reports a timeout instead of hanging.
+// counter; acquire fence after the poll).  The grid (<= 64 workgroups at LP = 512) is launched
+// cooperatively (launch_coresident): co-resident by the runtime's guarantee; every spin is still
+// bounded and reports a timeout instead of hanging.
 // Convergence: a sweep whose rotations all had cos^2 = g^2 / (ab) <= quad2 ends the iteration (the
 // next would only square them); and when a sweep's largest pre-rotation cosine is <= sqrt(tol_chk)
 // (quadratic convergence: small enough to have squared below tol_chk), the whole grid checks max cos
@@ -812,9 +813,8 @@ hipError_t launch_block_jacobi_ex(const double* src, int64_t lds, int src_rowmaj
     if (G < 1) return hipErrorInvalidValue;
     hipError_t e = hipMemsetAsync(sync, 0, kSyncWords * sizeof(unsigned), s);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(block_jacobi_kernel, dim3(LP / 32 * G), dim3(kBJThreads), block_jacobi_lds(MR / G), s, src, lds,
-                       src_rowmajor, mrv, l, MR, LP, G, X, J, Uw, sync, info, quad2, tol_chk * tol_chk);
-    e = hipGetLastError();
+    e = launch_coresident(block_jacobi_kernel, dim3(LP / 32 * G), dim3(kBJThreads), block_jacobi_lds(MR / G), s, src,
+                          lds, src_rowmajor, mrv, l, MR, LP, G, X, J, Uw, sync, info, quad2, tol_chk * tol_chk);
     if (e != hipSuccess) return e;
     const size_t lds_fin = (size_t)LP * 8 * 2 + (size_t)LP * 4 + 64;
     hipLaunchKernelGGL((block_jacobi_finish_kernel<T>), dim3(1), dim3(1024), lds_fin, s, X, l, MR, LP, sync, S);
