@@ -441,7 +441,9 @@ def main():
             sk = {"bound": "hbm", "achieved": sk_gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": sk_gbs / PEAK_HBM_GBS}
         else:
             sk = {"bound": "mfma", "achieved": sk_tf, "peak": sk_peak, "unit": "TFLOP/s", "frac": sk_tf / sk_peak}
-        sk.update({"kernel": "sketch Y = A Omega" + (" (e4m3 x e4m3, v_mfma_f32_16x16x32_fp8_fp8)" if dt == "fp8" else ""),
+        sk.update({"kernel": "sketch Y = A Omega" + (" (e4m3 x e4m3, " + ("v_mfma_f32_16x16x32_fp8_fp8" if os.environ.get("RSVD_FP8_SCALED") == "0"
+                                          else "block-scaled v_mfma_scale_f32_16x16x128_f8f6f4, unit scales") + ")"
+                                          if dt == "fp8" else ""),
                    "avg_launch_us": sk_s * 1e6, "achieved_TFLOPs": sk_tf, "achieved_GBps": sk_gbs, "launches_timed": sk_n})
         roof["sketch"] = sk
 

@@ -58,6 +58,8 @@ struct rsvd_handle_s {
 
 constexpr int kFlagWords = 32;
 constexpr int kFlagGramTimeout = 2, kFlagJacobiTimeout = 3, kFlagUnrepaired = 20, kFlagNonFinite = 21;
+// the split-Gram fallback test (wide.cpp cholqr_pass) and its factor's breakdown count (never read)
+constexpr int kFlagSplitIll = 24, kFlagSplitScratch = 25;
 
 // Per-run reset of the non-sticky flag words ([0..1] and [4..19]; the sticky words stay).
 inline hipError_t reset_run_flags(int* dflags, hipStream_t s) {

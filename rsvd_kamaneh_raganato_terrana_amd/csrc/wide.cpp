@@ -22,6 +22,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <string>
 
 #include "handle.hpp"
@@ -272,18 +273,46 @@ struct WideEngine {
     }
 
     double tol() const { return sizeof(T) == 4 ? 1e-13 : 1e-28; }
+    // the split Gram's relative entry error is ~3e-8 of sqrt(G_ii G_jj): pivots below 1e-5 of their
+    // diagonal (cond(P) past ~300) are refactored from the fp64 Gram
+    static constexpr double kSplitIllTol = 1e-5;
+    bool split_gram = false;
+    bool chol2 = true;  // two-level factor at LP = 512 (RSVD_CHOL2=0: the one-workgroup LP = 512 kernel)
     // panel_gemm's operand in the panel precision: fp64 matrices as-is, fp32 copies for fp32 panels
     const T* mat(const double* m64, const float* m32) const {
         if constexpr (sizeof(T) == 8) return m64; else return m32;
     }
 
     // One CholeskyQR pass Out = P chol(P^T P)^-1 (+ bf16 hi/lo of Out).  `pred`: predicated pass.
+    // fp32 panels of bf16 / e4m3 A (one rank, unpredicated passes): the Gram by the three-piece bf16
+    // split (wide_qr.hip gram_split_kernel, |dG| ~ 1e-8 |G|); when a pivot of its factor falls below
+    // kSplitIllTol of its diagonal (cond(P) beyond ~300, or a breakdown) the fp64 Gram and factor
+    // run again, predicated on that test (h->dflags[kFlagSplitIll]), and their R / R^-1 / flags stand.
     int cholqr_pass(const T* P, int64_t rows, const GramPlan& gp, T* Out, bool sharded, bf16_t* hi, bf16_t* lo,
                     int* flag, const int* pred) {
+        float* r32 = sizeof(T) == 4 ? Rinv32 : nullptr;
+        // LP = 512, l > 256: the two-level factor (wide_qr.hip launch_chol_wide_2level; JX is free
+        // scratch until the small SVD) for unpredicated passes
+        const bool two = chol2 && L.LP == 512 && L.l > 256;
+        auto factor = [&](int* fl, double ill_tol, int* ill) -> hipError_t {
+            if (two) return launch_chol_wide_2level(G, L.l, tol(), R, Rinv, r32, colflag, fl, W, JX, s, ill_tol, ill);
+            return launch_chol_wide(G, L.l, L.LP, tol(), R, Rinv, r32, colflag, fl, W, nullptr, s, ill_tol, ill);
+        };
+        if (split_gram && !sharded && !pred) {
+            int* ill = h->dflags + kFlagSplitIll;
+            RSVD_CK(launch_gram_split(reinterpret_cast<const float*>(P), rows, L.LP, gp, gslab, G, s));
+            RSVD_CK(factor(h->dflags + kFlagSplitScratch, kSplitIllTol, ill));
+            RSVD_CK(launch_gram_wide<T>(P, nullptr, rows, L.LP, gp, gslab, G, ill, s));
+            RSVD_CK(launch_chol_wide(G, L.l, L.LP, tol(), R, Rinv, r32, colflag, flag, W, ill, s));
+            RSVD_CK(launch_panel_gemm<T>(P, rows, L.LP, mat(Rinv, Rinv32), 1, Out, 0, 0, hi, lo, nullptr, s));
+            return RSVD_OK;
+        }
         RSVD_CK(launch_gram_wide<T>(P, nullptr, rows, L.LP, gp, gslab, G, pred, s));
         if (sharded) RSVD_TRY(allreduce(G, (int64_t)L.LP * L.LP, RSVD_F64));
-        RSVD_CK(launch_chol_wide(G, L.l, L.LP, tol(), R, Rinv, sizeof(T) == 4 ? Rinv32 : nullptr, colflag, flag, W,
-                                 pred, s));
+        if (pred)
+            RSVD_CK(launch_chol_wide(G, L.l, L.LP, tol(), R, Rinv, r32, colflag, flag, W, pred, s));
+        else
+            RSVD_CK(factor(flag, 0.0, nullptr));
         RSVD_CK(launch_panel_gemm<T>(P, rows, L.LP, mat(Rinv, Rinv32), 1, Out, 0, 0, hi, lo, pred, s));
         return RSVD_OK;
     }
@@ -465,6 +494,19 @@ int wide_typed(rsvd_handle_t h, const rsvd_desc_t* d, const void* A, const void*
     h->info.splits_tn = L.lowp ? L.wtn.splits : L.ptn.splits;
     WideEngine<T> E(h, L, d->dtype);
     E.qr_mode = d->qr_mode;
+    // the split Gram: fp32 panels of bf16 / e4m3 A (RSVD_GRAM_SPLIT=0 in the environment: fp64 Grams only)
+    {
+        static const int env = [] {
+            const char* v = std::getenv("RSVD_GRAM_SPLIT");
+            return v ? std::atoi(v) : 1;
+        }();
+        E.split_gram = env != 0 && sizeof(T) == 4 && L.lowp && gram_split_ok(L.LP);
+        static const int env2 = [] {
+            const char* v = std::getenv("RSVD_CHOL2");
+            return v ? std::atoi(v) : 1;
+        }();
+        E.chol2 = env2 != 0;
+    }
     E.lowp_inter = (d->flags & RSVD_FLAG_LOWP_INTERMEDIATES) != 0;
     E.seed = d->seed;
     E.nsh = L.nsh;

@@ -34,6 +34,7 @@ struct WProjPlan {
     int sd = 1;       // v3: S-panel prefetch distance in k-steps (1 or 2; A runs as far ahead as LDS allows)
     bool tn2 = false; // v3 TN at LP = 256 with two k-steps per A slot (128-B A lines)
     bool half = false; // e4m3 A at LP = 512: two LP = 256 column-half launches (256-row tiles)
+    bool tn4 = false;  // e4m3 TN at LP 256 / 512: four k-steps per A slot (128-B A lines, wproj3tn4_kernel)
     int abl = 0;      // lab-only ablations of the v3 kernel (tools/wide_lab.cpp), never set by the engine
     int kn = -1;      // lab-only knob override of the LP = 256 v3 kernels (-1: the engine's choice)
 };
@@ -74,8 +75,23 @@ hipError_t launch_gram_wide(const T* P, const T* P2, int64_t rows, int LP, const
 // R = chol(G[:l,:l]) (upper) and Rinv = R^-1, LP x LP fp64 zero-padded, one workgroup.  A pivot
 // d_k <= tol * G_kk (or not finite) is a breakdown: R row k := e_k, colflag[k] = 1, *flag += 1.
 // Also writes Rinv as fp32 when Rinv32 != nullptr.  `work`: LP x LP fp64.  `pred`: as above.
+// ill (nullable): set to 1 when a pivot d_k <= ill_tol * G_kk (else 0) -- the split-Gram fallback test.
 hipError_t launch_chol_wide(const double* G, int l, int LP, double tol, double* R, double* Rinv, float* Rinv32,
-                            int* colflag, int* flag, double* work, const int* pred, hipStream_t s);
+                            int* colflag, int* flag, double* work, const int* pred, hipStream_t s,
+                            double ill_tol = 0.0, int* ill = nullptr, const double* d0src = nullptr);
+// The same factor at LP = 512 (l > 256) in two 256-column levels: R11 = chol(G11) and
+// S = G22 - R12^T R12 (R12 = R11^-T G12) on the one-workgroup LP = 256 kernel, the off-diagonal
+// blocks R12 and Rinv12 = -Rinv11 R12 Rinv22 on the MFMA GEMM, breakdowns judged against the
+// diagonal of G as the one-level factor does.  scratch: 7 x 256^2 + 768 doubles.
+hipError_t launch_chol_wide_2level(const double* G, int l, double tol, double* R, double* Rinv, float* Rinv32,
+                                   int* colflag, int* flag, double* work, double* scratch, hipStream_t s,
+                                   double ill_tol = 0.0, int* ill = nullptr);
+constexpr size_t kChol2ScratchDoubles = (size_t)7 * 256 * 256 + 768;
+// G = P^T P of an fp32 panel by the three-piece bf16 split on the bf16 MFMA (fp64 accumulation per
+// 32-row step; |dG| ~ 1e-8 |G|) -- same plan / slab layout as launch_gram_wide.  LP in {128, 256, 512}.
+bool gram_split_ok(int LP);
+hipError_t launch_gram_split(const float* P, int64_t rows, int LP, const GramPlan& gp, double* slabs, double* G,
+                             hipStream_t s);
 // 1 (default): chol_reg_kernel for LP <= 128, chol_wide_kernel above; 0: chol_wide_kernel everywhere;
 // 2: also chol_reg_kernel at LP = 256 (lab A/B only).
 extern int chol_variant;

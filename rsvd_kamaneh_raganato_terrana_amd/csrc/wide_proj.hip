@@ -23,6 +23,8 @@
 // the row blocks of one K chunk on one XCD so their shared S chunk is an L2 hit.
 #include <type_traits>
 
+#include <cstdlib>
+
 #include "common.hpp"
 #include "kernels.hpp"
 #include "wide.hpp"
@@ -285,12 +287,12 @@ template <> struct W2Cfg<128, true> { static constexpr int WR = 4, WC = 2, G = 4
 template <> struct W2Cfg<256, false> { static constexpr int WR = 4, WC = 2, G = 8; };
 template <> struct W2Cfg<512, false> { static constexpr int WR = 2, WC = 4, G = 8; };
 
-template <int LP, bool SPLIT, bool FP8, bool DS = false, bool S8 = false>
+template <int LP, bool SPLIT, bool FP8, bool DS = false, bool S8 = false, bool SC = false>
 struct W2Shape {
     static constexpr int WR = W2Cfg<LP, DS>::WR, WC = W2Cfg<LP, DS>::WC, G = W2Cfg<LP, DS>::G;
     static constexpr int WI = WR * 64;            // output rows per workgroup
     static constexpr int NS = SPLIT ? 2 : 1;
-    static constexpr int KSS = DS ? 2 * KS : KS;  // k rows per stage
+    static constexpr int KSS = SC ? 4 * KS : (DS ? 2 * KS : KS);  // k rows per stage (SC: one K = 128 MFMA)
     static constexpr int SBYTES = KSS * LP * (S8 ? 1 : 2);  // one S panel tile (e4m3 S: one byte per element)
     static constexpr int ABYTES = KSS * WI * (FP8 ? 1 : 2);  // the A tile
     static constexpr int STAGE = NS * SBYTES + ABYTES;
@@ -378,13 +380,20 @@ __device__ __forceinline__ bf16x8_t fp8x8_to_bf16x8(i32x2 v) {
 // Omega -- so both operands stay e4m3 and the product runs on v_mfma_f32_16x16x32_fp8_fp8: no
 // widening of A, half the S bytes through L2 and LDS.  The S image is [32 k][LP] bytes swizzled
 // like the e4m3 A image and read with ds_read_b64_tr_b8.
-template <bool FP8, bool NN, int LP, bool SPLIT, bool DS = false, int KN = 0, bool S8 = false>
+// SC (with S8; K and the K chunks multiples of 128): 128-deep stages on the block-scaled
+// v_mfma_scale_f32_16x16x128_f8f6f4 with unit E8M0 scales (127) -- e4m3 x e4m3 exact, twice the
+// non-scaled fp8 form's rate (MI355X_MICROARCH.md "Matrix cores").  A lane's 32-byte fragment is
+// four ds_read_b64_tr_b8 at k rows 32 i + 8 h + (r >> 1), i = 0..3 (k = 32 i + 8 h .. + 7 of its
+// column), the same k set for the A and the B operand -- the contraction only needs the two
+// operands' k orders to agree (tools/mfma_scale_probe.hip: exact against a host product).
+template <bool FP8, bool NN, int LP, bool SPLIT, bool DS = false, int KN = 0, bool S8 = false, bool SC = false>
 __global__ __launch_bounds__(512) void wproj2_kernel(const void* __restrict__ Av, int64_t lda, int64_t rows_out,
                                                      int64_t K, int64_t arows, const bf16_t* __restrict__ Shi,
                                                      const bf16_t* __restrict__ Slo, float* __restrict__ out,
                                                      int64_t slab_stride, int64_t kchunk, int nrowblk, int s_pitch,
                                                      int o_pitch) {
-    typedef W2Shape<LP, SPLIT, FP8, DS, S8> SH;
+    typedef W2Shape<LP, SPLIT, FP8, DS, S8, SC> SH;
+    static_assert(!SC || S8, "scaled fp8 MFMA: e4m3 x e4m3 sketch only");
     static_assert(!DS || (!NN && !FP8), "double-step stages: bf16 TN only");
     static_assert(!S8 || (FP8 && NN && !SPLIT && LP >= 256), "e4m3 S: single-pass e4m3 NN at LP >= 256");
     constexpr int KSS = SH::KSS;
@@ -514,6 +523,52 @@ __global__ __launch_bounds__(512) void wproj2_kernel(const void* __restrict__ Av
         const uint32_t At = slot + NS * SH::SBYTES;
 #pragma unroll
         for (int ss = 0; ss < KSS / KS; ++ss) {  // the k-steps of the stage
+            if constexpr (SC) {  // one 128-deep step: A fragments [RT][4 x 8 B], B per column tile, double-buffered
+                typedef __attribute__((ext_vector_type(8))) int i32x8;
+                const int kb = 8 * h + (r >> 1);
+                i32x2 a8[RT][4];
+#pragma unroll
+                for (int t = 0; t < RT; ++t)
+#pragma unroll
+                    for (int i4 = 0; i4 < 4; ++i4) {
+                        const int k = kb + 32 * i4;
+                        a8[t][i4] = tr8_read_a(At + k * WI + 16 * ((4 * wr + t) ^ swz8<WI>(k)) + 8 * (r & 1));
+                    }
+                auto bread8 = [&](int g, i32x2 (&b)[4]) {
+#pragma unroll
+                    for (int i4 = 0; i4 < 4; ++i4) {
+                        const int k = kb + 32 * i4;
+                        b[i4] = tr8_read_a(slot + k * LP + 16 * ((wc * G + g) ^ swz8<LP>(k)) + 8 * (r & 1));
+                    }
+                };
+                i32x2 b8[2][4];
+                bread8(0, b8[0]);
+#pragma unroll
+                for (int t = 0; t < RT; ++t) wait_lgkm0(a8[t][0], a8[t][1], a8[t][2], a8[t][3]);
+                wait_lgkm0(b8[0][0], b8[0][1], b8[0][2], b8[0][3]);
+                i32x8 af8[RT];
+#pragma unroll
+                for (int t = 0; t < RT; ++t)
+                    af8[t] = i32x8{a8[t][0].x, a8[t][0].y, a8[t][1].x, a8[t][1].y,
+                                   a8[t][2].x, a8[t][2].y, a8[t][3].x, a8[t][3].y};
+#pragma unroll
+                for (int g = 0; g < G; ++g) {
+                    if (g + 1 < G) bread8(g + 1, b8[(g + 1) & 1]);
+                    __builtin_amdgcn_sched_barrier(0);
+                    const i32x2* b = b8[g & 1];
+                    const i32x8 bf = i32x8{b[0].x, b[0].y, b[1].x, b[1].y, b[2].x, b[2].y, b[3].x, b[3].y};
+#pragma unroll
+                    for (int t = 0; t < RT; ++t)
+                        acc[t][g] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(af8[t], bf, acc[t][g], 0, 0, 0,
+                                                                                     127, 0, 127);
+                    __builtin_amdgcn_sched_barrier(0);
+                    if (g + 1 < G) {
+                        i32x2(&n)[4] = b8[(g + 1) & 1];
+                        wait_lgkm0(n[0], n[1], n[2], n[3]);
+                    }
+                }
+                break;  // the whole 128-deep stage
+            }
             bf16x8_t af[RT];
             i32x2 a1[RT], a2[RT];
             i32x4 a4[RT];
@@ -1179,6 +1234,202 @@ __global__ __launch_bounds__(512) void wproj3tn2_kernel(const bf16_t* __restrict
         }
 }
 
+// v3 TN for e4m3 A at LP = 256 (and LP = 512 as two column halves): FOUR 32-deep k-steps per A
+// slot, so every A column contributes one full 128-B line per slot -- the e4m3 TN of wproj2 read
+// 32-B column runs per k-step, which the fabric fetched about 4x over (C5: 4.3-4.5 GB per launch
+// against 1.07 GB of A, profiles/r03_v1_c5_traffic.json).  A slot: [WI j][128 i] bytes, row j's
+// 16-B unit u (rows 16 u .. 16 u + 15) at unit u ^ ((j >> 1) & 7); a lane's step-hs fragment is the
+// 8 bytes of k 32 hs + 8 h .. + 7 of its column (ds_read_b64), widened to bf16 exactly.  S (the
+// bf16 hi / lo panels) keeps v3's 32-step row images, with a row pitch s_pitch (512 for a half of
+// an LP = 512 panel) and the output pitch o_pitch.  K chunks are multiples of 128 rows.
+// Ring: A 2 slots x 32 KiB, S 2 slots (hi + lo) x 33 KiB.  A(d + 1) is issued in step 4 d + 1 behind
+// S(4 d + 2), so step 4 d + 2 waits for all but it and step 4 d + 3 for everything.
+template <int OFF>
+__device__ __forceinline__ i32x2 read64_o(uint32_t a) {
+    i32x2 v;
+    asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(v) : "v"(a), "i"(OFF));
+    return v;
+}
+
+template <bool SPLIT>
+__global__ __launch_bounds__(512) void wproj3tn4_kernel(const uint8_t* __restrict__ A, int64_t lda, int64_t rows_out,
+                                                        int64_t K, int64_t arows, const bf16_t* __restrict__ Shi,
+                                                        const bf16_t* __restrict__ Slo, float* __restrict__ out,
+                                                        int64_t slab_stride, int64_t kchunk, int nrowblk, int s_pitch,
+                                                        int o_pitch) {
+    constexpr int LP = 256;
+    typedef W3Shape<LP, false, SPLIT, 1> SH;
+    typedef typename SH::SImg SImg;
+    constexpr int WR = SH::WR, G = SH::G, WI = SH::WI, NS = SH::NS;
+    constexpr int ASLOT = WI * 128, APW2 = ASLOT / 1024 / 8;
+    constexpr int SBASE = 2 * ASLOT;
+    extern __shared__ __attribute__((aligned(1024))) char smem_raw[];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int r = lane & 15, h = lane >> 4, q = r >> 2, p = r & 3;
+    const int wr = w % WR, wc = w / WR;
+    const int bid = xcd_remap(blockIdx.x, gridDim.x);
+    const int rb = bid % nrowblk, sp = bid / nrowblk;
+    const int64_t row0 = (int64_t)rb * WI;
+    const int64_t kbeg = (int64_t)sp * kchunk;
+    const int64_t kend = (kbeg + kchunk < K) ? kbeg + kchunk : K;
+    const int nsteps = (int)((kend - kbeg + KS - 1) / KS);
+    const int nd = (nsteps + 3) / 4;
+
+    int32_t soff[SH::SPW];
+#pragma unroll
+    for (int t = 0; t < SH::SPW; ++t) {
+        constexpr int LPR = 64 / SImg::RP;
+        const int pc = t * 8 + w;
+        soff[t] = SImg::row_of(pc, lane / LPR) * s_pitch + 8 * (lane % LPR);
+    }
+    int64_t aoff[APW2];
+    int arow[APW2];
+#pragma unroll
+    for (int t = 0; t < APW2; ++t) {
+        const int u = (t * 8 + w) * 64 + lane, j = u >> 3, pu = u & 7;
+        int64_t jc = row0 + j;
+        jc = jc < rows_out ? jc : rows_out - 1;
+        const int i = 16 * (pu ^ ((j >> 1) & 7));
+        aoff[t] = jc * lda + i;
+        arow[t] = i;
+    }
+    auto issueS = [&](int st) {
+        char* slot = smem_raw + SBASE + (st & 1) * SH::SSLOT;
+        const int64_t k0 = kbeg + (int64_t)st * KS;
+#pragma unroll
+        for (int a = 0; a < NS; ++a) {
+            const bf16_t* S = (a ? Slo : Shi) + k0 * s_pitch;
+#pragma unroll
+            for (int t = 0; t < SH::SPW; ++t) glds16(S + soff[t], slot + a * SH::SIMG + (t * 8 + w) * SImg::PITCH);
+        }
+    };
+    auto issueA = [&](int d) {
+        char* slot = smem_raw + (d & 1) * ASLOT;
+        const int64_t k0 = kbeg + (int64_t)d * 4 * KS;
+        const bool tail = k0 + 4 * KS > arows;
+#pragma unroll
+        for (int t = 0; t < APW2; ++t) {
+            const uint8_t* src = A + k0 + aoff[t];
+            if (tail && k0 + arow[t] + 16 > arows) src = A + (arows - 16 - arow[t]) + aoff[t];
+            glds16(src, slot + (t * 8 + w) * 1024);
+        }
+    };
+
+    const int colS = wc * G * 16 + 4 * p;
+    const int k1 = 8 * h + q, k2 = k1 + 4;
+    const uint32_t lS1 = SImg::off(k1) + 2 * colS, lS2 = SImg::off(k2) + 2 * colS;
+    const int sw = (r >> 1) & 7;
+    uint32_t lA[4];
+#pragma unroll
+    for (int hs = 0; hs < 4; ++hs) lA[hs] = (wr * 64 + r) * 128 + 16 * ((2 * hs + (h >> 1)) ^ sw) + 8 * (h & 1);
+
+    f32x4 acc[RT][G];
+#pragma unroll
+    for (int t = 0; t < RT; ++t)
+#pragma unroll
+        for (int g = 0; g < G; ++g) acc[t][g] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    if (nsteps > 0) {
+        issueA(0);
+        issueS(0);
+    }
+    const uint32_t lds0 = lds_addr(smem_raw);
+    for (int st = 0; st < nsteps; ++st) {
+        const int d = st >> 2, hs = st & 3;
+        if (hs == 2 && d + 1 < nd) wait_vm<APW2>();
+        else wait_vm<0>();
+        __builtin_amdgcn_s_barrier();
+        if (st + 1 < nsteps) issueS(st + 1);
+        if (hs == 1 && d + 1 < nd) issueA(d + 1);
+        const uint32_t sS = lds0 + SBASE + (uint32_t)((st & 1) * SH::SSLOT);
+        const uint32_t sA = lds0 + (uint32_t)((d & 1) * ASLOT);
+        const uint32_t bS1 = sS + lS1, bS2 = sS + lS2;
+        const uint32_t bA = sA + (hs == 0 ? lA[0] : (hs == 1 ? lA[1] : (hs == 2 ? lA[2] : lA[3])));
+        auto wait_b = [&](i32x2* b) {
+            if (SPLIT) wait_lgkm0(b[0], b[1], b[2], b[3]);
+            else wait_lgkm0(b[0], b[1]);
+        };
+        i32x2 a2[RT];
+        bf16x8_t af[RT];
+        auto aread = [&](auto tc) {
+            constexpr int t = decltype(tc)::value;
+            a2[t] = read64_o<2048 * t>(bA);
+        };
+        static_for<RT>(aread);
+        auto bread = [&](auto gc, i32x2* b) {
+            constexpr int g = decltype(gc)::value;
+            b[0] = tr_read_o<32 * g>(bS1);
+            b[1] = tr_read_o<32 * g>(bS2);
+            if constexpr (SPLIT) {
+                b[2] = tr_read_o<SH::SIMG + 32 * g>(bS1);
+                b[3] = tr_read_o<SH::SIMG + 32 * g>(bS2);
+            }
+        };
+        i32x2 bb[2][4];
+        bread(std::integral_constant<int, 0>{}, bb[0]);
+        wait_b(bb[0]);
+#pragma unroll
+        for (int t = 0; t < RT; ++t) {
+            wait_lgkm0(a2[t]);
+            af[t] = fp8x8_to_bf16x8(a2[t]);
+        }
+        auto gstep = [&](auto gc) {
+            constexpr int g = decltype(gc)::value;
+            if constexpr (g + 1 < G) bread(std::integral_constant<int, g + 1>{}, bb[(g + 1) & 1]);
+            __builtin_amdgcn_sched_barrier(0);
+            const i32x2* b = bb[g & 1];
+            const bf16x8_t bh = join2(b[0], b[1]);
+#pragma unroll
+            for (int t = 0; t < RT; ++t) acc[t][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[t], bh, acc[t][g], 0, 0, 0);
+            if constexpr (SPLIT) {
+                const bf16x8_t bl = join2(b[2], b[3]);
+#pragma unroll
+                for (int t = 0; t < RT; ++t) acc[t][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[t], bl, acc[t][g], 0, 0, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (g + 1 < G) wait_b(bb[(g + 1) & 1]);
+        };
+        static_for<G>(gstep);
+    }
+
+    float* dst = out + (int64_t)sp * slab_stride;
+#pragma unroll
+    for (int t = 0; t < RT; ++t)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int64_t row = row0 + wr * 64 + 16 * t + 4 * h + j;
+            if (row < rows_out) {
+#pragma unroll
+                for (int g = 0; g < G; ++g) dst[row * o_pitch + wc * G * 16 + 16 * g + r] = acc[t][g][j];
+            }
+        }
+}
+
+// e4m3 TN through wproj3tn4_kernel: LP = 256 in one dispatch, LP = 512 as two 256-column halves
+// (S columns 256 hf .., pitch 512, into output columns 256 hf ..).
+template <bool SPLIT>
+hipError_t wproj3tn4_go(const void* A, int64_t lda, int64_t m, int64_t n, const bf16_t* Shi, const bf16_t* Slo, int LP,
+                        const WProjPlan& p, float* slabs, float* Out, hipStream_t s, hipEvent_t done) {
+    typedef W3Shape<256, false, SPLIT, 1> SH;
+    constexpr size_t lds = 2 * (size_t)SH::WI * 128 + 2 * (size_t)SH::SSLOT;
+    static_assert(lds <= 163840, "TN4 LDS");
+    const int64_t rows_out = n, K = m;
+    float* o = p.splits == 1 ? Out : slabs;
+    const int64_t stride = rows_out * LP;
+    for (int hf = 0; hf < LP / 256; ++hf) {
+        hipLaunchKernelGGL((wproj3tn4_kernel<SPLIT>), dim3(p.blocks * p.splits), dim3(512), lds, s,
+                           reinterpret_cast<const uint8_t*>(A), lda, rows_out, K, m, Shi + 256 * hf,
+                           Slo ? Slo + 256 * hf : nullptr, o + 256 * hf, stride, p.chunk, p.blocks, LP, LP);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    hipError_t e = hipSuccess;
+    if (done) e = hipEventRecord(done, s);
+    if (e != hipSuccess || p.splits == 1) return e;
+    return launch_sum_slabs<float>(slabs, stride, p.splits, stride, Out, s);
+}
+
 template <bool SPLIT>
 hipError_t wproj3tn2_go(const void* A, int64_t lda, int64_t m, int64_t n, const bf16_t* Shi, const bf16_t* Slo,
                         const WProjPlan& p, float* slabs, float* Out, hipStream_t s, hipEvent_t done) {
@@ -1211,10 +1462,10 @@ hipError_t wproj3tn2_go(const void* A, int64_t lda, int64_t m, int64_t n, const 
 }
 
 
-template <bool FP8, bool NN, int LP, bool SPLIT, bool DS = false, bool S8 = false>
+template <bool FP8, bool NN, int LP, bool SPLIT, bool DS = false, bool S8 = false, bool SC = false>
 hipError_t wproj2_go(const void* A, int64_t lda, int64_t m, int64_t n, const bf16_t* Shi, const bf16_t* Slo,
                      const WProjPlan& p, float* slabs, float* Out, hipStream_t s, hipEvent_t done) {
-    typedef W2Shape<LP, SPLIT, FP8, DS, S8> SH;
+    typedef W2Shape<LP, SPLIT, FP8, DS, S8, SC> SH;
     const int64_t rows_out = NN ? m : n, K = NN ? n : m;
     float* o = p.splits == 1 ? Out : slabs;
     const int64_t stride = rows_out * LP;
@@ -1223,8 +1474,8 @@ hipError_t wproj2_go(const void* A, int64_t lda, int64_t m, int64_t n, const bf1
     // each line for the next k-step (non-temporal: +4..13 %), so TN keeps the default policy
     // (profiles/r02_wide_lab_knobs.txt).
     constexpr int KN = NN ? 3 : 0;
-    hipLaunchKernelGGL((wproj2_kernel<FP8, NN, LP, SPLIT, DS, KN, S8>), dim3(p.blocks * p.splits), dim3(512), SH::LDS, s,
-                       A, lda, rows_out, K, m, Shi, Slo, o, stride, p.chunk, p.blocks, LP, LP);
+    hipLaunchKernelGGL((wproj2_kernel<FP8, NN, LP, SPLIT, DS, KN, S8, SC>), dim3(p.blocks * p.splits), dim3(512), SH::LDS,
+                       s, A, lda, rows_out, K, m, Shi, Slo, o, stride, p.chunk, p.blocks, LP, LP);
     hipError_t e = hipGetLastError();
     if (e == hipSuccess && done) e = hipEventRecord(done, s);
     if (e != hipSuccess || p.splits == 1) return e;
@@ -1237,10 +1488,10 @@ hipError_t wproj2_go(const void* A, int64_t lda, int64_t m, int64_t n, const bf1
 // halves before the next k-step used them: 4x A traffic from HBM).  Each half runs the LP = 256
 // tile (256 rows x 256 columns: S 2x A per k-step) on its 256 columns of S (pitch 512) into its
 // 256 columns of the output / slabs (pitch 512).  Same per-element arithmetic: bit-identical.
-template <bool FP8, bool NN, bool SPLIT, bool S8 = false>
+template <bool FP8, bool NN, bool SPLIT, bool S8 = false, bool SC = false>
 hipError_t wproj2_half_go(const void* A, int64_t lda, int64_t m, int64_t n, const bf16_t* Shi, const bf16_t* Slo,
                           const WProjPlan& p, float* slabs, float* Out, hipStream_t s, hipEvent_t done) {
-    typedef W2Shape<256, SPLIT, FP8, false, S8> SH;
+    typedef W2Shape<256, SPLIT, FP8, false, S8, SC> SH;
     const int64_t rows_out = NN ? m : n, K = NN ? n : m;
     float* o = p.splits == 1 ? Out : slabs;
     const int64_t stride = rows_out * 512;
@@ -1250,7 +1501,7 @@ hipError_t wproj2_half_go(const void* A, int64_t lda, int64_t m, int64_t n, cons
         const bf16_t* sh = S8 ? reinterpret_cast<const bf16_t*>(reinterpret_cast<const uint8_t*>(Shi) + 256 * hf)
                               : Shi + 256 * hf;
         const bf16_t* sl = Slo ? Slo + 256 * hf : nullptr;
-        hipLaunchKernelGGL((wproj2_kernel<FP8, NN, 256, SPLIT, false, KN, S8>), dim3(p.blocks * p.splits), dim3(512),
+        hipLaunchKernelGGL((wproj2_kernel<FP8, NN, 256, SPLIT, false, KN, S8, SC>), dim3(p.blocks * p.splits), dim3(512),
                            SH::LDS, s, A, lda, rows_out, K, m, sh, sl, o + 256 * hf, stride, p.chunk, p.blocks, 512, 512);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
@@ -1315,6 +1566,11 @@ hipError_t wproj_lp(int nn, int fp8, const void* A, int64_t lda, int64_t m, int6
 #undef GO3
         }
     }
+    if constexpr (LP == 256 || LP == 512) {
+        if (p.tn4 && fp8 && !nn)
+            return split ? wproj3tn4_go<true>(A, lda, m, n, Shi, Slo, LP, p, slabs, Out, s, d)
+                         : wproj3tn4_go<false>(A, lda, m, n, Shi, Slo, LP, p, slabs, Out, s, d);
+    }
     if constexpr (LP == 512) {
         if (p.v2 && p.half && fp8) {
             if (nn) return split ? wproj2_half_go<true, true, true>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d)
@@ -1357,6 +1613,14 @@ bool wproj_supported_lp(int LP) {
 
 int wproj_rows_per_block(int LP) { return LP <= 128 ? 256 : (LP == 256 ? 128 : 64); }
 
+static bool tn4_enabled() {  // RSVD_FP8_TN4=0 in the environment: the wproj2 e4m3 TN (A/B)
+    static const int env = [] {
+        const char* v = std::getenv("RSVD_FP8_TN4");
+        return v ? std::atoi(v) : 1;
+    }();
+    return env != 0;
+}
+
 WProjPlan plan_wproj(int64_t rows_out, int64_t K, int LP, bool v2, bool nn, bool fp8) {
     WProjPlan p;
     p.v2 = v2 && LP >= 128;
@@ -1364,6 +1628,8 @@ WProjPlan plan_wproj(int64_t rows_out, int64_t K, int LP, bool v2, bool nn, bool
     p.tn2 = p.v3 && !nn && LP == 256;  // two k-steps per A slot: K chunks of whole 64-row pairs
     p.ds = p.v2 && LP == 128 && !nn && !fp8 && K % 64 == 0;  // double-step TN stages (whole 64-row K chunks)
     p.half = p.v2 && fp8 && LP == 512;  // two LP = 256 column halves (wproj2_half_go)
+    // e4m3 TN: four k-steps per A slot (wproj3tn4_kernel; K chunks of whole 128-row slots)
+    p.tn4 = p.v2 && fp8 && !nn && (LP == 256 || LP == 512) && tn4_enabled();
     const int WI = p.v2 ? (LP == 128 ? (p.ds ? 256 : 512) : ((LP == 256 || p.half) ? 256 : 128))
                         : wproj_rows_per_block(LP);
     p.blocks = (int)((rows_out + WI - 1) / WI);
@@ -1374,7 +1640,7 @@ WProjPlan plan_wproj(int64_t rows_out, int64_t K, int LP, bool v2, bool nn, bool
     if (splits > 128) splits = 128;
     if (splits < 1) splits = 1;
     int64_t chunk = (K + splits - 1) / splits;
-    const int kq = (p.ds || p.tn2) ? 2 * KS : KS;
+    const int kq = p.tn4 ? 4 * KS : ((p.ds || p.tn2) ? 2 * KS : KS);
     chunk = (chunk + kq - 1) / kq * kq;
     p.chunk = chunk;
     p.splits = (int)((K + chunk - 1) / chunk);
@@ -1387,6 +1653,16 @@ hipError_t launch_wproj_s8(const void* A, int64_t lda, int64_t m, int64_t n, con
                            float* slabs, float* Out, hipStream_t s, hipEvent_t done) {
     if (!wproj_s8_supported(p, LP)) return hipErrorInvalidValue;
     const bf16_t* S = reinterpret_cast<const bf16_t*>(S8);
+    // the block-scaled K = 128 form when every stage is whole (RSVD_FP8_SCALED=0: the K = 32 form)
+    static const int env = [] {
+        const char* v = std::getenv("RSVD_FP8_SCALED");
+        return v ? std::atoi(v) : 1;
+    }();
+    const bool sc = env != 0 && n % 128 == 0 && p.chunk % 128 == 0;
+    if (sc) {
+        if (LP == 256) return wproj2_go<true, true, 256, false, false, true, true>(A, lda, m, n, S, nullptr, p, slabs, Out, s, done);
+        if (p.half) return wproj2_half_go<true, true, false, true, true>(A, lda, m, n, S, nullptr, p, slabs, Out, s, done);
+    }
     if (LP == 256) return wproj2_go<true, true, 256, false, false, true>(A, lda, m, n, S, nullptr, p, slabs, Out, s, done);
     if (p.half) return wproj2_half_go<true, true, false, true>(A, lda, m, n, S, nullptr, p, slabs, Out, s, done);
     return wproj2_go<true, true, 512, false, false, true>(A, lda, m, n, S, nullptr, p, slabs, Out, s, done);

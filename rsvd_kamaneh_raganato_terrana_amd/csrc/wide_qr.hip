@@ -18,6 +18,7 @@
 #include <utility>
 
 #include "common.hpp"
+#include "dense.hpp"
 #include "kernels.hpp"
 #include "wide.hpp"
 
@@ -265,6 +266,194 @@ __global__ __launch_bounds__(512) void gram_sym_kernel(const T* __restrict__ P, 
     gram_sym_dispatch<T, LP>(w * G::NH + hb, P, beg, end, chunk, slabs, tile, std::make_integer_sequence<int, G::NW>{});
 }
 
+// ------------------------------------------------------------------------------------------------
+// Split Gram of an fp32 panel on the bf16 MFMA.  Every fp32 value is EXACTLY h + m + t with
+// h = bf16(v), m = bf16(v - h), t = bf16(v - h - m) (8 + 8 + 8 significant bits), and the six
+// products hh, hm, mh, mm, ht, th carry P_ki P_kj to ~2^-24 of |P_ki P_kj| (the dropped mt, tm,
+// tt are below it).  Each bf16 product is exact in fp32; one v_mfma_f32_16x16x32_bf16 sums 32 rows
+// of them in fp32 and that partial is added to an fp64 accumulator after every 32-row step, so
+// the rounding does not grow with the panel height: measured on a cond 1e3 panel (numpy model of
+// the same arithmetic, 65536 x 256) |G_split - G|_F / |G|_F = 8e-9, max |dG_ij| / sqrt(G_ii G_jj)
+// = 3e-8.  Six bf16 MFMAs at 32x the fp64 MFMA rate: the Gram becomes an HBM read of the panel
+// (C4 65536 x 256: ~100 -> ~20 us).  It is only used where its accuracy is enough -- CholeskyQR of
+// the fp32 panels of bf16 / e4m3 A, with the factor's pivots checked against kSplitIllTol
+// (launch_chol_wide, `ill`) and the fp64 Gram + factor re-run (predicated) when one is below it.
+// Layout: a 32-row step is staged as three [LP column][32 row] bf16 images (64-B columns, 16-B
+// unit u of column c at u ^ ((c >> 1) & 3): the 16-lane ds_read_b128 of one tile is conflict-free);
+// lane (r, h) of tile t reads rows 8h .. 8h + 7 of column 16t + r -- the A and the B fragment of
+// v_mfma_f32_16x16x32_bf16 alike (G = P^T P: both operands are "column, rows k" reads).
+// Upper tile pairs (ta <= tb) are dealt to the NH x 8 waves of a chunk at compile time; the
+// partial tiles go to gram_sym's (chunk, 32x32 block) slab layout, summed by gram_reduce_kernel.
+typedef __attribute__((ext_vector_type(8))) short bf16x8s;
+
+template <int LP> struct GramSplit {
+    static constexpr int NH = LP == 512 ? 8 : (LP == 256 ? 2 : 1);  // workgroups per chunk (as GramSym)
+    static constexpr int LNH = LP == 512 ? 3 : (LP == 256 ? 1 : 0);
+    static constexpr int NT = LP / 16, NP = NT * (NT + 1) / 2, NW = 8 * NH, PPW = (NP + NW - 1) / NW;
+    static constexpr int NB = LP / 32, NBLK = NB * (NB + 1) / 2;
+    static constexpr int IMG = LP * 64;                // bytes of one piece image (LP columns x 32 rows bf16)
+    static constexpr int STEP = 3 * IMG;               // the three pieces of a 32-row step
+    static constexpr int NBUF = STEP * 2 <= 98304 ? 2 : 1;
+    static constexpr int NU = 2 * LP;                  // 4-row x 4-column units of a 32-row step
+    static constexpr int LPT = (NU + 511) / 512;       // ... per thread
+};
+
+__device__ __forceinline__ uint32_t f2bf_bits(float x) {  // round to nearest even (finite x)
+    const uint32_t u = __float_as_uint(x);
+    return (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
+}
+
+template <int LP, int WG, int... I>
+__device__ __forceinline__ void gram_split_mma(const char* img, int r, int h, f32x4 (&acc)[GramSplit<LP>::PPW],
+                                               std::integer_sequence<int, I...>) {
+    typedef GramSplit<LP> G;
+    const uint32_t lo = (uint32_t)(r * 64 + 16 * (h ^ ((r >> 1) & 3)));
+    auto frag = [&](int piece, int t) {
+        return *reinterpret_cast<const bf16x8s*>(img + piece * G::IMG + t * 1024 + lo);
+    };
+    auto one = [&](auto ic) {
+        constexpr int i = decltype(ic)::value, p = WG + G::NW * i;
+        if constexpr (p < G::NP) {
+            constexpr int a = PairOf<G::NT, p>::a, b = PairOf<G::NT, p>::b;
+            const bf16x8s ha = frag(0, a), ma = frag(1, a), ta = frag(2, a);
+            const bf16x8s hb = frag(0, b), mb = frag(1, b), tb = frag(2, b);
+            f32x4 c = acc[i];
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ta, hb, c, 0, 0, 0);  // smallest terms first
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ha, tb, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ma, mb, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ma, hb, c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ha, mb, c, 0, 0, 0);
+            acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ha, hb, c, 0, 0, 0);
+        }
+    };
+    (one(std::integral_constant<int, I>{}), ...);
+}
+
+template <int LP, int WG>
+__device__ __forceinline__ void gram_split_body(const float* __restrict__ P, int64_t beg, int64_t end, int chunk,
+                                                double* __restrict__ slabs, char* smem) {
+    typedef GramSplit<LP> G;
+    constexpr int PPW = G::PPW, LPT = G::LPT;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int r = lane & 15, h = lane >> 4;
+    f32x4 acc[PPW];
+    double acc64[PPW][4];
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+        acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc64[i][j] = 0.0;
+    }
+    // thread unit u = tid + 512 t (u < NU): rows kr = 4 (u & 7) .. + 3 of columns 4 (u >> 3) .. + 3
+    // (the 8 lanes of an octet fill one column's 64 B; for a fixed row the octets read 128 B runs)
+    float4 reg[LPT][4];
+    auto load = [&](int64_t r0) {
+#pragma unroll
+        for (int t = 0; t < LPT; ++t) {
+            const int u = tid + 512 * t;
+            const int64_t row = r0 + 4 * (u & 7);
+            const int c = 4 * (u >> 3);
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                reg[t][q] = (u < G::NU && row + q < end) ? *reinterpret_cast<const float4*>(P + (row + q) * LP + c)
+                                                         : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
+    auto stage = [&](char* img) {
+#pragma unroll
+        for (int t = 0; t < LPT; ++t) {
+            const int u = tid + 512 * t;
+            if (u >= G::NU) break;
+            const int kr = 4 * (u & 7);  // first of the 4 rows (0..28)
+            const int c0 = 4 * (u >> 3);
+            const int rot = (u >> 3) & 3;  // octets write columns of alternating parity (LDS banks)
+#pragma unroll
+            for (int i0 = 0; i0 < 4; ++i0) {
+                const int i = (i0 + rot) & 3;
+                const int c = c0 + i;
+                uint32_t pw[3][2];
+#pragma unroll
+                for (int q = 0; q < 4; q += 2) {
+                    uint32_t bits[2][3];
+#pragma unroll
+                    for (int e = 0; e < 2; ++e) {
+                        const float4 f = reg[t][q + e];
+                        const float v = i == 0 ? f.x : (i == 1 ? f.y : (i == 2 ? f.z : f.w));
+                        const uint32_t bh = f2bf_bits(v);
+                        const float rm = v - __uint_as_float(bh << 16);
+                        const uint32_t bm = f2bf_bits(rm);
+                        const float rt = rm - __uint_as_float(bm << 16);
+                        bits[e][0] = bh;
+                        bits[e][1] = bm;
+                        bits[e][2] = f2bf_bits(rt);
+                    }
+#pragma unroll
+                    for (int x = 0; x < 3; ++x) pw[x][q >> 1] = bits[0][x] | (bits[1][x] << 16);
+                }
+                // rows kr .. kr + 3 of column c: 8 B inside 16-B unit kr >> 3 (swizzled), offset 8 ((kr >> 2) & 1)
+                const int off = c * 64 + 16 * ((kr >> 3) ^ ((c >> 1) & 3)) + 8 * ((kr >> 2) & 1);
+#pragma unroll
+                for (int x = 0; x < 3; ++x)
+                    *reinterpret_cast<uint2*>(img + x * G::IMG + off) = make_uint2(pw[x][0], pw[x][1]);
+            }
+        }
+    };
+    int buf = 0;
+    if (beg < end) load(beg);
+    for (int64_t r0 = beg; r0 < end; r0 += 32) {
+        char* img = smem + buf * G::STEP;
+        if (G::NBUF == 1) __syncthreads();  // single buffer: the previous step's reads are done
+        stage(img);
+        __syncthreads();
+        if (r0 + 32 < end) load(r0 + 32);
+        gram_split_mma<LP, WG>(img, r, h, acc, std::make_integer_sequence<int, PPW>{});
+#pragma unroll
+        for (int i = 0; i < PPW; ++i) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc64[i][j] += (double)acc[i][j];
+            acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+        buf = G::NBUF - 1 - buf;
+    }
+#pragma unroll
+    for (int i = 0; i < PPW; ++i) {
+        const int p = WG + G::NW * i;
+        if (p < G::NP) {
+            const int ta = pair_ta(G::NT, p), tb = pair_tb(G::NT, p);
+            const int a = ta >> 1, b = tb >> 1;
+            const int blk = a * G::NB - a * (a - 1) / 2 + (b - a);
+            double* dst = slabs + ((int64_t)chunk * G::NBLK + blk) * 1024;
+            const bool mirror = (a == b) && (ta != tb);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {  // bf16 MFMA D: col = lane & 15, row = 4 h + j
+                const int li = 16 * (ta & 1) + 4 * h + j, lj = 16 * (tb & 1) + r;
+                dst[li * 32 + lj] = acc64[i][j];
+                if (mirror) dst[lj * 32 + li] = acc64[i][j];
+            }
+        }
+    }
+}
+
+template <int LP, int... W>
+__device__ __forceinline__ void gram_split_dispatch(int wg, const float* P, int64_t beg, int64_t end, int chunk,
+                                                    double* slabs, char* smem, std::integer_sequence<int, W...>) {
+    ((wg == W ? gram_split_body<LP, W>(P, beg, end, chunk, slabs, smem) : void()), ...);
+}
+
+template <int LP>
+__global__ __launch_bounds__(512) void gram_split_kernel(const float* __restrict__ P, int64_t rows, int64_t rpc,
+                                                         int nchunk, double* __restrict__ slabs) {
+    typedef GramSplit<LP> G;
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int hb = G::NH == 1 ? 0 : (blockIdx.x >> 3) & (G::NH - 1);
+    const int chunk = G::NH == 1 ? blockIdx.x : ((blockIdx.x & 7) | ((blockIdx.x >> (3 + G::LNH)) << 3));
+    if (chunk >= nchunk) return;
+    const int64_t beg = (int64_t)chunk * rpc;
+    const int64_t end = (beg + rpc < rows) ? beg + rpc : rows;
+    gram_split_dispatch<LP>(w * G::NH + hb, P, beg, end, chunk, slabs, smem_raw, std::make_integer_sequence<int, G::NW>{});
+}
+
 __global__ void gram_reduce_kernel(const double* __restrict__ slabs, int nblk, int nchunk, int LP, int cross,
                                    double* __restrict__ G, const int* __restrict__ pred) {
     if (pred && *pred == 0) return;
@@ -354,9 +543,9 @@ __device__ __forceinline__ double rsqrt_nr(double d) {
 // blocks (global), D^-1 (Di, LDS, row-major), the breakdown rows (bad) and flags.
 __device__ __forceinline__ void chol_diag16_fast(double (&col)[16], int p16, int l, int LP, double tol,
                                                  const double* d0, double* Di, int* bad, double* R, double* Rinv,
-                                                 int* colflag, int* flag, int lane) {
+                                                 int* colflag, int* flag, int lane, double ill_tol, int* ill_s) {
     const int j = lane & 15;
-    int badmask = 0;
+    int badmask = 0, illm = 0;
     double acc[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[i] = 0.0;
@@ -367,6 +556,7 @@ __device__ __forceinline__ void chol_diag16_fast(double (&col)[16], int p16, int
         const bool pad = gk >= l;
         const bool isbad = !pad && (!(dkk > tol * d0[gk]) || !(d0[gk] > 0.0) || !isfinite(dkk));
         if (isbad) badmask |= 1 << k;
+        if (!pad && !(dkk > ill_tol * d0[gk])) illm = 1;  // (wave-uniform) a pivot too small for the split Gram
         const bool unit = pad || isbad;
         const double y = unit ? 1.0 : rsqrt_nr(dkk);
         const double rk = unit ? 1.0 : dkk * y;
@@ -397,6 +587,7 @@ __device__ __forceinline__ void chol_diag16_fast(double (&col)[16], int p16, int
             *reinterpret_cast<double2*>(Rinv + (int64_t)(p16 + j) * LP + p16 + i) =
                 *reinterpret_cast<const double2*>(Di + j * 16 + i);
     }
+    if (lane == 0 && illm) *ill_s = 1;
     if (lane == 0 && badmask) {
         atomicAdd(flag, __popc(badmask));
         for (int k = 0; k < 16; ++k)
@@ -444,9 +635,11 @@ __global__ __launch_bounds__(NT) void chol_wide_kernel(const double* __restrict_
                                                                  double tol, double* __restrict__ W,
                                                                  double* __restrict__ R, double* __restrict__ Rinv,
                                                                  int* __restrict__ colflag, int* __restrict__ flag,
-                                                                 const int* __restrict__ pred) {
+                                                                 const int* __restrict__ pred, double ill_tol,
+                                                                 int* __restrict__ ill, const double* __restrict__ d0src) {
     if (pred && *pred == 0) return;
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    __shared__ int ill_s;
     const int np = LP / 16;
     const int ldr = LP + kCholPad;
     constexpr int nw = NT / 64;
@@ -489,9 +682,10 @@ __global__ __launch_bounds__(NT) void chol_wide_kernel(const double* __restrict_
         }
     }
     for (int i = tid; i < LP; i += NT) {
-        d0[i] = (i < l) ? G[(int64_t)i * LP + i] : 0.0;
+        d0[i] = (i < l) ? (d0src ? d0src[i] : G[(int64_t)i * LP + i]) : 0.0;
         colflag[i] = 0;
     }
+    if (tid == 0) ill_s = 0;
     __syncthreads();
     CHOL_TS(0);
 
@@ -568,7 +762,7 @@ __global__ __launch_bounds__(NT) void chol_wide_kernel(const double* __restrict_
                 __builtin_amdgcn_s_waitcnt(0xc07f);
                 __builtin_amdgcn_wave_barrier();
                 chol_diag16_fast(col, 16 * b1, l, LP, tol, d0, Dd + (b1 & 1) * 256, bad + (b1 & 1) * 16, R, Rinv,
-                                 colflag, flag, lane);
+                                 colflag, flag, lane, ill_tol, &ill_s);
             } else if (p >= 0) {
                 // local tile t of the (nt2 x nt2) upper triangle; t = 0 is wave 0's
                 TriWalk tw(wv, nt2);
@@ -615,6 +809,7 @@ __global__ __launch_bounds__(NT) void chol_wide_kernel(const double* __restrict_
         __syncthreads();
         if (p >= 0) CHOL_TS(2 + 2 * p);
     }
+    if (ill && tid == 0) *ill = ill_s;
 }
 
 size_t chol_lds_bytes(int LP) {
@@ -650,9 +845,11 @@ template <int NP>
 __global__ __launch_bounds__(64 * kCholRegWaves) void chol_reg_kernel(const double* __restrict__ G, int l, double tol,
                                                                       double* __restrict__ R, double* __restrict__ Rinv,
                                                                       int* __restrict__ colflag, int* __restrict__ flag,
-                                                                      const int* __restrict__ pred) {
+                                                                      const int* __restrict__ pred, double ill_tol,
+                                                                      int* __restrict__ ill, const double* __restrict__ d0src) {
     if (pred && *pred == 0) return;
     typedef CholReg<NP> C;
+    __shared__ int ill_s;
     constexpr int LP = C::LP, NW = C::NW, NT = C::NT, S = C::S, SL = C::SL, LDR = C::LDR;
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
     double* Di = reinterpret_cast<double*>(smem_raw);  // [2][256]
@@ -700,9 +897,10 @@ __global__ __launch_bounds__(64 * kCholRegWaves) void chol_reg_kernel(const doub
         }
     };
     for (int i = tid; i < LP; i += 64 * NW) {
-        d0[i] = (i < l) ? G[(int64_t)i * LP + i] : 0.0;
+        d0[i] = (i < l) ? (d0src ? d0src[i] : G[(int64_t)i * LP + i]) : 0.0;
         colflag[i] = 0;
     }
+    if (tid == 0) ill_s = 0;
     __syncthreads();
     CHOL_TS(200);
 
@@ -728,11 +926,14 @@ __global__ __launch_bounds__(64 * kCholRegWaves) void chol_reg_kernel(const doub
             __builtin_amdgcn_s_waitcnt(0xc07f);
             __builtin_amdgcn_wave_barrier();
             chol_diag16_fast(col, p16, l, LP, tol, d0, Di + (p & 1) * 256, bad + (p & 1) * 16, R, Rinv,
-                            colflag, flag, lane);
+                            colflag, flag, lane, ill_tol, &ill_s);
         }
         __syncthreads();
         if (p < 32) CHOL_TS(1 + 3 * p);
-        if (p == NP - 1) break;
+        if (p == NP - 1) {
+            if (ill && tid == 0) *ill = ill_s;
+            break;
+        }
         // (B) strip R[p][jb] = D_p^-T W[p][jb] (0 for rows that broke down or are padding)
         {
             const double* Dp = Di + (p & 1) * 256;
@@ -1174,31 +1375,141 @@ hipError_t launch_gram_wide(const T* P, const T* P2, int64_t rows, int LP, const
     return hipGetLastError();
 }
 
+bool gram_split_ok(int LP) { return LP == 128 || LP == 256 || LP == 512; }
+
+hipError_t launch_gram_split(const float* P, int64_t rows, int LP, const GramPlan& gp, double* slabs, double* G,
+                             hipStream_t s) {
+    if (!gram_split_ok(LP)) return hipErrorInvalidValue;
+    const int grid = LP == 128 ? gp.chunks : (gp.chunks + 7) / 8 * 8 * (LP == 256 ? 2 : 8);
+    if (LP == 128)
+        hipLaunchKernelGGL(gram_split_kernel<128>, dim3(grid), dim3(512),
+                           GramSplit<128>::NBUF * GramSplit<128>::STEP, s, P, rows, gp.rows_per_chunk, gp.chunks, slabs);
+    else if (LP == 256)
+        hipLaunchKernelGGL(gram_split_kernel<256>, dim3(grid), dim3(512),
+                           GramSplit<256>::NBUF * GramSplit<256>::STEP, s, P, rows, gp.rows_per_chunk, gp.chunks, slabs);
+    else
+        hipLaunchKernelGGL(gram_split_kernel<512>, dim3(grid), dim3(512),
+                           GramSplit<512>::NBUF * GramSplit<512>::STEP, s, P, rows, gp.rows_per_chunk, gp.chunks, slabs);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const int64_t tot = (int64_t)gp.blocks * 1024;
+    hipLaunchKernelGGL(gram_reduce_kernel, dim3((int)((tot + 255) / 256)), dim3(256), 0, s, slabs, gp.blocks,
+                       gp.chunks, LP, 0, G, (const int*)nullptr);
+    return hipGetLastError();
+}
+
 int chol_variant = 1;
 
 hipError_t launch_chol_wide(const double* G, int l, int LP, double tol, double* R, double* Rinv, float* Rinv32,
-                            int* colflag, int* flag, double* work, const int* pred, hipStream_t s) {
+                            int* colflag, int* flag, double* work, const int* pred, hipStream_t s, double ill_tol,
+                            int* ill, const double* d0src) {
     if (LP % 16 || LP > 512) return hipErrorInvalidValue;
     // LP = 256: chol_wide_kernel (its wave-0 look-ahead overlaps the diagonal factor with the other waves'
     // updates; the register-resident kernel spills there, 174 vs 161 us measured); LP <= 128: chol_reg_kernel
     // (LP = 128: 63 vs 71 us, LP = 64: 31 vs 37 us, tools/wide_lab chol)
     if (chol_variant >= 1 && LP == 128)
         hipLaunchKernelGGL(chol_reg_kernel<8>, dim3(1), dim3(64 * kCholRegWaves), CholReg<8>::lds_bytes, s, G, l, tol,
-                           R, Rinv, colflag, flag, pred);
+                           R, Rinv, colflag, flag, pred, ill_tol, ill, d0src);
     else if (chol_variant >= 1 && LP == 64)
         hipLaunchKernelGGL(chol_reg_kernel<4>, dim3(1), dim3(64 * kCholRegWaves), CholReg<4>::lds_bytes, s, G, l, tol,
-                           R, Rinv, colflag, flag, pred);
+                           R, Rinv, colflag, flag, pred, ill_tol, ill, d0src);
     else if (chol_variant == 2 && LP == 256)  // lab only
         hipLaunchKernelGGL(chol_reg_kernel<16>, dim3(1), dim3(64 * kCholRegWaves), CholReg<16>::lds_bytes, s, G, l,
-                           tol, R, Rinv, colflag, flag, pred);
+                           tol, R, Rinv, colflag, flag, pred, ill_tol, ill, d0src);
     else
         hipLaunchKernelGGL((chol_wide_kernel<kCholThreads, kCholBatch>), dim3(1), dim3(kCholThreads), chol_lds_bytes(LP),
-                           s, G, l, LP, tol, work, R, Rinv, colflag, flag, pred);
+                           s, G, l, LP, tol, work, R, Rinv, colflag, flag, pred, ill_tol, ill, d0src);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(rinv_wide_kernel, dim3(LP / 16), dim3(256), 0, s, LP, R, Rinv, Rinv32, pred);
     return hipGetLastError();
 }
+
+// ---- two-level LP = 512 factor (launch_chol_wide_2level) ----------------------------------------
+// Ga = G11, Sb = G22 (256 x 256, ld 256), d0b = diag(G22): the breakdown / ill tests of the second
+// level judge S's pivots against G's own diagonal, as the one-level factor does
+__global__ void chol2_prep_kernel(const double* __restrict__ G, double* __restrict__ Ga, double* __restrict__ Sb,
+                                  double* __restrict__ d0b) {
+    const int i = blockIdx.x, c = threadIdx.x;  // 256 x 256
+    Ga[i * 256 + c] = G[(int64_t)i * 512 + c];
+    Sb[i * 256 + c] = G[(int64_t)(256 + i) * 512 + 256 + c];
+    if (c == 0) d0b[i] = G[(int64_t)(256 + i) * 512 + 256 + i];
+}
+// rows of R12 (row-major, ld 512) whose first-level pivot broke down are zero, as the one-level
+// factor's strips are
+__global__ void chol2_zero_rows_kernel(double* __restrict__ R12, const int* __restrict__ colflag) {
+    const int i = blockIdx.x, c = threadIdx.x;
+    if (colflag[i]) R12[(int64_t)i * 512 + c] = 0.0;
+}
+// R / Rinv (512 x 512 row-major) from the level blocks; Rinv32 the fp32 copy; ill = ill1 | ill2
+__global__ void chol2_assemble_kernel(const double* __restrict__ R11, const double* __restrict__ Ri11,
+                                      const double* __restrict__ R22, const double* __restrict__ Ri22,
+                                      double* __restrict__ R, double* __restrict__ Rinv, float* __restrict__ Rinv32,
+                                      const int* __restrict__ ill2, int* __restrict__ ill) {
+    const int i = blockIdx.x, c = threadIdx.x;  // 512 x 256: columns c and c + 256 of row i
+    const int64_t o = (int64_t)i * 512;
+    if (i < 256) {
+        R[o + c] = R11[i * 256 + c];
+        Rinv[o + c] = Ri11[i * 256 + c];
+        if (Rinv32) {
+            Rinv32[o + c] = (float)Ri11[i * 256 + c];
+            Rinv32[o + 256 + c] = (float)Rinv[o + 256 + c];
+        }
+    } else {
+        const int i2 = i - 256;
+        R[o + c] = 0.0;
+        Rinv[o + c] = 0.0;
+        R[o + 256 + c] = R22[i2 * 256 + c];
+        Rinv[o + 256 + c] = Ri22[i2 * 256 + c];
+        if (Rinv32) {
+            Rinv32[o + c] = 0.f;
+            Rinv32[o + 256 + c] = (float)Ri22[i2 * 256 + c];
+        }
+    }
+    if (ill && i == 0 && c == 0 && *ill2) *ill = 1;
+}
+
+// row-major C (M x N, ldc) = alpha op(A) op(B) + beta C through the column-major GEMM (C^T = op(B)^T op(A)^T)
+static hipError_t gemm_rm(int ta, int tb, int M, int N, int K, double alpha, const double* A, int lda,
+                          const double* B, int ldb, double beta, double* C, int ldc, hipStream_t s) {
+    return launch_gemm<double>(tb, ta, N, M, K, alpha, B, ldb, A, lda, beta, C, ldc, s);
+}
+
+hipError_t launch_chol_wide_2level(const double* G, int l, double tol, double* R, double* Rinv, float* Rinv32,
+                                   int* colflag, int* flag, double* work, double* scratch, hipStream_t s,
+                                   double ill_tol, int* ill) {
+    if (l <= 256 || l > 512) return hipErrorInvalidValue;
+    constexpr int B = 256, B2 = B * B;
+    double *Ga = scratch, *R11 = Ga + B2, *Ri11 = R11 + B2, *Sb = Ri11 + B2, *R22 = Sb + B2, *Ri22 = R22 + B2,
+           *T = Ri22 + B2, *d0b = T + B2;
+    int* ill2 = reinterpret_cast<int*>(d0b + 256);
+    hipLaunchKernelGGL(chol2_prep_kernel, dim3(B), dim3(B), 0, s, G, Ga, Sb, d0b);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    // level 1: R11, Ri11 = chol(G11) (columns 0 .. 255 of colflag)
+    e = launch_chol_wide(Ga, B, B, tol, R11, Ri11, nullptr, colflag, flag, work, nullptr, s, ill_tol, ill);
+    if (e != hipSuccess) return e;
+    // R12 = Ri11^T G12 -> R[:256, 256:] (ld 512), broken-down rows zeroed
+    e = gemm_rm(1, 0, B, B, B, 1.0, Ri11, B, G + B, 512, 0.0, R + B, 512, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(chol2_zero_rows_kernel, dim3(B), dim3(B), 0, s, R + B, colflag);
+    // S = G22 - R12^T R12
+    e = gemm_rm(1, 0, B, B, B, -1.0, R + B, 512, R + B, 512, 1.0, Sb, B, s);
+    if (e != hipSuccess) return e;
+    // level 2 on the l - 256 valid columns of S, tested against diag(G22)
+    e = launch_chol_wide(Sb, l - B, B, tol, R22, Ri22, nullptr, colflag + B, flag, work, nullptr, s, ill_tol,
+                         ill ? ill2 : nullptr, d0b);
+    if (e != hipSuccess) return e;
+    // Rinv12 = -Ri11 (R12 Ri22) -> Rinv[:256, 256:]
+    e = gemm_rm(0, 0, B, B, B, 1.0, R + B, 512, Ri22, B, 0.0, T, B, s);
+    if (e != hipSuccess) return e;
+    e = gemm_rm(0, 0, B, B, B, -1.0, Ri11, B, T, B, 0.0, Rinv + B, 512, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(chol2_assemble_kernel, dim3(512), dim3(B), 0, s, R11, Ri11, R22, Ri22, R, Rinv, Rinv32,
+                       ill2, ill);
+    return hipGetLastError();
+}
+
 
 template <typename T>
 hipError_t launch_panel_gemm(const T* In, int64_t rows, int LP, const T* Mm, int upper, T* Out, int64_t ldo,

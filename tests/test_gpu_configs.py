@@ -140,3 +140,21 @@ def test_lowp_intermediates_flag(engine):
     _check(U, S, V, Uo, So, Vo, A_exact, 1e-4, 1e-3)
     U2, S2, V2 = engine.rsvd(Ad, l, q=2, seed=99)
     assert rel_fro(S, S2.cpu().double().numpy()) < 1e-4
+
+
+@pytest.mark.parametrize("decay,l", [(0.995, 128), (0.9, 128), (0.97, 256), (0.985, 512)])
+def test_split_gram_paths(engine, decay, l):
+    """The split Gram (wide_qr.hip gram_split_kernel, bf16 / e4m3 A): its factor is kept while every
+    pivot stays above kSplitIllTol of its diagonal (0.995^i: cond(Y) ~ 2 at l = 128), and the fp64
+    Gram + factor re-run (predicated) past it (0.9^i over 2 l columns: sigma_l / sigma_1 ~ 1e-6;
+    0.97^i at l = 256; 0.985^i at l = 512) -- both must meet the 1e-4 bar against the oracle."""
+    torch = _torch()
+    m, n = 4096, 2048
+    A32 = gapped_matrix(m, n, 2 * l, decay=decay, seed=l + 7).astype(np.float32) * 4
+    Ad = _dev_colmajor(A32, torch.bfloat16)
+    A_exact = Ad.float().cpu().double().numpy()
+    Om = engine.generate_omega(n, l, seed=5, dtype=torch.bfloat16).cpu().double().numpy()
+    Uo, So, Vo = oracle.rsvd(A_exact, l, q=2, Omega=Om)
+    U, S, V = engine.rsvd(Ad, l, q=2, seed=5)
+    U, S, V = (x.cpu().double().numpy() for x in (U, S, V))
+    _check(U, S, V, Uo, So, Vo, A_exact, 1e-4, 1e-3)

@@ -143,15 +143,19 @@ def test_fp8_decode_all_codes(engine):
     assert float(S[1]) < 1e-4 * ref
 
 
-def test_wide_rank_deficient_is_orthonormal(engine):
-    """rank(A) = 6 < l = 128: breakdown columns are completed (repair pass), U and V stay
-    orthonormal and A is reconstructed exactly, as the reference's Householder Q would."""
+@pytest.mark.parametrize("l,rank", [(128, 6), (512, 6), (512, 300), (300, 280)])
+def test_wide_rank_deficient_is_orthonormal(engine, l, rank):
+    """rank(A) < l: breakdown columns are completed (repair pass), U and V stay orthonormal and A
+    is reconstructed exactly, as the reference's Householder Q would.  l = 512 runs the two-level
+    LP = 512 factor (wide_qr.hip launch_chol_wide_2level) with breakdowns in its first level
+    (rank 6) and only in its second (rank 300)."""
     torch = _torch()
     rng = np.random.default_rng(4)
-    m, n, l = 1200, 800, 128
-    # small-integer factors: every entry of A is an integer <= 24 in magnitude, exact in bf16,
-    # so the bf16 matrix the GPU sees has rank exactly 6
-    A = (rng.integers(-2, 3, (m, 6)) @ rng.integers(-2, 3, (6, n))).astype(np.float32)
+    m, n = 1200, 800
+    # small-integer factors: every entry of A is an integer <= 4 rank in magnitude, exact in bf16
+    # (up to 256), so the bf16 matrix the GPU sees has exactly the chosen rank
+    A = (rng.integers(-1, 2, (m, rank)) @ rng.integers(-1, 2, (rank, n))).astype(np.float32)
+    assert np.abs(A).max() <= 256
     U, S, V = engine.rsvd(_dev_colmajor(A, torch.bfloat16), l, q=1, seed=9)
     torch.cuda.synchronize()
     U, S, V = (x.cpu().double().numpy() for x in (U, S, V))
@@ -159,7 +163,7 @@ def test_wide_rank_deficient_is_orthonormal(engine):
     assert np.linalg.norm(V.T @ V - np.eye(l)) < 1e-3
     Ab = _dev_colmajor(A, torch.bfloat16).float().cpu().double().numpy()
     assert np.linalg.norm(Ab - (U * S) @ V.T) < 1e-4 * np.linalg.norm(Ab)
-    assert np.all(S[6:] < 1e-4 * S[0])
+    assert np.all(S[rank:] < 1e-4 * S[0])
 
 
 def test_wide_range_finder_subspace(engine):
