@@ -153,7 +153,7 @@ int rsvd_set_comm(rsvd_handle_t h, int rank, int world, rsvd_allreduce_fn fn, vo
  * each rank orthonormalises its rows (CholeskyQR with the l x l Gram all-reduced), the next
  * skinny operand and the final V are all-gathered.  fn = NULL switches back to the replicated
  * n side.  SVDMethod::Power runs keep the replicated n side.  rsvd_workspace_bytes covers the
- * padded n-side panels of any world up to 64. */
+ * padded n-side panels of any world up to 64; past 64 ranks the n side stays replicated. */
 int rsvd_set_collectives(rsvd_handle_t h, rsvd_collective_fn fn, void *user);
 
 /* Library-owned RCCL (ABI 6): the handle creates and owns an RCCL communicator over the ranks'
@@ -200,7 +200,10 @@ int rsvd_set_workspace(rsvd_handle_t h, void *ptr, size_t bytes);
  * rows of an n x n V_ -- include/SVD_class.hpp rebuilds that layout); triplets past an early stop
  * (sigma < 1e-12) are zero and rsvd_get_info reports how many were kept.  omega: optional n x l column-major (ld = ldo) sketch in that element
  * type (rounded to bf16 / e4m3 for the low-precision types); NULL => Philox(desc->seed).
- * l <= 512. */
+ * l <= 512 on the wide engine; 512 < l <= 4096 (the reference has no cap, src/rSVD.cpp:72) on one GPU
+ * through dense_big.cpp's column-major blocks (MFMA GEMM products, block CGS2 + CholeskyQR3, the
+ * block Jacobi small SVD; bf16 / e4m3 A widened to fp32 once), methods Jacobi / ParallelJacobi
+ * (RSVD_ERR_UNSUPPORTED for Power, for row-sharded handles and past 4096). */
 int rsvd_run(rsvd_handle_t h, const rsvd_desc_t *desc, const void *A, const void *omega, int64_t ldo,
              void *U, int64_t ldu, void *S, void *V, int64_t ldv);
 

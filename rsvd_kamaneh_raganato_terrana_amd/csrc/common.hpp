@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstdlib>
 #include <tuple>
 
 namespace rsvd {
@@ -67,8 +68,23 @@ template <> struct Vec16<double> {
 // a cooperative launch, so co-residency is the runtime's guarantee -- the launch fails when the
 // grid cannot be resident at once (e.g. CUs held by another process's kernels) -- instead of an
 // assumption the kernel's bounded spins can only report after the fact.
+// RSVD_COOP=0 in the environment launches them plainly (the same kernel; for profiling runs:
+// rocprofv3 7.2's kernel-trace teardown segfaults at process exit after a cooperative launch --
+// C4 / C5 traces, never C2's -- although the trace it wrote is complete).
+inline bool coop_launch_enabled() {
+    static const int env = [] {
+        const char* v = std::getenv("RSVD_COOP");
+        return v ? std::atoi(v) : 1;
+    }();
+    return env != 0;
+}
+
 template <typename... P, typename... A>
 hipError_t launch_coresident(void (*kernel)(P...), dim3 grid, dim3 block, size_t lds, hipStream_t s, A&&... a) {
+    if (!coop_launch_enabled()) {
+        hipLaunchKernelGGL(kernel, grid, block, lds, s, static_cast<P>(a)...);
+        return hipGetLastError();
+    }
     std::tuple<P...> args(static_cast<P>(a)...);
     void* argv[sizeof...(P) > 0 ? sizeof...(P) : 1];
     std::apply([&](auto&... x) {

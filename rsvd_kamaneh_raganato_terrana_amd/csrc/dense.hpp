@@ -88,6 +88,11 @@ hipError_t launch_identity_cols(T* Y, int64_t ldy, int64_t rows, int cols, int64
 // zero the strictly lower part of a column-major rows x cols matrix
 template <typename T>
 hipError_t launch_zero_below(T* R, int64_t ldr, int64_t rows, int64_t cols, hipStream_t s);
+// D (m x n fp32, ld m) = bf16 (fp8 = 0) or OCP e4m3 (fp8 = 1) A (column-major, ld lda), exactly
+hipError_t launch_lowp_to_f32(const void* A, int64_t lda, int64_t m, int64_t n, int fp8, float* D, hipStream_t s);
+// D (rows x cols fp32, column-major, ld) = a bf16 row-major panel (rows x LP)
+hipError_t launch_bf16_panel_to_f32(const uint16_t* P, int64_t rows, int cols, int LP, float* D, int64_t ld,
+                                    hipStream_t s);
 // D (m x n fp64, ld m) = A (column-major, ld lda)
 template <typename T>
 hipError_t launch_widen(const T* A, int64_t lda, int64_t m, int64_t n, double* D, hipStream_t s);

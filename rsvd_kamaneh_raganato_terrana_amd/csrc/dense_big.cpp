@@ -22,6 +22,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <string>
 
 #include "dense.hpp"
@@ -97,8 +98,9 @@ struct QrBig {
     float* R32;
     int* colflag;
 
-    QrBig(rsvd_handle_t h_, const QrBigWs<T>& L_) : h(h_), s(h_->stream), L(L_) {
-        char* b = h->ws + L.off_bo;
+    QrBig(rsvd_handle_t h_, const QrBigWs<T>& L_, char* base = nullptr) : h(h_), s(h_->stream), L(L_) {
+        if (!base) base = h->ws;
+        char* b = base + L.off_bo;
         P = reinterpret_cast<T*>(b + L.bo.off_P);
         Q = reinterpret_cast<T*>(b + L.bo.off_Q);
         T1 = reinterpret_cast<T*>(b + L.bo.off_T1);
@@ -110,8 +112,8 @@ struct QrBig {
         W = reinterpret_cast<double*>(b + L.bo.off_W);
         R32 = reinterpret_cast<float*>(b + L.bo.off_R32);
         colflag = reinterpret_cast<int*>(b + L.bo.off_colflag);
-        Y = reinterpret_cast<T*>(h->ws + L.off_Y);
-        C = reinterpret_cast<T*>(h->ws + L.off_C);
+        Y = reinterpret_cast<T*>(base + L.off_Y);
+        C = reinterpret_cast<T*>(base + L.off_C);
     }
 
     double tol() const { return sizeof(T) == 4 ? 1e-13 : 1e-28; }
@@ -142,6 +144,31 @@ struct QrBig {
         if (c0 == 0) return RSVD_OK;
         RSVD_CK(launch_gemm<T>(1, 0, c0, w, m, T(1), Qp, ldq, Y, m, T(0), C, c0, s));
         RSVD_CK(launch_gemm<T>(0, 0, m, w, c0, T(-1), Qp, ldq, C, c0, T(1), Y, m, s));
+        return RSVD_OK;
+    }
+    // Qo (rows x K, ld rows) = an orthonormal basis of span(Src[:, :K]) (K <= rows), 512-column
+    // blocks: CGS2 against the earlier blocks, shifted CholeskyQR3 + repair, and (past the first
+    // block) one more projection + orthonormalisation, as qr_big_typed
+    int orth_cols(const T* Src, int64_t lds, int64_t K, T* Qo, uint64_t seed) {
+        const int64_t rows = L.bo.rows;
+        const int LPb = L.bo.LP;
+        for (int64_t c0 = 0; c0 < K; c0 += kQrBlock) {
+            const int w = (int)std::min<int64_t>(kQrBlock, K - c0);
+            RSVD_CK(hipMemsetAsync(h->dflags + 4, 0, sizeof(int), s));  // this block's breakdown count
+            RSVD_CK(hipMemcpy2DAsync(Y, sizeof(T) * rows, Src + c0 * lds, sizeof(T) * lds, sizeof(T) * rows, w,
+                                     hipMemcpyDeviceToDevice, s));
+            RSVD_TRY(project(Qo, rows, rows, c0, w));
+            RSVD_TRY(project(Qo, rows, rows, c0, w));
+            RSVD_CK(launch_colmajor_to_panel<T>(Y, rows, rows, w, LPb, P, s));
+            RSVD_TRY(orth(w, seed + 2 * (uint64_t)c0));
+            if (c0 > 0) {
+                RSVD_CK(launch_panel_to_colmajor<T>(Q, rows, w, LPb, Y, rows, s));
+                RSVD_TRY(project(Qo, rows, rows, c0, w));
+                RSVD_CK(launch_colmajor_to_panel<T>(Y, rows, rows, w, LPb, P, s));
+                RSVD_TRY(orth(w, seed + 2 * (uint64_t)c0 + 1));
+            }
+            RSVD_CK(launch_panel_to_colmajor<T>(Q, rows, w, LPb, Qo + c0 * rows, rows, s));
+        }
         return RSVD_OK;
     }
 };
@@ -263,6 +290,149 @@ int svd_big_typed(rsvd_handle_t h, int64_t m, int64_t n, const T* A, int64_t lda
     return RSVD_OK;
 }
 
+
+// ---- rSVD() past 512 sketch columns (src/rSVD.cpp:72-133 has no cap on l) ------------------------
+// The same algorithm as the wide engine, in column-major blocks: Omega (Philox, or the caller's;
+// rounded to bf16 / e4m3 for those A types as rsvd_generate_omega documents), Y = A Omega,
+// Q = orth(Y), q x {Z = A^T Q, X = orth(Z), Y = A X, Q = orth(Y)}, B^T = A^T Q, Q_B = orth(B^T),
+// R = Q_B^T B^T, W = R^T = U_w S V_w^T (block Jacobi, l <= 4096), U = Q U_w, V = Q_B V_w.  Products
+// on the MFMA GEMM (gemm.hip) in the panel precision (fp64 for fp64 A, fp32 otherwise; bf16 / e4m3
+// A widened to fp32 once -- exact), orthonormalisations by orth_cols (block CGS2 + CholeskyQR3).
+template <typename T>
+struct BigLWs {
+    QrBigWs<T> qm, qn;
+    int MR, LP;
+    size_t off_qm, off_qn, off_A32, off_Om, off_Y, off_Q, off_Z, off_X, off_R, off_R64, off_JX, off_JJ, off_Uw, off_Vw,
+        off_U32, off_S, off_sync, off_om16, total;
+    BigLWs(const rsvd_desc_t* d)
+        : qm(d->m, std::min<int64_t>(d->l, d->m)), qn(d->n, std::min<int64_t>(d->l, d->n)) {
+        const int64_t m = d->m, n = d->n, l = d->l;
+        MR = (int)rup(l, 32);
+        LP = (int)rup(l, 32);
+        const bool lowp = d->dtype == RSVD_BF16 || d->dtype == RSVD_FP8_E4M3;
+        size_t o = 0;
+        auto take = [&](size_t bytes) {
+            const size_t at = o;
+            o = align256(o + bytes);
+            return at;
+        };
+        off_qm = take(qm.total);
+        off_qn = take(qn.total);
+        off_A32 = take(lowp ? sizeof(float) * (size_t)m * n : 0);
+        off_Om = take(sizeof(T) * (size_t)n * l);
+        off_Y = take(sizeof(T) * (size_t)m * l);
+        off_Q = take(sizeof(T) * (size_t)m * l);
+        off_Z = take(sizeof(T) * (size_t)n * l);
+        off_X = take(sizeof(T) * (size_t)n * rup(l, 32));  // (also the Philox panel, pitch rup(l, 32))
+        off_R = take(sizeof(T) * (size_t)l * l);
+        off_R64 = take(sizeof(T) == 4 ? sizeof(double) * (size_t)l * l : 0);
+        off_JX = take(sizeof(double) * 2 * (size_t)MR * LP);
+        off_JJ = take(sizeof(double) * 2 * (size_t)LP * LP);
+        off_Uw = take(sizeof(double) * (size_t)MR * LP);
+        off_Vw = take(sizeof(double) * (size_t)LP * LP);
+        off_U32 = take(sizeof(T) == 4 ? sizeof(float) * (size_t)MR * LP : 0);
+        off_S = take(sizeof(double) * LP);
+        off_sync = take(sizeof(unsigned) * kBJSyncWords);
+        off_om16 = take(lowp ? (size_t)2 * n * rup(l, 16) : 0);
+        total = o;
+    }
+};
+
+template <typename T>
+int big_rsvd_typed(rsvd_handle_t h, const rsvd_desc_t* d, const void* Av, const void* omega, int64_t ldo, void* U,
+                   int64_t ldu, void* S, void* V, int64_t ldv, void* Qout, int64_t ldq) {
+    BigLWs<T> L(d);
+    RSVD_TRY(ensure_ws(h, L.total));
+    RSVD_CK(reset_run_flags(h->dflags, h->stream));
+    hipStream_t s = h->stream;
+    char* b = h->ws;
+    const int64_t m = d->m, n = d->n, l = d->l;
+    auto ptr = [&](size_t off) { return reinterpret_cast<T*>(b + off); };
+    T *Om = ptr(L.off_Om), *Y = ptr(L.off_Y), *Q = ptr(L.off_Q), *Z = ptr(L.off_Z), *X = ptr(L.off_X), *R = ptr(L.off_R);
+    QrBig<T> Em(h, L.qm, b + L.off_qm), En(h, L.qn, b + L.off_qn);
+    const bool lowp = d->dtype == RSVD_BF16 || d->dtype == RSVD_FP8_E4M3;
+    const int f8 = d->dtype == RSVD_FP8_E4M3;
+    // A in the panel precision
+    const T* A = reinterpret_cast<const T*>(Av);
+    int64_t lda = d->lda;
+    if (lowp) {
+        float* A32 = reinterpret_cast<float*>(b + L.off_A32);
+        RSVD_CK(launch_lowp_to_f32(Av, d->lda, m, n, f8, A32, s));
+        A = reinterpret_cast<const T*>(A32);
+        lda = m;
+    }
+    // Omega (n x l, column-major)
+    if (lowp) {
+        const int LP16 = (int)rup(l, 16);
+        uint16_t* pan = reinterpret_cast<uint16_t*>(b + L.off_om16);
+        if (omega) {
+            RSVD_CK(launch_omega_lowp_from(reinterpret_cast<const float*>(omega), ldo, n, (int)l, LP16, f8, pan, s));
+            RSVD_CK(launch_bf16_panel_to_f32(pan, n, (int)l, LP16, reinterpret_cast<float*>(Om), n, s));
+        } else {
+            RSVD_CK(launch_omega_lowp(pan, n, (int)l, LP16, d->seed, f8, reinterpret_cast<float*>(Om), s));
+        }
+    } else if (omega) {
+        RSVD_CK(hipMemcpy2DAsync(Om, sizeof(T) * n, omega, sizeof(T) * ldo, sizeof(T) * n, l, hipMemcpyDeviceToDevice, s));
+    } else {
+        // Philox in the panel layout (ld LP = l rounded to 32: X is free scratch until the first orth)
+        const int LPo = (int)rup(l, 32);
+        RSVD_CK(launch_philox_omega<T>(X, n, (int)l, LPo, d->seed, s));
+        RSVD_CK(launch_panel_to_colmajor<T>(X, n, (int)l, LPo, Om, n, s));
+    }
+    const uint64_t sd = d->seed ^ 0xB16Full;
+    // intermediate_step (src/rSVD.cpp:57-70)
+    RSVD_CK(launch_gemm<T>(0, 0, m, l, n, T(1), A, lda, Om, n, T(0), Y, m, s));  // Y = A Omega
+    RSVD_TRY(Em.orth_cols(Y, m, l, Q, sd));
+    for (int i = 0; i < d->q; ++i) {
+        RSVD_CK(launch_gemm<T>(1, 0, n, l, m, T(1), A, lda, Q, m, T(0), Z, n, s));  // Z = A^T Q
+        RSVD_TRY(En.orth_cols(Z, n, l, X, sd + 1000003ull * (2 * i + 1)));
+        RSVD_CK(launch_gemm<T>(0, 0, m, l, n, T(1), A, lda, X, n, T(0), Y, m, s));  // Y = A X
+        RSVD_TRY(Em.orth_cols(Y, m, l, Q, sd + 1000003ull * (2 * i + 2)));
+    }
+    if (Qout) {
+        RSVD_CK(hipMemcpy2DAsync(Qout, sizeof(T) * ldq, Q, sizeof(T) * m, sizeof(T) * m, l, hipMemcpyDeviceToDevice, s));
+        return RSVD_OK;
+    }
+    // B^T = A^T Q, Q_B = orth(B^T), R = Q_B^T B^T (src/rSVD.cpp:89, SVD_class.hpp:116-123)
+    RSVD_CK(launch_gemm<T>(1, 0, n, l, m, T(1), A, lda, Q, m, T(0), Z, n, s));
+    RSVD_TRY(En.orth_cols(Z, n, l, X, sd + 7));
+    RSVD_CK(launch_gemm<T>(1, 0, l, l, n, T(1), X, n, Z, n, T(0), R, l, s));
+    const double* R64 = reinterpret_cast<const double*>(R);
+    if (sizeof(T) == 4) {
+        double* w = reinterpret_cast<double*>(b + L.off_R64);
+        RSVD_CK(launch_widen<T>(R, l, l, l, w, s));
+        R64 = w;
+    }
+    RSVD_CK(launch_check_finite<double>(R64, (int)(l * l), h->dflags + kFlagNonFinite, s));
+    // W = R^T: X column c = row c of R (the row-major read of the column-major R)
+    double* JXp = reinterpret_cast<double*>(b + L.off_JX);
+    double* JJp = reinterpret_cast<double*>(b + L.off_JJ);
+    double* Uw = reinterpret_cast<double*>(b + L.off_Uw);
+    double* Vw = reinterpret_cast<double*>(b + L.off_Vw);
+    double* Sd = reinterpret_cast<double*>(b + L.off_S);
+    unsigned* sync = reinterpret_cast<unsigned*>(b + L.off_sync);
+    RSVD_CK(launch_block_jacobi_ex<double>(R64, l, 1, (int)l, (int)l, L.MR, L.LP, JXp, JJp, Uw, Vw, Sd, sync,
+                                           h->dflags + 1, s, sizeof(T) == 4 ? 1e-8 : 1e-16,
+                                           sizeof(T) == 4 ? kBJTolF32 : kBJTolF64));
+    const double asc = d->a_scale != 0.0 ? d->a_scale : 1.0;
+    RSVD_CK(launch_convert_scale<T>(Sd, reinterpret_cast<T*>(S), (int)l, std::fabs(asc), s));
+    // U = Q U_w, V = Q_B V_w (U_w, V_w row-major with pitch LP: their column-major views are the transposes)
+    const T* uw = reinterpret_cast<const T*>(Uw);
+    const T* vw = reinterpret_cast<const T*>(Vw);
+    if (sizeof(T) == 4) {
+        float* u32 = reinterpret_cast<float*>(b + L.off_U32);
+        float* v32 = reinterpret_cast<float*>(JXp);  // free after the Jacobi finish
+        RSVD_CK(launch_convert_scale<float>(Uw, u32, L.MR * L.LP, 1.0, s));
+        RSVD_CK(launch_convert_scale<float>(Vw, v32, L.LP * L.LP, 1.0, s));
+        uw = reinterpret_cast<const T*>(u32);
+        vw = reinterpret_cast<const T*>(v32);
+    }
+    RSVD_CK(launch_gemm<T>(0, 1, m, l, l, T(1), Q, m, uw, L.LP, T(0), reinterpret_cast<T*>(U), ldu, s));
+    RSVD_CK(launch_gemm<T>(0, 1, n, l, l, T(1), X, n, vw, L.LP, T(0), reinterpret_cast<T*>(V), ldv, s));
+    if (asc < 0.0) RSVD_CK(launch_scale_cols<T>(reinterpret_cast<T*>(V), n, (int)l, ldv, -1.0, s));
+    RSVD_CK(launch_check_finite<T>(reinterpret_cast<const T*>(S), (int)l, h->dflags + kFlagNonFinite, s));
+    return RSVD_OK;
+}
 }  // namespace
 
 size_t qr_big_workspace(int64_t m, int64_t n, int full, int dtype) {
@@ -292,6 +462,28 @@ int svd_big(rsvd_handle_t h, int64_t m, int64_t n, const void* A, int64_t lda, i
                                      static_cast<double*>(S), static_cast<double*>(V), ldv);
     return svd_big_typed<float>(h, m, n, static_cast<const float*>(A), lda, static_cast<float*>(U), ldu,
                                 static_cast<float*>(S), static_cast<float*>(V), ldv);
+}
+
+size_t big_rsvd_workspace(const rsvd_desc_t* d) {
+    return d->dtype == RSVD_F64 ? BigLWs<double>(d).total : BigLWs<float>(d).total;
+}
+
+int big_rsvd_run(rsvd_handle_t h, const rsvd_desc_t* d, const void* A, const void* omega, int64_t ldo, void* U,
+                 int64_t ldu, void* S, void* V, int64_t ldv, void* Qout, int64_t ldq) {
+    if (d->l > kBigLMax) {
+        h->err = "l > 4096 not supported (the block Jacobi small SVD is built for l <= 4096)";
+        return RSVD_ERR_UNSUPPORTED;
+    }
+    if (h->world > 1 || (d->flags & RSVD_FLAG_FORCE_NSHARD)) {
+        h->err = "l > 512 runs on one GPU (no row sharding past the wide engine's panels)";
+        return RSVD_ERR_UNSUPPORTED;
+    }
+    if (!Qout && (d->method == RSVD_SVD_POWER || d->method == RSVD_SVD_POWER_IC)) {
+        h->err = "SVDMethod::Power is built for l <= 512";
+        return RSVD_ERR_UNSUPPORTED;
+    }
+    if (d->dtype == RSVD_F64) return big_rsvd_typed<double>(h, d, A, omega, ldo, U, ldu, S, V, ldv, Qout, ldq);
+    return big_rsvd_typed<float>(h, d, A, omega, ldo, U, ldu, S, V, ldv, Qout, ldq);
 }
 
 }  // namespace rsvd

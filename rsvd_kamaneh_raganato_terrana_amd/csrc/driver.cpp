@@ -80,7 +80,7 @@ int check_desc_msg(const rsvd_desc_t* d, const char** err) {
         *err = "Unsupported SVD method";  // src/rSVD.cpp:123 wording
         return RSVD_ERR_UNSUPPORTED;
     }
-    if (d->l > 512) { *err = "l > 512 not supported"; return RSVD_ERR_UNSUPPORTED; }
+    if (d->l > kBigLMax) { *err = "l > 4096 not supported"; return RSVD_ERR_UNSUPPORTED; }
     if (d->l > d->n || d->l > d->m) { *err = "l > min(m, n) not supported"; return RSVD_ERR_UNSUPPORTED; }
     if (!std::isfinite(d->a_scale)) { *err = "a_scale is not finite"; return RSVD_ERR_INVALID_ARG; }
     return RSVD_OK;
@@ -520,6 +520,10 @@ int rsvd_workspace_bytes(const rsvd_desc_t* d, size_t* bytes) {
     if (!d || !bytes) return RSVD_ERR_INVALID_ARG;
     const char* err = "";
     RSVD_TRY(check_desc_msg(d, &err));
+    if (d->l > 512) {  // dense_big.cpp
+        *bytes = big_rsvd_workspace(d);
+        return RSVD_OK;
+    }
     RSVD_TRY(wide_workspace_bytes(d, bytes));
     if (wide_path(d)) return RSVD_OK;
     // narrow single-GPU layout, or the wide engine's when the handle is row-sharded: the larger
@@ -538,6 +542,7 @@ int rsvd_run(rsvd_handle_t h, const rsvd_desc_t* d, const void* A, const void* o
         return RSVD_ERR_INVALID_ARG;
     }
     RSVD_TRY(set_device(h));
+    if (d->l > 512) return big_rsvd_run(h, d, A, omega, ldo, U, ldu, S, V, ldv, nullptr, 0);
     if (wide_path(d) || h->world > 1 || (d->flags & RSVD_FLAG_FORCE_NSHARD))
         return wide_run(h, d, A, omega, ldo, U, ldu, S, V, ldv, nullptr, 0);
     if (d->dtype == RSVD_F64) return run_typed<double>(h, d, A, omega, ldo, U, ldu, S, V, ldv, nullptr, 0);
@@ -553,6 +558,7 @@ int rsvd_range_finder(rsvd_handle_t h, const rsvd_desc_t* d, const void* A, cons
         return RSVD_ERR_INVALID_ARG;
     }
     RSVD_TRY(set_device(h));
+    if (d->l > 512) return big_rsvd_run(h, d, A, omega, ldo, nullptr, 0, nullptr, nullptr, 0, Q, ldq);
     if (wide_path(d) || h->world > 1) return wide_run(h, d, A, omega, ldo, nullptr, 0, nullptr, nullptr, 0, Q, ldq);
     if (d->dtype == RSVD_F64) return run_typed<double>(h, d, A, omega, ldo, nullptr, 0, nullptr, nullptr, 0, Q, ldq);
     return run_typed<float>(h, d, A, omega, ldo, nullptr, 0, nullptr, nullptr, 0, Q, ldq);

@@ -222,7 +222,49 @@ __global__ void widen_kernel(const T* __restrict__ A, int64_t lda, int64_t m, in
 
 inline unsigned grid_for(int64_t n) { return (unsigned)std::min<int64_t>((n + 255) / 256, 4096); }
 
+// OCP e4m3fn -> fp32 (exact): 1 sign, 4 exponent (bias 7), 3 mantissa bits; S.1111.111 is NaN
+__device__ __forceinline__ float e4m3_to_f32(uint32_t b) {
+    const uint32_t e = (b >> 3) & 15u, mt = b & 7u;
+    float v;
+    if (e == 15u && mt == 7u) v = __builtin_nanf("");
+    else if (e == 0u) v = (float)mt * 0x1p-9f;
+    else v = __uint_as_float(((e + 120u) << 23) | (mt << 20));
+    return (b & 0x80u) ? -v : v;
+}
+
+// bf16 / e4m3 A (column-major, ld lda) -> fp32 (column-major, ld m)
+__global__ void lowp_to_f32_kernel(const void* __restrict__ A, int64_t lda, int64_t m, int64_t n, int fp8,
+                                   float* __restrict__ D) {
+    const int64_t tot = m * n;
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < tot; e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t o = (e % m) + (e / m) * lda;
+        D[e] = fp8 ? e4m3_to_f32(reinterpret_cast<const uint8_t*>(A)[o])
+                   : __uint_as_float((uint32_t)reinterpret_cast<const uint16_t*>(A)[o] << 16);
+    }
+}
+
+// bf16 row-major panel (rows x LP) -> fp32 column-major (rows x cols, ld)
+__global__ void bf16_panel_to_f32_kernel(const uint16_t* __restrict__ P, int64_t rows, int cols, int LP,
+                                         float* __restrict__ D, int64_t ld) {
+    const int64_t tot = rows * cols;
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < tot; e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = e % rows, j = e / rows;
+        D[i + j * ld] = __uint_as_float((uint32_t)P[i * LP + j] << 16);
+    }
+}
+
 }  // namespace
+
+hipError_t launch_lowp_to_f32(const void* A, int64_t lda, int64_t m, int64_t n, int fp8, float* D, hipStream_t s) {
+    hipLaunchKernelGGL(lowp_to_f32_kernel, dim3(grid_for(m * n)), dim3(256), 0, s, A, lda, m, n, fp8, D);
+    return hipGetLastError();
+}
+
+hipError_t launch_bf16_panel_to_f32(const uint16_t* P, int64_t rows, int cols, int LP, float* D, int64_t ld,
+                                    hipStream_t s) {
+    hipLaunchKernelGGL(bf16_panel_to_f32_kernel, dim3(grid_for(rows * cols)), dim3(256), 0, s, P, rows, cols, LP, D, ld);
+    return hipGetLastError();
+}
 
 template <typename T>
 hipError_t launch_gemm(int ta, int tb, int64_t M, int64_t N, int64_t K, T alpha, const T* A, int64_t lda, const T* B,

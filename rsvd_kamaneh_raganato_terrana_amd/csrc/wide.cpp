@@ -56,7 +56,8 @@ struct WideLayout {
     ProjPlan pnn, ptn;
     GramPlan gm, gn, gx;
     size_t off_Xn, off_Zn, off_Ym, off_Qm, off_T1, off_Xh, off_Xl, off_Qh, off_Ql, off_X8, off_pslab, off_gslab;
-    size_t off_G, off_R, off_Rinv, off_W, off_R1, off_Uw, off_Vw, off_JX, off_JJ, off_M32, off_colflag, off_sync, total;
+    size_t off_G, off_R, off_Rinv, off_W, off_R1, off_Uw, off_Vw, off_JX, off_JJ, off_M32, off_MS, off_colflag, off_sync,
+        total;
 
     int64_t mpad, npad;  // bf16 panel rows, zero-padded to a multiple of 32 (wproj2 reads whole k-steps)
     bool s8 = false;     // the sketch runs e4m3 x e4m3 on the fp8 MFMA
@@ -130,6 +131,7 @@ struct WideLayout {
         off_JX = take(sizeof(double) * 2 * L2);
         off_JJ = take(sizeof(double) * 2 * L2);
         off_M32 = take(sizeof(float) * 3 * L2);  // Rinv, Uw, Vw in fp32 (panel_gemm operand for fp32 panels)
+        off_MS = take(sizeof(T) == 4 ? sizeof(bf16_t) * 3 * L2 : 0);  // the three bf16 pieces of panel_gemm's M
         off_colflag = take(sizeof(int) * LP);
         off_sync = take(sizeof(unsigned) * kBJSyncWords);
         total = o;
@@ -187,6 +189,7 @@ struct WideEngine {
         Rinv32 = reinterpret_cast<float*>(b + L.off_M32);
         Uw32 = Rinv32 + (size_t)L.LP * L.LP;
         Vw32 = Uw32 + (size_t)L.LP * L.LP;
+        Ms = sizeof(T) == 4 ? reinterpret_cast<bf16_t*>(b + L.off_MS) : nullptr;
         colflag = reinterpret_cast<int*>(b + L.off_colflag);
         sync = reinterpret_cast<unsigned*>(b + L.off_sync);
     }
@@ -273,10 +276,16 @@ struct WideEngine {
     }
 
     double tol() const { return sizeof(T) == 4 ? 1e-13 : 1e-28; }
-    // the split Gram's relative entry error is ~3e-8 of sqrt(G_ii G_jj): pivots below 1e-5 of their
-    // diagonal (cond(P) past ~300) are refactored from the fp64 Gram
-    static constexpr double kSplitIllTol = 1e-5;
+    // the split Gram's entry error is ~3e-8 of sqrt(G_ii G_jj).  A pivot ratio d_k / G_kk above 1e-6
+    // is then known to a few per cent, and the factor's only use -- Q = P R^-1 spanning span(P) --
+    // tolerates that: Q's departure from orthonormality is ~eps_G cond(P)^2 <= 0.03 (intermediate
+    // panels; output panels take a second pass).  Below it (cond(P) past ~1e3, breakdowns) the
+    // fp64 Gram and factor run again.
+    static constexpr double kSplitIllTol = 1e-7;
     bool split_gram = false;
+    bool split_panel = false;  // panel products on the bf16 MFMA, three-piece split (RSVD_PANEL_SPLIT=0: fp32 MFMA)
+    bf16_t* Ms = nullptr;
+    bf16_t* ms() const { return split_panel ? Ms : nullptr; }
     bool chol2 = true;  // two-level factor at LP = 512 (RSVD_CHOL2=0: the one-workgroup LP = 512 kernel)
     // panel_gemm's operand in the panel precision: fp64 matrices as-is, fp32 copies for fp32 panels
     const T* mat(const double* m64, const float* m32) const {
@@ -286,7 +295,7 @@ struct WideEngine {
     // One CholeskyQR pass Out = P chol(P^T P)^-1 (+ bf16 hi/lo of Out).  `pred`: predicated pass.
     // fp32 panels of bf16 / e4m3 A (one rank, unpredicated passes): the Gram by the three-piece bf16
     // split (wide_qr.hip gram_split_kernel, |dG| ~ 1e-8 |G|); when a pivot of its factor falls below
-    // kSplitIllTol of its diagonal (cond(P) beyond ~300, or a breakdown) the fp64 Gram and factor
+    // kSplitIllTol of its diagonal (cond(P) beyond ~1e3, or a breakdown) the fp64 Gram and factor
     // run again, predicated on that test (h->dflags[kFlagSplitIll]), and their R / R^-1 / flags stand.
     int cholqr_pass(const T* P, int64_t rows, const GramPlan& gp, T* Out, bool sharded, bf16_t* hi, bf16_t* lo,
                     int* flag, const int* pred) {
@@ -304,7 +313,7 @@ struct WideEngine {
             RSVD_CK(factor(h->dflags + kFlagSplitScratch, kSplitIllTol, ill));
             RSVD_CK(launch_gram_wide<T>(P, nullptr, rows, L.LP, gp, gslab, G, ill, s));
             RSVD_CK(launch_chol_wide(G, L.l, L.LP, tol(), R, Rinv, r32, colflag, flag, W, ill, s));
-            RSVD_CK(launch_panel_gemm<T>(P, rows, L.LP, mat(Rinv, Rinv32), 1, Out, 0, 0, hi, lo, nullptr, s));
+            RSVD_CK(launch_panel_gemm<T>(P, rows, L.LP, mat(Rinv, Rinv32), 1, Out, 0, 0, hi, lo, nullptr, s, ms()));
             return RSVD_OK;
         }
         RSVD_CK(launch_gram_wide<T>(P, nullptr, rows, L.LP, gp, gslab, G, pred, s));
@@ -313,7 +322,7 @@ struct WideEngine {
             RSVD_CK(launch_chol_wide(G, L.l, L.LP, tol(), R, Rinv, r32, colflag, flag, W, pred, s));
         else
             RSVD_CK(factor(flag, 0.0, nullptr));
-        RSVD_CK(launch_panel_gemm<T>(P, rows, L.LP, mat(Rinv, Rinv32), 1, Out, 0, 0, hi, lo, pred, s));
+        RSVD_CK(launch_panel_gemm<T>(P, rows, L.LP, mat(Rinv, Rinv32), 1, Out, 0, 0, hi, lo, pred, s, ms()));
         return RSVD_OK;
     }
 
@@ -408,9 +417,9 @@ struct WideEngine {
             RSVD_CK(launch_convert_scale<float>(Vc, Vw32, L2, 1.0, s));
         }
         RSVD_CK(launch_panel_gemm<T>(Qm, L.m, L.LP, mat(Up, Uw32), 0, reinterpret_cast<T*>(U), ldu, L.l, nullptr,
-                                     nullptr, nullptr, s));
+                                     nullptr, nullptr, s, ms()));
         RSVD_CK(launch_panel_gemm<T>(Xn, L.n, L.LP, mat(Vc, Vw32), 0, reinterpret_cast<T*>(V), ldv, L.l, nullptr,
-                                     nullptr, nullptr, s));
+                                     nullptr, nullptr, s, ms()));
         return finish(d, S, V, ldv);
     }
 
@@ -452,15 +461,15 @@ struct WideEngine {
             RSVD_CK(launch_convert_scale<float>(Vw, Vw32, L2, 1.0, s));
         }
         RSVD_CK(launch_panel_gemm<T>(Qm, L.m, L.LP, mat(Uw, Uw32), 0, reinterpret_cast<T*>(U), ldu, L.l, nullptr,
-                                     nullptr, nullptr, s));
+                                     nullptr, nullptr, s, ms()));
         if (nsh) {  // V rows of this shard as a panel (in Zn, free by now), all-gathered, then V
             RSVD_CK(launch_panel_gemm<T>(Xn + c0 * L.LP, L.nc, L.LP, mat(Vw, Vw32), 0, Zn + c0 * L.LP, 0, 0, nullptr,
-                                         nullptr, nullptr, s));
+                                         nullptr, nullptr, s, ms()));
             RSVD_TRY(collective(RSVD_COLL_ALL_GATHER, Zn + c0 * L.LP, Zn, L.nc * L.LP, tdt()));
             RSVD_CK(launch_panel_to_colmajor<T>(Zn, L.n, L.l, L.LP, reinterpret_cast<T*>(V), ldv, s));
         } else {
             RSVD_CK(launch_panel_gemm<T>(Xn, L.n, L.LP, mat(Vw, Vw32), 0, reinterpret_cast<T*>(V), ldv, L.l, nullptr,
-                                         nullptr, nullptr, s));
+                                         nullptr, nullptr, s, ms()));
         }
         return finish(d, S, V, ldv);
     }
@@ -472,7 +481,9 @@ int wide_typed(rsvd_handle_t h, const rsvd_desc_t* d, const void* A, const void*
     // n-side sharding: a collective hook on a sharded handle, not for SVDMethod::Power (its stage
     // runs on the whole Q_B) nor for the range-finder-only entry point (Qout)
     // (RSVD_FLAG_FORCE_NSHARD: the same code path at world 1, so one GPU runs the RCCL calls)
-    const bool nshard = (h->world > 1 || (d->flags & RSVD_FLAG_FORCE_NSHARD)) && h->coll && !Qout &&
+    // (past 64 ranks the n side stays replicated: rsvd_workspace_bytes sizes the padded n-side
+    // panels for worlds up to 64, and a caller-provided workspace is sized by it)
+    const bool nshard = (h->world > 1 || (d->flags & RSVD_FLAG_FORCE_NSHARD)) && h->world <= 64 && h->coll && !Qout &&
                         d->method != RSVD_SVD_POWER && d->method != RSVD_SVD_POWER_IC;
     WideLayout<T> L(d, (reinterpret_cast<uintptr_t>(A) & 15) == 0, h->world, nshard);
     RSVD_TRY(ensure_ws(h, L.total));
@@ -506,6 +517,11 @@ int wide_typed(rsvd_handle_t h, const rsvd_desc_t* d, const void* A, const void*
             return v ? std::atoi(v) : 1;
         }();
         E.chol2 = env2 != 0;
+        static const int env3 = [] {
+            const char* v = std::getenv("RSVD_PANEL_SPLIT");
+            return v ? std::atoi(v) : 1;
+        }();
+        E.split_panel = env3 != 0 && sizeof(T) == 4 && L.lowp && L.LP % 32 == 0 && L.LP >= 128;
     }
     E.lowp_inter = (d->flags & RSVD_FLAG_LOWP_INTERMEDIATES) != 0;
     E.seed = d->seed;

@@ -87,8 +87,8 @@ hipError_t launch_chol_wide_2level(const double* G, int l, double tol, double* R
                                    int* colflag, int* flag, double* work, double* scratch, hipStream_t s,
                                    double ill_tol = 0.0, int* ill = nullptr);
 constexpr size_t kChol2ScratchDoubles = (size_t)7 * 256 * 256 + 768;
-// G = P^T P of an fp32 panel by the three-piece bf16 split on the bf16 MFMA (fp64 accumulation per
-// 32-row step; |dG| ~ 1e-8 |G|) -- same plan / slab layout as launch_gram_wide.  LP in {128, 256, 512}.
+// G = P^T P of an fp32 panel by the three-piece bf16 split on the bf16 MFMA (fp32 chunk sums added
+// in fp64; |dG| ~ 1e-8 |G|) -- same plan / slab layout as launch_gram_wide.  LP in {128, 256, 512}.
 bool gram_split_ok(int LP);
 hipError_t launch_gram_split(const float* P, int64_t rows, int LP, const GramPlan& gp, double* slabs, double* G,
                              hipStream_t s);
@@ -100,9 +100,12 @@ extern int chol_variant;
 // Out layouts: row-major panel (ldo = 0) or the caller's column-major matrix (first
 // `cols` columns, leading dimension ldo).  Optionally also writes the bf16 hi / lo panels of Out
 // (row-major, LP wide).  `pred`: as above.
+// msplit (fp32 panels, LP a multiple of 32 >= 128; 3 LP^2 bf16 of scratch): the product runs on the
+// bf16 MFMA with both operands split in three bf16 pieces (panel_split_kernel) instead of the fp32 MFMA.
 template <typename T>
 hipError_t launch_panel_gemm(const T* In, int64_t rows, int LP, const T* M, int upper, T* Out, int64_t ldo,
-                             int cols, bf16_t* hi, bf16_t* lo, const int* pred, hipStream_t s);
+                             int cols, bf16_t* hi, bf16_t* lo, const int* pred, hipStream_t s,
+                             bf16_t* msplit = nullptr);
 // y[0..n) = (T)(x * sc)
 template <typename T>
 hipError_t launch_convert_scale(const double* x, T* y, int n, double sc, hipStream_t s);
@@ -159,5 +162,13 @@ int wide_workspace_bytes(const rsvd_desc_t* d, size_t* bytes);
 // rSVD (Qout == nullptr) or intermediate_step (Q into Qout) on the handle's stream.
 int wide_run(rsvd_handle_t h, const rsvd_desc_t* d, const void* A, const void* omega, int64_t ldo, void* U,
              int64_t ldu, void* S, void* V, int64_t ldv, void* Qout, int64_t ldq);
+
+// ---- dense_big.cpp: rSVD() past the wide engine's 512 sketch columns --------------------------------
+// One GPU, SVDMethod Jacobi / ParallelJacobi, l <= kBigLMax; column-major blocks on the MFMA GEMM
+// (bf16 / e4m3 A widened to fp32 once), block CGS2 + CholeskyQR3 orthonormalisation, block Jacobi.
+constexpr int kBigLMax = 4096;
+int big_rsvd_run(rsvd_handle_t h, const rsvd_desc_t* d, const void* A, const void* omega, int64_t ldo, void* U,
+                 int64_t ldu, void* S, void* V, int64_t ldv, void* Qout, int64_t ldq);
+size_t big_rsvd_workspace(const rsvd_desc_t* d);
 
 }  // namespace rsvd

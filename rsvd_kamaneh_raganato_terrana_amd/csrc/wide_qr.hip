@@ -270,11 +270,10 @@ __global__ __launch_bounds__(512) void gram_sym_kernel(const T* __restrict__ P, 
 // Split Gram of an fp32 panel on the bf16 MFMA.  Every fp32 value is EXACTLY h + m + t with
 // h = bf16(v), m = bf16(v - h), t = bf16(v - h - m) (8 + 8 + 8 significant bits), and the six
 // products hh, hm, mh, mm, ht, th carry P_ki P_kj to ~2^-24 of |P_ki P_kj| (the dropped mt, tm,
-// tt are below it).  Each bf16 product is exact in fp32; one v_mfma_f32_16x16x32_bf16 sums 32 rows
-// of them in fp32 and that partial is added to an fp64 accumulator after every 32-row step, so
-// the rounding does not grow with the panel height: measured on a cond 1e3 panel (numpy model of
-// the same arithmetic, 65536 x 256) |G_split - G|_F / |G|_F = 8e-9, max |dG_ij| / sqrt(G_ii G_jj)
-// = 3e-8.  Six bf16 MFMAs at 32x the fp64 MFMA rate: the Gram becomes an HBM read of the panel
+// tt are below it).  Each bf16 product is exact in fp32; the v_mfma_f32_16x16x32_bf16 chains sum a
+// row chunk (<= 1024 rows at the configs' sizes) in fp32 and the chunk partials are summed in fp64,
+// so the rounding does not grow with the panel height: numpy model of the same arithmetic on a
+// cond 1e3 panel (65536 x 256): |G_split - G|_F / |G|_F ~ 1e-8, max |dG_ij| / sqrt(G_ii G_jj) ~ 3e-8.  Six bf16 MFMAs at 32x the fp64 MFMA rate: the Gram becomes an HBM read of the panel
 // (C4 65536 x 256: ~100 -> ~20 us).  It is only used where its accuracy is enough -- CholeskyQR of
 // the fp32 panels of bf16 / e4m3 A, with the factor's pivots checked against kSplitIllTol
 // (launch_chol_wide, `ill`) and the fp64 Gram + factor re-run (predicated) when one is below it.
@@ -286,71 +285,72 @@ __global__ __launch_bounds__(512) void gram_sym_kernel(const T* __restrict__ P, 
 // partial tiles go to gram_sym's (chunk, 32x32 block) slab layout, summed by gram_reduce_kernel.
 typedef __attribute__((ext_vector_type(8))) short bf16x8s;
 
+// Work split: the tiles are cut into groups of TG (4; 2 at LP = 128) and each wave owns one
+// group pair (A <= B) -- TG x TG tile pairs whose A-side fragments stay in registers for the step
+// while the B-side ones stream (each fragment feeds TG x 6 MFMAs: ~0.25 KB of LDS reads per MFMA;
+// one fragment pair per tile pair read 1 KB per MFMA and made the kernel LDS-bound).  Diagonal
+// group pairs compute their TG^2 tile pairs in full and store the upper ones.  The fp32 MFMA
+// accumulators run over the whole row chunk (<= 1024 rows for the panels of the bf16 / e4m3
+// configs) and the chunk partials are summed in fp64 by gram_reduce_kernel.
 template <int LP> struct GramSplit {
-    static constexpr int NH = LP == 512 ? 8 : (LP == 256 ? 2 : 1);  // workgroups per chunk (as GramSym)
-    static constexpr int LNH = LP == 512 ? 3 : (LP == 256 ? 1 : 0);
-    static constexpr int NT = LP / 16, NP = NT * (NT + 1) / 2, NW = 8 * NH, PPW = (NP + NW - 1) / NW;
+    static constexpr int TG = LP == 128 ? 2 : 4;
+    static constexpr int NT = LP / 16, NTG = NT / TG, NBK = NTG * (NTG + 1) / 2;
+    static constexpr int NH = LP == 512 ? 4 : 1;  // workgroups per chunk
+    static constexpr int LNH = LP == 512 ? 2 : 0;
+    static constexpr int NWW = NBK / NH;          // waves per workgroup (10, 10, 9)
+    static constexpr int THREADS = 64 * NWW;
     static constexpr int NB = LP / 32, NBLK = NB * (NB + 1) / 2;
-    static constexpr int IMG = LP * 64;                // bytes of one piece image (LP columns x 32 rows bf16)
-    static constexpr int STEP = 3 * IMG;               // the three pieces of a 32-row step
+    static constexpr int IMG = LP * 64;           // bytes of one piece image (LP columns x 32 rows bf16)
+    static constexpr int STEP = 3 * IMG;          // the three pieces of a 32-row step
     static constexpr int NBUF = STEP * 2 <= 98304 ? 2 : 1;
-    static constexpr int NU = 2 * LP;                  // 4-row x 4-column units of a 32-row step
-    static constexpr int LPT = (NU + 511) / 512;       // ... per thread
+    static constexpr int NU = 2 * LP;             // 4-row x 4-column units of a 32-row step
+    static constexpr int LPT = (NU + THREADS - 1) / THREADS;
+    static_assert(NBK % NH == 0, "group pairs per workgroup");
 };
 
-__device__ __forceinline__ uint32_t f2bf_bits(float x) {  // round to nearest even (finite x)
-    const uint32_t u = __float_as_uint(x);
-    return (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
+// two fp32 -> packed bf16 (round to nearest even): lo = a, hi = b
+__device__ __forceinline__ uint32_t cvt_pk_bf16(float a, float b) {
+    uint32_t r;
+    asm volatile("v_cvt_pk_bf16_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
 }
 
-template <int LP, int WG, int... I>
-__device__ __forceinline__ void gram_split_mma(const char* img, int r, int h, f32x4 (&acc)[GramSplit<LP>::PPW],
-                                               std::integer_sequence<int, I...>) {
+template <int LP>
+__global__ __launch_bounds__(GramSplit<LP>::THREADS) void gram_split_kernel(const float* __restrict__ P, int64_t rows,
+                                                                          int64_t rpc, int nchunk,
+                                                                          double* __restrict__ slabs) {
     typedef GramSplit<LP> G;
-    const uint32_t lo = (uint32_t)(r * 64 + 16 * (h ^ ((r >> 1) & 3)));
-    auto frag = [&](int piece, int t) {
-        return *reinterpret_cast<const bf16x8s*>(img + piece * G::IMG + t * 1024 + lo);
-    };
-    auto one = [&](auto ic) {
-        constexpr int i = decltype(ic)::value, p = WG + G::NW * i;
-        if constexpr (p < G::NP) {
-            constexpr int a = PairOf<G::NT, p>::a, b = PairOf<G::NT, p>::b;
-            const bf16x8s ha = frag(0, a), ma = frag(1, a), ta = frag(2, a);
-            const bf16x8s hb = frag(0, b), mb = frag(1, b), tb = frag(2, b);
-            f32x4 c = acc[i];
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ta, hb, c, 0, 0, 0);  // smallest terms first
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ha, tb, c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ma, mb, c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ma, hb, c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ha, mb, c, 0, 0, 0);
-            acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ha, hb, c, 0, 0, 0);
+    constexpr int TG = G::TG, LPT = G::LPT;
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    const int tid = threadIdx.x, lane = tid & 63, r = lane & 15, h = lane >> 4;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int hb = G::NH == 1 ? 0 : (blockIdx.x >> 3) & (G::NH - 1);
+    const int chunk = G::NH == 1 ? blockIdx.x : ((blockIdx.x & 7) | ((blockIdx.x >> (3 + G::LNH)) << 3));
+    if (chunk >= nchunk) return;
+    const int64_t beg = (int64_t)chunk * rpc;
+    const int64_t end = (beg + rpc < rows) ? beg + rpc : rows;
+    // this wave's group pair (GA <= GB), row-major over the upper triangle of NTG x NTG
+    int GA = 0, GB = 0;
+    {
+        int rem = hb * G::NWW + w;
+        while (rem >= G::NTG - GA) {
+            rem -= G::NTG - GA;
+            ++GA;
         }
-    };
-    (one(std::integral_constant<int, I>{}), ...);
-}
-
-template <int LP, int WG>
-__device__ __forceinline__ void gram_split_body(const float* __restrict__ P, int64_t beg, int64_t end, int chunk,
-                                                double* __restrict__ slabs, char* smem) {
-    typedef GramSplit<LP> G;
-    constexpr int PPW = G::PPW, LPT = G::LPT;
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int r = lane & 15, h = lane >> 4;
-    f32x4 acc[PPW];
-    double acc64[PPW][4];
-#pragma unroll
-    for (int i = 0; i < PPW; ++i) {
-        acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc64[i][j] = 0.0;
+        GB = GA + rem;
     }
-    // thread unit u = tid + 512 t (u < NU): rows kr = 4 (u & 7) .. + 3 of columns 4 (u >> 3) .. + 3
-    // (the 8 lanes of an octet fill one column's 64 B; for a fixed row the octets read 128 B runs)
+    f32x4 acc[TG][TG];
+#pragma unroll
+    for (int i = 0; i < TG; ++i)
+#pragma unroll
+        for (int j = 0; j < TG; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    // thread unit u = tid + THREADS t (u < NU): rows kr = 4 (u & 7) .. + 3 of columns 4 (u >> 3) .. + 3
     float4 reg[LPT][4];
     auto load = [&](int64_t r0) {
 #pragma unroll
         for (int t = 0; t < LPT; ++t) {
-            const int u = tid + 512 * t;
+            const int u = tid + G::THREADS * t;
             const int64_t row = r0 + 4 * (u & 7);
             const int c = 4 * (u >> 3);
 #pragma unroll
@@ -362,9 +362,9 @@ __device__ __forceinline__ void gram_split_body(const float* __restrict__ P, int
     auto stage = [&](char* img) {
 #pragma unroll
         for (int t = 0; t < LPT; ++t) {
-            const int u = tid + 512 * t;
+            const int u = tid + G::THREADS * t;
             if (u >= G::NU) break;
-            const int kr = 4 * (u & 7);  // first of the 4 rows (0..28)
+            const int kr = 4 * (u & 7);
             const int c0 = 4 * (u >> 3);
             const int rot = (u >> 3) & 3;  // octets write columns of alternating parity (LDS banks)
 #pragma unroll
@@ -374,21 +374,17 @@ __device__ __forceinline__ void gram_split_body(const float* __restrict__ P, int
                 uint32_t pw[3][2];
 #pragma unroll
                 for (int q = 0; q < 4; q += 2) {
-                    uint32_t bits[2][3];
-#pragma unroll
-                    for (int e = 0; e < 2; ++e) {
-                        const float4 f = reg[t][q + e];
-                        const float v = i == 0 ? f.x : (i == 1 ? f.y : (i == 2 ? f.z : f.w));
-                        const uint32_t bh = f2bf_bits(v);
-                        const float rm = v - __uint_as_float(bh << 16);
-                        const uint32_t bm = f2bf_bits(rm);
-                        const float rt = rm - __uint_as_float(bm << 16);
-                        bits[e][0] = bh;
-                        bits[e][1] = bm;
-                        bits[e][2] = f2bf_bits(rt);
-                    }
-#pragma unroll
-                    for (int x = 0; x < 3; ++x) pw[x][q >> 1] = bits[0][x] | (bits[1][x] << 16);
+                    const float4 f0 = reg[t][q], f1 = reg[t][q + 1];
+                    const float a = i == 0 ? f0.x : (i == 1 ? f0.y : (i == 2 ? f0.z : f0.w));
+                    const float b = i == 0 ? f1.x : (i == 1 ? f1.y : (i == 2 ? f1.z : f1.w));
+                    // exact three-piece split, two rows at a time: h = bf16(v), m = bf16(v - h), t = v - h - m
+                    const uint32_t ph = cvt_pk_bf16(a, b);
+                    const float ra = a - __uint_as_float(ph << 16), rb = b - __uint_as_float(ph & 0xffff0000u);
+                    const uint32_t pm = cvt_pk_bf16(ra, rb);
+                    const float ta = ra - __uint_as_float(pm << 16), tb = rb - __uint_as_float(pm & 0xffff0000u);
+                    pw[0][q >> 1] = ph;
+                    pw[1][q >> 1] = pm;
+                    pw[2][q >> 1] = cvt_pk_bf16(ta, tb);
                 }
                 // rows kr .. kr + 3 of column c: 8 B inside 16-B unit kr >> 3 (swizzled), offset 8 ((kr >> 2) & 1)
                 const int off = c * 64 + 16 * ((kr >> 3) ^ ((c >> 1) & 3)) + 8 * ((kr >> 2) & 1);
@@ -398,60 +394,56 @@ __device__ __forceinline__ void gram_split_body(const float* __restrict__ P, int
             }
         }
     };
+    const uint32_t lo = (uint32_t)(r * 64 + 16 * (h ^ ((r >> 1) & 3)));
+    auto frag = [&](const char* img, int piece, int t) {
+        return *reinterpret_cast<const bf16x8s*>(img + piece * G::IMG + t * 1024 + lo);
+    };
     int buf = 0;
     if (beg < end) load(beg);
     for (int64_t r0 = beg; r0 < end; r0 += 32) {
-        char* img = smem + buf * G::STEP;
+        char* img = smem_raw + buf * G::STEP;
         if (G::NBUF == 1) __syncthreads();  // single buffer: the previous step's reads are done
         stage(img);
         __syncthreads();
         if (r0 + 32 < end) load(r0 + 32);
-        gram_split_mma<LP, WG>(img, r, h, acc, std::make_integer_sequence<int, PPW>{});
+        bf16x8s fa[TG][3];
 #pragma unroll
-        for (int i = 0; i < PPW; ++i) {
+        for (int i = 0; i < TG; ++i)
 #pragma unroll
-            for (int j = 0; j < 4; ++j) acc64[i][j] += (double)acc[i][j];
-            acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+            for (int x = 0; x < 3; ++x) fa[i][x] = frag(img, x, GA * TG + i);
+#pragma unroll
+        for (int j = 0; j < TG; ++j) {
+            const bf16x8s hb_ = frag(img, 0, GB * TG + j), mb = frag(img, 1, GB * TG + j), tb = frag(img, 2, GB * TG + j);
+#pragma unroll
+            for (int i = 0; i < TG; ++i) {
+                f32x4 c = acc[i][j];
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][2], hb_, c, 0, 0, 0);  // smallest terms first
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], tb, c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][1], mb, c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][1], hb_, c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], mb, c, 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], hb_, c, 0, 0, 0);
+            }
         }
         buf = G::NBUF - 1 - buf;
     }
 #pragma unroll
-    for (int i = 0; i < PPW; ++i) {
-        const int p = WG + G::NW * i;
-        if (p < G::NP) {
-            const int ta = pair_ta(G::NT, p), tb = pair_tb(G::NT, p);
+    for (int i = 0; i < TG; ++i)
+#pragma unroll
+        for (int j = 0; j < TG; ++j) {
+            const int ta = GA * TG + i, tb = GB * TG + j;
+            if (ta > tb) continue;  // (diagonal group pairs) the mirror of an upper pair
             const int a = ta >> 1, b = tb >> 1;
             const int blk = a * G::NB - a * (a - 1) / 2 + (b - a);
             double* dst = slabs + ((int64_t)chunk * G::NBLK + blk) * 1024;
             const bool mirror = (a == b) && (ta != tb);
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {  // bf16 MFMA D: col = lane & 15, row = 4 h + j
-                const int li = 16 * (ta & 1) + 4 * h + j, lj = 16 * (tb & 1) + r;
-                dst[li * 32 + lj] = acc64[i][j];
-                if (mirror) dst[lj * 32 + li] = acc64[i][j];
+            for (int e = 0; e < 4; ++e) {  // bf16 MFMA D: col = lane & 15, row = 4 h + e
+                const int li = 16 * (ta & 1) + 4 * h + e, lj = 16 * (tb & 1) + r;
+                dst[li * 32 + lj] = (double)acc[i][j][e];
+                if (mirror) dst[lj * 32 + li] = (double)acc[i][j][e];
             }
         }
-    }
-}
-
-template <int LP, int... W>
-__device__ __forceinline__ void gram_split_dispatch(int wg, const float* P, int64_t beg, int64_t end, int chunk,
-                                                    double* slabs, char* smem, std::integer_sequence<int, W...>) {
-    ((wg == W ? gram_split_body<LP, W>(P, beg, end, chunk, slabs, smem) : void()), ...);
-}
-
-template <int LP>
-__global__ __launch_bounds__(512) void gram_split_kernel(const float* __restrict__ P, int64_t rows, int64_t rpc,
-                                                         int nchunk, double* __restrict__ slabs) {
-    typedef GramSplit<LP> G;
-    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int hb = G::NH == 1 ? 0 : (blockIdx.x >> 3) & (G::NH - 1);
-    const int chunk = G::NH == 1 ? blockIdx.x : ((blockIdx.x & 7) | ((blockIdx.x >> (3 + G::LNH)) << 3));
-    if (chunk >= nchunk) return;
-    const int64_t beg = (int64_t)chunk * rpc;
-    const int64_t end = (beg + rpc < rows) ? beg + rpc : rows;
-    gram_split_dispatch<LP>(w * G::NH + hb, P, beg, end, chunk, slabs, smem_raw, std::make_integer_sequence<int, G::NW>{});
 }
 
 __global__ void gram_reduce_kernel(const double* __restrict__ slabs, int nblk, int nchunk, int LP, int cross,
@@ -1218,6 +1210,173 @@ __global__ __launch_bounds__(256) void panel_gemm_kernel(const T* __restrict__ I
 }
 
 // ------------------------------------------------------------------------------------------------
+// Out = In * M for fp32 panels on the bf16 MFMA (panel_split_kernel): the three-piece split of
+// the Gram kernel on both operands (In = h + m + t per element in registers, M pre-split into
+// transposed piece images Mt[x][c][k] by split_mat_kernel) and the six products hH, hM, mH, mM,
+// hT, tH per 32-deep k-step -- each term exact in fp32, the fp32 accumulation as the fp32 MFMA's.
+// Six bf16 MFMAs cost 6/16 of one fp32 MFMA of the same shape: the product becomes a read of In
+// plus the writes.  Workgroup: 128 rows x 128 columns (4 waves x 32 rows, 8 column tiles), M's
+// 32 x 128 piece chunk staged in LDS per k-step (double-buffered, 64-B columns, 16-B units
+// swizzled by (c >> 1) & 3 as the Gram images), In's fragment (8 consecutive k of one row) loaded
+// one k-step ahead.  Upper-triangular M: K stops at the block's last column.
+__global__ void split_mat_kernel(const float* __restrict__ M, int LP, bf16_t* __restrict__ Mt) {
+    // Mt[x][c][k] = piece x of M[k][c]
+    const int64_t L2 = (int64_t)LP * LP;
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < L2; e += (int64_t)gridDim.x * blockDim.x) {
+        const int c = (int)(e / LP), k = (int)(e % LP);
+        const float v = M[(int64_t)k * LP + c];
+        const bf16_t bh = f2bf(v);
+        const float rm = v - bf2f(bh);
+        const bf16_t bm = f2bf(rm);
+        Mt[e] = bh;
+        Mt[L2 + e] = bm;
+        Mt[2 * L2 + e] = f2bf(rm - bf2f(bm));
+    }
+}
+
+__global__ __launch_bounds__(256) void panel_split_kernel(const float* __restrict__ In, int64_t rows, int LP,
+                                                          const bf16_t* __restrict__ Mt, int upper,
+                                                          float* __restrict__ Out, int64_t ldo, int cols,
+                                                          bf16_t* __restrict__ hi, bf16_t* __restrict__ lo, int ncb,
+                                                          const int* __restrict__ pred) {
+    if (pred && *pred == 0) return;
+    // workgroup tile 128 rows x 128 columns: wave w owns rows 32 w .. + 31 (two 16-row tiles), so
+    // each staged M chunk (24 KiB) feeds 128 rows
+    constexpr int CT = 128, G = CT / 16, RT2 = 2, IMG = CT * 64, STEPB = 3 * IMG;
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int r = lane & 15, h = lane >> 4;
+    const int bid = xcd_remap(blockIdx.x, gridDim.x);
+    const int cb = bid % ncb;
+    const int64_t row0 = (int64_t)(bid / ncb) * 128;
+    const int c0 = cb * CT;
+    const int kmax = upper ? ((c0 + CT < LP) ? c0 + CT : LP) : LP;
+    const int nk = (kmax + 31) / 32;
+    const int64_t L2 = (int64_t)LP * LP;
+    f32x4 acc[RT2][G];
+#pragma unroll
+    for (int t = 0; t < RT2; ++t)
+#pragma unroll
+        for (int g = 0; g < G; ++g) acc[t][g] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // M chunk staging: 3 pieces x 128 columns x 64 B = 1536 16-B units, 6 per thread
+    auto stage = [&](int ks, char* img) {
+#pragma unroll
+        for (int t = 0; t < 6; ++t) {
+            const int u = tid + 256 * t;
+            const int x = u / 512, rem = u % 512, c = rem >> 2, un = rem & 3;
+            uint4 v = make_uint4(0u, 0u, 0u, 0u);
+            if (c0 + c < LP) v = *reinterpret_cast<const uint4*>(Mt + x * L2 + (int64_t)(c0 + c) * LP + 32 * ks + 8 * un);
+            *reinterpret_cast<uint4*>(img + x * IMG + c * 64 + 16 * (un ^ ((c >> 1) & 3))) = v;
+        }
+    };
+    // In vectors of this / the next k-step (swapped, never indexed at run time)
+    float4 cur[RT2][2], nxt[RT2][2];
+    auto loadA = [&](int ks, float4 (&a)[RT2][2]) {
+        const int k = 32 * ks + 8 * h;
+#pragma unroll
+        for (int t = 0; t < RT2; ++t) {
+            const int64_t row = row0 + 32 * w + 16 * t + r;
+            if (row < rows && k < LP) {
+                a[t][0] = *reinterpret_cast<const float4*>(In + row * LP + k);
+                a[t][1] = *reinterpret_cast<const float4*>(In + row * LP + k + 4);
+            } else {
+                a[t][0] = a[t][1] = make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+        }
+    };
+    const uint32_t lofs = (uint32_t)(r * 64 + 16 * (h ^ ((r >> 1) & 3)));
+    if (nk > 0) {
+        loadA(0, cur);
+        stage(0, smem_raw);
+    }
+    for (int ks = 0; ks < nk; ++ks) {
+        char* img = smem_raw + (ks & 1) * STEPB;
+        __syncthreads();  // chunk ks staged; chunk ks - 1's readers are done
+        if (ks + 1 < nk) {
+            loadA(ks + 1, nxt);
+            stage(ks + 1, smem_raw + ((ks + 1) & 1) * STEPB);
+        }
+        // In fragments of this k-step: three pieces of 8 consecutive k of the lane's row, per row tile
+        bf16x8s fa[RT2][3];
+#pragma unroll
+        for (int t = 0; t < RT2; ++t) {
+            const float v[8] = {cur[t][0].x, cur[t][0].y, cur[t][0].z, cur[t][0].w,
+                                cur[t][1].x, cur[t][1].y, cur[t][1].z, cur[t][1].w};
+            uint32_t ph[4], pm[4], pt[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                ph[j] = cvt_pk_bf16(v[2 * j], v[2 * j + 1]);
+                const float ra = v[2 * j] - __uint_as_float(ph[j] << 16);
+                const float rb = v[2 * j + 1] - __uint_as_float(ph[j] & 0xffff0000u);
+                pm[j] = cvt_pk_bf16(ra, rb);
+                pt[j] = cvt_pk_bf16(ra - __uint_as_float(pm[j] << 16), rb - __uint_as_float(pm[j] & 0xffff0000u));
+            }
+            fa[t][0] = __builtin_bit_cast(bf16x8s, make_uint4(ph[0], ph[1], ph[2], ph[3]));
+            fa[t][1] = __builtin_bit_cast(bf16x8s, make_uint4(pm[0], pm[1], pm[2], pm[3]));
+            fa[t][2] = __builtin_bit_cast(bf16x8s, make_uint4(pt[0], pt[1], pt[2], pt[3]));
+        }
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const char* base = img + g * 1024 + lofs;
+            const bf16x8s bh = *reinterpret_cast<const bf16x8s*>(base);
+            const bf16x8s bm = *reinterpret_cast<const bf16x8s*>(base + IMG);
+            const bf16x8s bt = *reinterpret_cast<const bf16x8s*>(base + 2 * IMG);
+#pragma unroll
+            for (int t = 0; t < RT2; ++t) {
+                f32x4 c = acc[t][g];
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[t][2], bh, c, 0, 0, 0);  // smallest terms first
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[t][0], bt, c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[t][1], bm, c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[t][1], bh, c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[t][0], bm, c, 0, 0, 0);
+                acc[t][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[t][0], bh, c, 0, 0, 0);
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < RT2; ++t) {
+            cur[t][0] = nxt[t][0];
+            cur[t][1] = nxt[t][1];
+        }
+    }
+    // epilogue.  bf16 MFMA D: col = r (output column c0 + 16 g + r), row = 4 h + j within the 16-row tile
+    if (ldo == 0) {
+#pragma unroll
+        for (int t = 0; t < RT2; ++t)
+#pragma unroll
+            for (int g = 0; g < G; ++g)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const int64_t orow = row0 + 32 * w + 16 * t + 4 * h + j;
+                    const int c = c0 + 16 * g + r;
+                    if (orow < rows && c < LP) {
+                        const float v = acc[t][g][j];
+                        if (Out) Out[orow * LP + c] = v;
+                        if (hi) {
+                            const bf16_t bh = f2bf(v);
+                            hi[orow * LP + c] = bh;
+                            if (lo) lo[orow * LP + c] = f2bf(v - bf2f(bh));
+                        }
+                    }
+                }
+        return;
+    }
+    // column-major caller output: transpose through LDS, store column segments contiguously
+    __syncthreads();
+    float* Ts = reinterpret_cast<float*>(smem_raw);  // [CT][128 + 1]
+#pragma unroll
+    for (int t = 0; t < RT2; ++t)
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) Ts[(16 * g + r) * 129 + 32 * w + 16 * t + 4 * h + j] = acc[t][g][j];
+    __syncthreads();
+    for (int e = tid; e < CT * 128; e += 256) {
+        const int c = e / 128, lr = e % 128;
+        if (c0 + c < cols && row0 + lr < rows) Out[row0 + lr + (int64_t)(c0 + c) * ldo] = Ts[c * 129 + lr];
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
 template <typename T>
 __global__ void repair_kernel(const T* __restrict__ Q, int64_t rows, int l, int LP, const int* __restrict__ colflag,
                               const int* __restrict__ flag, uint64_t seed, int64_t row_off, int64_t rows_total,
@@ -1380,16 +1539,16 @@ bool gram_split_ok(int LP) { return LP == 128 || LP == 256 || LP == 512; }
 hipError_t launch_gram_split(const float* P, int64_t rows, int LP, const GramPlan& gp, double* slabs, double* G,
                              hipStream_t s) {
     if (!gram_split_ok(LP)) return hipErrorInvalidValue;
-    const int grid = LP == 128 ? gp.chunks : (gp.chunks + 7) / 8 * 8 * (LP == 256 ? 2 : 8);
-    if (LP == 128)
-        hipLaunchKernelGGL(gram_split_kernel<128>, dim3(grid), dim3(512),
-                           GramSplit<128>::NBUF * GramSplit<128>::STEP, s, P, rows, gp.rows_per_chunk, gp.chunks, slabs);
-    else if (LP == 256)
-        hipLaunchKernelGGL(gram_split_kernel<256>, dim3(grid), dim3(512),
-                           GramSplit<256>::NBUF * GramSplit<256>::STEP, s, P, rows, gp.rows_per_chunk, gp.chunks, slabs);
-    else
-        hipLaunchKernelGGL(gram_split_kernel<512>, dim3(grid), dim3(512),
-                           GramSplit<512>::NBUF * GramSplit<512>::STEP, s, P, rows, gp.rows_per_chunk, gp.chunks, slabs);
+    auto go = [&](auto lpc) {
+        constexpr int L = decltype(lpc)::value;
+        typedef GramSplit<L> GS;
+        const int grid = GS::NH == 1 ? gp.chunks : (gp.chunks + 7) / 8 * 8 * GS::NH;
+        hipLaunchKernelGGL(gram_split_kernel<L>, dim3(grid), dim3(GS::THREADS), GS::NBUF * GS::STEP, s, P, rows,
+                           gp.rows_per_chunk, gp.chunks, slabs);
+    };
+    if (LP == 128) go(std::integral_constant<int, 128>{});
+    else if (LP == 256) go(std::integral_constant<int, 256>{});
+    else go(std::integral_constant<int, 512>{});
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const int64_t tot = (int64_t)gp.blocks * 1024;
@@ -1469,9 +1628,40 @@ __global__ void chol2_assemble_kernel(const double* __restrict__ R11, const doub
     if (ill && i == 0 && c == 0 && *ill2) *ill = 1;
 }
 
-// row-major C (M x N, ldc) = alpha op(A) op(B) + beta C through the column-major GEMM (C^T = op(B)^T op(A)^T)
+// row-major C (256 x 256, ldc) = alpha op(A) B + beta C (op(A) = A or A^T; A, B 256 x 256 row-major
+// with ld lda / ldb): one wave per 16 x 16 output tile (256 workgroups -- the 64 x 64-tile general
+// GEMM kept 16 CUs busy, 56 us per product), four independent fp64 MFMA chains over K = 256, every
+// operand an L2 hit.
+__global__ __launch_bounds__(64) void gemm256_f64_kernel(int ta, double alpha, const double* __restrict__ A, int lda,
+                                                         const double* __restrict__ B, int ldb, double beta,
+                                                         double* __restrict__ C, int ldc) {
+    const int lane = threadIdx.x, r = lane & 15, h = lane >> 4;
+    const int i0 = 16 * (blockIdx.x >> 4), j0 = 16 * (blockIdx.x & 15);
+    f64x4 acc[4] = {MD::zero(), MD::zero(), MD::zero(), MD::zero()};
+#pragma unroll 4
+    for (int k0 = 0; k0 < 256; k0 += 16) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int k = k0 + 4 * u + h;
+            const double a = ta ? A[(int64_t)k * lda + i0 + r] : A[(int64_t)(i0 + r) * lda + k];
+            acc[u] = MD::mma(a, B[(int64_t)k * ldb + j0 + r], acc[u]);
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {  // f64 D: col = r, row = h + 4 j
+        double* c = C + (int64_t)(i0 + MD::row(h, j)) * ldc + j0 + r;
+        const double v = alpha * ((acc[0][j] + acc[1][j]) + (acc[2][j] + acc[3][j]));
+        *c = beta == 0.0 ? v : v + beta * *c;
+    }
+}
+
 static hipError_t gemm_rm(int ta, int tb, int M, int N, int K, double alpha, const double* A, int lda,
                           const double* B, int ldb, double beta, double* C, int ldc, hipStream_t s) {
+    if (M == 256 && N == 256 && K == 256 && tb == 0) {
+        hipLaunchKernelGGL(gemm256_f64_kernel, dim3(256), dim3(64), 0, s, ta, alpha, A, lda, B, ldb, beta, C, ldc);
+        return hipGetLastError();
+    }
+    // row-major C = op(A) op(B) through the column-major GEMM (C^T = op(B)^T op(A)^T)
     return launch_gemm<double>(tb, ta, N, M, K, alpha, B, ldb, A, lda, beta, C, ldc, s);
 }
 
@@ -1513,9 +1703,23 @@ hipError_t launch_chol_wide_2level(const double* G, int l, double tol, double* R
 
 template <typename T>
 hipError_t launch_panel_gemm(const T* In, int64_t rows, int LP, const T* Mm, int upper, T* Out, int64_t ldo,
-                             int cols, bf16_t* hi, bf16_t* lo, const int* pred, hipStream_t s) {
+                             int cols, bf16_t* hi, bf16_t* lo, const int* pred, hipStream_t s, bf16_t* msplit) {
     if (!Mm || LP % 16 || (!Out && (ldo != 0 || !hi))) return hipErrorInvalidValue;
     const int64_t rb = (rows + 63) / 64;
+    if constexpr (sizeof(T) == 4) {
+        if (msplit && LP % 32 == 0 && LP >= 128) {  // the bf16-split product (panel_split_kernel)
+            const int64_t L2 = (int64_t)LP * LP;
+            hipLaunchKernelGGL(split_mat_kernel, dim3((unsigned)std::min<int64_t>((L2 + 255) / 256, 1024)), dim3(256), 0,
+                               s, reinterpret_cast<const float*>(Mm), LP, msplit);
+            const int ncb = (LP + 127) / 128;
+            const int64_t rb2 = (rows + 127) / 128;
+            const size_t lds = std::max<size_t>((size_t)2 * 3 * 128 * 64, (size_t)128 * 129 * 4);
+            hipLaunchKernelGGL(panel_split_kernel, dim3((unsigned)(rb2 * ncb)), dim3(256), lds, s,
+                               reinterpret_cast<const float*>(In), rows, LP, msplit, upper,
+                               reinterpret_cast<float*>(Out), ldo, cols, hi, lo, ncb, pred);
+            return hipGetLastError();
+        }
+    }
 #define GO(CT)                                                                                                  \
     {                                                                                                           \
         const int ncb = (LP + CT - 1) / CT;                                                                     \
@@ -1579,7 +1783,7 @@ hipError_t launch_convert_scale(const double* x, T* y, int n, double sc, hipStre
     template hipError_t launch_gram_wide<T>(const T*, const T*, int64_t, int, const GramPlan&, double*, double*,    \
                                             const int*, hipStream_t);                                               \
     template hipError_t launch_panel_gemm<T>(const T*, int64_t, int, const T*, int, T*, int64_t, int, bf16_t*,      \
-                                             bf16_t*, const int*, hipStream_t);                                     \
+                                             bf16_t*, const int*, hipStream_t, bf16_t*);                            \
     template hipError_t launch_repair_panel<T>(const T*, int64_t, int, int, const int*, const int*, uint64_t,       \
                                                int64_t, int64_t, int64_t, T*, hipStream_t, int64_t);                \
     template hipError_t launch_split_bf16<T>(const T*, int64_t, int, bf16_t*, bf16_t*, hipStream_t);

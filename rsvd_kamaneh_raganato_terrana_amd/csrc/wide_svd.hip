@@ -32,8 +32,8 @@
 // cooperatively (launch_coresident): co-resident by the runtime's guarantee; every spin is still
 // bounded and reports a timeout instead of hanging.
 // Convergence: a sweep whose rotations all had cos^2 = g^2 / (ab) <= quad2 ends the iteration (the
-// next would only square them); and when a sweep's largest pre-rotation cosine is <= sqrt(tol_chk)
-// (quadratic convergence: small enough to have squared below tol_chk), the whole grid checks max cos
+// next would only square them); and when a sweep's largest pre-rotation cosine is <= 10 sqrt(tol_chk)
+// (quadratic convergence: close to having squared below tol_chk), the whole grid checks max cos
 // over ALL column pairs of the new X
 // (an LP x LP fp64 MFMA Gram, every workgroup a 32-column slice) and stops at <= tol_chk -- which
 // saves the confirming sweep the first rule needs.
@@ -598,7 +598,9 @@ __global__ __launch_bounds__(kBJThreads) void block_jacobi_kernel(const double* 
         if (rot == 0 || big == 0) break;
         // the global check, once the sweep's rotations were small enough to have squared below tol_chk2
         const double pre = u64_as_double(__hip_atomic_load(smax + sweep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-        if (tol_chk2 > 0.0 && pre <= sqrt(tol_chk2)) {  // pre-rotation cos <= sqrt(tol): squared below ~tol
+        // (triggered at a pre-rotation cos^2 100x above sqrt(tol): a failed check costs one LP x LP
+        // Gram and a barrier, a missed one a whole sweep -- the C4 solve sat on the 7 / 8 sweep border)
+        if (tol_chk2 > 0.0 && pre <= 100.0 * sqrt(tol_chk2)) {
             const double mx = slice_max_cos2(Xb + (size_t)par * L2X, MR, LP, pr, g, G, w, lane, negl);
             if (tid == 0) lmax = 0ull;
             __syncthreads();

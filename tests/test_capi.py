@@ -89,7 +89,7 @@ def test_workspace_bytes_and_argument_checks(lib):
     assert lib.rsvd_workspace_bytes(ctypes.byref(_desc(dtype=_capi.F64)), ctypes.byref(nb64)) == 0
     assert nb64.value > nb.value
     # 1 = RSVD_ERR_INVALID_ARG, 2 = RSVD_ERR_UNSUPPORTED
-    for bad, code in ((dict(l=0), 1), (dict(q=-1), 1), (dict(lda=100), 1), (dict(l=513), 2), (dict(m=10, l=16), 2),
+    for bad, code in ((dict(l=0), 1), (dict(q=-1), 1), (dict(lda=100), 1), (dict(l=4097), 2), (dict(m=10, l=16), 2),
                       (dict(dtype=7), 2), (dict(method=7), 2), (dict(flags=4), 1)):
         assert lib.rsvd_workspace_bytes(ctypes.byref(_desc(**bad)), ctypes.byref(nb)) == code, bad
     assert lib.rsvd_workspace_bytes(ctypes.byref(_desc(flags=_capi.FLAG_LOWP_INTERMEDIATES)), ctypes.byref(nb)) == 0
