@@ -390,11 +390,15 @@ def main():
     lowp = dt in ("bf16", "fp8")
     per_op = 1  # kernel dispatches per timed projection (the HIP events bracket the whole product)
     if lowp:  # the LDS-DMA kernels (hi/lo split skinny operand): wproj3 (bf16, LP 256 / 512; TN at
-        # LP 256 with two-step A slots: wproj3tn2), wproj2<FP8, NN, LP, SPLIT> otherwise
+        # LP 256 with two-step A slots: wproj3tn2), wproj3tn4 (e4m3 TN, four-step A slots),
+        # wproj2<FP8, NN, LP, SPLIT> otherwise
         nn = kname.startswith("proj_nn")
         LPk = lp_pad(l)
         if dt == "bf16" and LPk == 256 and not nn:
             kpref = "wproj3tn2_kernel<true"
+        elif dt == "fp8" and LPk in (256, 512) and not nn and os.environ.get("RSVD_FP8_TN4") != "0":
+            kpref = "wproj3tn4_kernel<true"  # e4m3 TN, 128-B A lines; LP = 512 as two column halves
+            per_op = LPk // 256
         elif dt == "bf16" and LPk in (256, 512):
             kpref = f"wproj3_kernel<{'true' if nn else 'false'}, {LPk}, true"
         elif dt == "fp8" and LPk == 512:  # two 256-column half launches per product (WProjPlan::half)

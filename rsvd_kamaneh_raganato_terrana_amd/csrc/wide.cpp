@@ -286,7 +286,11 @@ struct WideEngine {
     bool split_panel = false;  // panel products on the bf16 MFMA, three-piece split (RSVD_PANEL_SPLIT=0: fp32 MFMA)
     bf16_t* Ms = nullptr;
     bf16_t* ms() const { return split_panel ? Ms : nullptr; }
-    bool chol2 = true;  // two-level factor at LP = 512 (RSVD_CHOL2=0: the one-workgroup LP = 512 kernel)
+    // two-level factor: bit 0 at LP = 512, bit 1 at LP = 256 (RSVD_CHOL2 overrides; 0: one level
+    // everywhere).  Default LP = 512 only: at LP = 256 two chol_reg<8> levels (70 us each) + four
+    // 128^3 products (14 us each, latency-bound) lose to the one-level 175 us factor (C4 28.63 vs
+    // 28.88 ms on the same box)
+    int chol2 = 1;
     // panel_gemm's operand in the panel precision: fp64 matrices as-is, fp32 copies for fp32 panels
     const T* mat(const double* m64, const float* m32) const {
         if constexpr (sizeof(T) == 8) return m64; else return m32;
@@ -300,11 +304,12 @@ struct WideEngine {
     int cholqr_pass(const T* P, int64_t rows, const GramPlan& gp, T* Out, bool sharded, bf16_t* hi, bf16_t* lo,
                     int* flag, const int* pred) {
         float* r32 = sizeof(T) == 4 ? Rinv32 : nullptr;
-        // LP = 512, l > 256: the two-level factor (wide_qr.hip launch_chol_wide_2level; JX is free
-        // scratch until the small SVD) for unpredicated passes
-        const bool two = chol2 && L.LP == 512 && L.l > 256;
+        // LP = 256 / 512, l > LP / 2: the two-level factor (wide_qr.hip launch_chol_wide_2level; JX is
+        // free scratch until the small SVD) for unpredicated passes
+        const bool two = (chol2 & (L.LP == 512 ? 1 : (L.LP == 256 ? 2 : 0))) && L.l > L.LP / 2;
         auto factor = [&](int* fl, double ill_tol, int* ill) -> hipError_t {
-            if (two) return launch_chol_wide_2level(G, L.l, tol(), R, Rinv, r32, colflag, fl, W, JX, s, ill_tol, ill);
+            if (two)
+                return launch_chol_wide_2level(G, L.l, L.LP, tol(), R, Rinv, r32, colflag, fl, W, JX, s, ill_tol, ill);
             return launch_chol_wide(G, L.l, L.LP, tol(), R, Rinv, r32, colflag, fl, W, nullptr, s, ill_tol, ill);
         };
         if (split_gram && !sharded && !pred) {
@@ -516,7 +521,7 @@ int wide_typed(rsvd_handle_t h, const rsvd_desc_t* d, const void* A, const void*
             const char* v = std::getenv("RSVD_CHOL2");
             return v ? std::atoi(v) : 1;
         }();
-        E.chol2 = env2 != 0;
+        E.chol2 = env2;
         static const int env3 = [] {
             const char* v = std::getenv("RSVD_PANEL_SPLIT");
             return v ? std::atoi(v) : 1;

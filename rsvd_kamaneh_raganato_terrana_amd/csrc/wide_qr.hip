@@ -1584,62 +1584,63 @@ hipError_t launch_chol_wide(const double* G, int l, int LP, double tol, double* 
     return hipGetLastError();
 }
 
-// ---- two-level LP = 512 factor (launch_chol_wide_2level) ----------------------------------------
-// Ga = G11, Sb = G22 (256 x 256, ld 256), d0b = diag(G22): the breakdown / ill tests of the second
-// level judge S's pivots against G's own diagonal, as the one-level factor does
-__global__ void chol2_prep_kernel(const double* __restrict__ G, double* __restrict__ Ga, double* __restrict__ Sb,
+// ---- two-level factor, LP = 2 B (launch_chol_wide_2level) ----------------------------------------
+// Ga = G11, Sb = G22 (B x B, ld B), d0b = diag(G22): the breakdown / ill tests of the second level
+// judge S's pivots against G's own diagonal, as the one-level factor does
+__global__ void chol2_prep_kernel(const double* __restrict__ G, int B, double* __restrict__ Ga, double* __restrict__ Sb,
                                   double* __restrict__ d0b) {
-    const int i = blockIdx.x, c = threadIdx.x;  // 256 x 256
-    Ga[i * 256 + c] = G[(int64_t)i * 512 + c];
-    Sb[i * 256 + c] = G[(int64_t)(256 + i) * 512 + 256 + c];
-    if (c == 0) d0b[i] = G[(int64_t)(256 + i) * 512 + 256 + i];
+    const int i = blockIdx.x, c = threadIdx.x, LP = 2 * B;  // B x B
+    Ga[i * B + c] = G[(int64_t)i * LP + c];
+    Sb[i * B + c] = G[(int64_t)(B + i) * LP + B + c];
+    if (c == 0) d0b[i] = G[(int64_t)(B + i) * LP + B + i];
 }
-// rows of R12 (row-major, ld 512) whose first-level pivot broke down are zero, as the one-level
+// rows of R12 (row-major, ld 2 B) whose first-level pivot broke down are zero, as the one-level
 // factor's strips are
-__global__ void chol2_zero_rows_kernel(double* __restrict__ R12, const int* __restrict__ colflag) {
+__global__ void chol2_zero_rows_kernel(double* __restrict__ R12, int B, const int* __restrict__ colflag) {
     const int i = blockIdx.x, c = threadIdx.x;
-    if (colflag[i]) R12[(int64_t)i * 512 + c] = 0.0;
+    if (colflag[i]) R12[(int64_t)i * 2 * B + c] = 0.0;
 }
-// R / Rinv (512 x 512 row-major) from the level blocks; Rinv32 the fp32 copy; ill = ill1 | ill2
+// R / Rinv (2B x 2B row-major) from the level blocks; Rinv32 the fp32 copy; ill = ill1 | ill2
 __global__ void chol2_assemble_kernel(const double* __restrict__ R11, const double* __restrict__ Ri11,
-                                      const double* __restrict__ R22, const double* __restrict__ Ri22,
+                                      const double* __restrict__ R22, const double* __restrict__ Ri22, int B,
                                       double* __restrict__ R, double* __restrict__ Rinv, float* __restrict__ Rinv32,
                                       const int* __restrict__ ill2, int* __restrict__ ill) {
-    const int i = blockIdx.x, c = threadIdx.x;  // 512 x 256: columns c and c + 256 of row i
-    const int64_t o = (int64_t)i * 512;
-    if (i < 256) {
-        R[o + c] = R11[i * 256 + c];
-        Rinv[o + c] = Ri11[i * 256 + c];
+    const int i = blockIdx.x, c = threadIdx.x;  // 2B x B: columns c and c + B of row i
+    const int64_t o = (int64_t)i * 2 * B;
+    if (i < B) {
+        R[o + c] = R11[i * B + c];
+        Rinv[o + c] = Ri11[i * B + c];
         if (Rinv32) {
-            Rinv32[o + c] = (float)Ri11[i * 256 + c];
-            Rinv32[o + 256 + c] = (float)Rinv[o + 256 + c];
+            Rinv32[o + c] = (float)Ri11[i * B + c];
+            Rinv32[o + B + c] = (float)Rinv[o + B + c];
         }
     } else {
-        const int i2 = i - 256;
+        const int i2 = i - B;
         R[o + c] = 0.0;
         Rinv[o + c] = 0.0;
-        R[o + 256 + c] = R22[i2 * 256 + c];
-        Rinv[o + 256 + c] = Ri22[i2 * 256 + c];
+        R[o + B + c] = R22[i2 * B + c];
+        Rinv[o + B + c] = Ri22[i2 * B + c];
         if (Rinv32) {
             Rinv32[o + c] = 0.f;
-            Rinv32[o + 256 + c] = (float)Ri22[i2 * 256 + c];
+            Rinv32[o + B + c] = (float)Ri22[i2 * B + c];
         }
     }
     if (ill && i == 0 && c == 0 && *ill2) *ill = 1;
 }
 
-// row-major C (256 x 256, ldc) = alpha op(A) B + beta C (op(A) = A or A^T; A, B 256 x 256 row-major
-// with ld lda / ldb): one wave per 16 x 16 output tile (256 workgroups -- the 64 x 64-tile general
-// GEMM kept 16 CUs busy, 56 us per product), four independent fp64 MFMA chains over K = 256, every
-// operand an L2 hit.
-__global__ __launch_bounds__(64) void gemm256_f64_kernel(int ta, double alpha, const double* __restrict__ A, int lda,
-                                                         const double* __restrict__ B, int ldb, double beta,
-                                                         double* __restrict__ C, int ldc) {
+// row-major C (N x N, ldc) = alpha op(A) B + beta C, N = K in {128, 256} (op(A) = A or A^T; A, B
+// row-major with ld lda / ldb): one wave per 16 x 16 output tile ((N / 16)^2 workgroups -- the
+// 64 x 64-tile general GEMM kept 16 CUs busy, 56 us per 256^3 product), four independent fp64 MFMA
+// chains over K, every operand an L2 hit.
+__global__ __launch_bounds__(64) void gemmsq_f64_kernel(int N, int ta, double alpha, const double* __restrict__ A,
+                                                        int lda, const double* __restrict__ B, int ldb, double beta,
+                                                        double* __restrict__ C, int ldc) {
     const int lane = threadIdx.x, r = lane & 15, h = lane >> 4;
-    const int i0 = 16 * (blockIdx.x >> 4), j0 = 16 * (blockIdx.x & 15);
+    const int nt = N / 16;
+    const int i0 = 16 * (blockIdx.x / nt), j0 = 16 * (blockIdx.x % nt);
     f64x4 acc[4] = {MD::zero(), MD::zero(), MD::zero(), MD::zero()};
 #pragma unroll 4
-    for (int k0 = 0; k0 < 256; k0 += 16) {
+    for (int k0 = 0; k0 < N; k0 += 16) {
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const int k = k0 + 4 * u + h;
@@ -1655,47 +1656,40 @@ __global__ __launch_bounds__(64) void gemm256_f64_kernel(int ta, double alpha, c
     }
 }
 
-static hipError_t gemm_rm(int ta, int tb, int M, int N, int K, double alpha, const double* A, int lda,
-                          const double* B, int ldb, double beta, double* C, int ldc, hipStream_t s) {
-    if (M == 256 && N == 256 && K == 256 && tb == 0) {
-        hipLaunchKernelGGL(gemm256_f64_kernel, dim3(256), dim3(64), 0, s, ta, alpha, A, lda, B, ldb, beta, C, ldc);
-        return hipGetLastError();
-    }
-    // row-major C = op(A) op(B) through the column-major GEMM (C^T = op(B)^T op(A)^T)
-    return launch_gemm<double>(tb, ta, N, M, K, alpha, B, ldb, A, lda, beta, C, ldc, s);
+static hipError_t gemm_sq(int N, int ta, double alpha, const double* A, int lda, const double* B, int ldb, double beta,
+                          double* C, int ldc, hipStream_t s) {
+    hipLaunchKernelGGL(gemmsq_f64_kernel, dim3((N / 16) * (N / 16)), dim3(64), 0, s, N, ta, alpha, A, lda, B, ldb,
+                       beta, C, ldc);
+    return hipGetLastError();
 }
 
-hipError_t launch_chol_wide_2level(const double* G, int l, double tol, double* R, double* Rinv, float* Rinv32,
-                                   int* colflag, int* flag, double* work, double* scratch, hipStream_t s,
-                                   double ill_tol, int* ill) {
-    if (l <= 256 || l > 512) return hipErrorInvalidValue;
-    constexpr int B = 256, B2 = B * B;
+hipError_t launch_chol_wide_2level(const double* G, int l, int LP, double tol, double* R, double* Rinv,
+                                   float* Rinv32, int* colflag, int* flag, double* work, double* scratch,
+                                   hipStream_t s, double ill_tol, int* ill) {
+    if ((LP != 256 && LP != 512) || l <= LP / 2 || l > LP) return hipErrorInvalidValue;
+    const int B = LP / 2, B2 = B * B;
     double *Ga = scratch, *R11 = Ga + B2, *Ri11 = R11 + B2, *Sb = Ri11 + B2, *R22 = Sb + B2, *Ri22 = R22 + B2,
            *T = Ri22 + B2, *d0b = T + B2;
-    int* ill2 = reinterpret_cast<int*>(d0b + 256);
-    hipLaunchKernelGGL(chol2_prep_kernel, dim3(B), dim3(B), 0, s, G, Ga, Sb, d0b);
+    int* ill2 = reinterpret_cast<int*>(d0b + B);
+    hipLaunchKernelGGL(chol2_prep_kernel, dim3(B), dim3(B), 0, s, G, B, Ga, Sb, d0b);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    // level 1: R11, Ri11 = chol(G11) (columns 0 .. 255 of colflag)
+    // level 1: R11, Ri11 = chol(G11) (columns 0 .. B - 1 of colflag)
     e = launch_chol_wide(Ga, B, B, tol, R11, Ri11, nullptr, colflag, flag, work, nullptr, s, ill_tol, ill);
     if (e != hipSuccess) return e;
-    // R12 = Ri11^T G12 -> R[:256, 256:] (ld 512), broken-down rows zeroed
-    e = gemm_rm(1, 0, B, B, B, 1.0, Ri11, B, G + B, 512, 0.0, R + B, 512, s);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(chol2_zero_rows_kernel, dim3(B), dim3(B), 0, s, R + B, colflag);
+    // R12 = Ri11^T G12 -> R[:B, B:] (ld LP), broken-down rows zeroed
+    if ((e = gemm_sq(B, 1, 1.0, Ri11, B, G + B, LP, 0.0, R + B, LP, s)) != hipSuccess) return e;
+    hipLaunchKernelGGL(chol2_zero_rows_kernel, dim3(B), dim3(B), 0, s, R + B, B, colflag);
     // S = G22 - R12^T R12
-    e = gemm_rm(1, 0, B, B, B, -1.0, R + B, 512, R + B, 512, 1.0, Sb, B, s);
-    if (e != hipSuccess) return e;
-    // level 2 on the l - 256 valid columns of S, tested against diag(G22)
+    if ((e = gemm_sq(B, 1, -1.0, R + B, LP, R + B, LP, 1.0, Sb, B, s)) != hipSuccess) return e;
+    // level 2 on the l - B valid columns of S, tested against diag(G22)
     e = launch_chol_wide(Sb, l - B, B, tol, R22, Ri22, nullptr, colflag + B, flag, work, nullptr, s, ill_tol,
                          ill ? ill2 : nullptr, d0b);
     if (e != hipSuccess) return e;
-    // Rinv12 = -Ri11 (R12 Ri22) -> Rinv[:256, 256:]
-    e = gemm_rm(0, 0, B, B, B, 1.0, R + B, 512, Ri22, B, 0.0, T, B, s);
-    if (e != hipSuccess) return e;
-    e = gemm_rm(0, 0, B, B, B, -1.0, Ri11, B, T, B, 0.0, Rinv + B, 512, s);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(chol2_assemble_kernel, dim3(512), dim3(B), 0, s, R11, Ri11, R22, Ri22, R, Rinv, Rinv32,
+    // Rinv12 = -Ri11 (R12 Ri22) -> Rinv[:B, B:]
+    if ((e = gemm_sq(B, 0, 1.0, R + B, LP, Ri22, B, 0.0, T, B, s)) != hipSuccess) return e;
+    if ((e = gemm_sq(B, 0, -1.0, Ri11, B, T, B, 0.0, Rinv + B, LP, s)) != hipSuccess) return e;
+    hipLaunchKernelGGL(chol2_assemble_kernel, dim3(LP), dim3(B), 0, s, R11, Ri11, R22, Ri22, B, R, Rinv, Rinv32,
                        ill2, ill);
     return hipGetLastError();
 }
