@@ -15,6 +15,7 @@
 // (repair_kernel + one predicated CholeskyQR pass) -- an orthonormal basis completed like the
 // reference's Householder Q.
 #include <algorithm>
+#include <cstdlib>
 #include <utility>
 
 #include "common.hpp"
@@ -535,9 +536,9 @@ __device__ __forceinline__ double rsqrt_nr(double d) {
 // blocks (global), D^-1 (Di, LDS, row-major), the breakdown rows (bad) and flags.
 __device__ __forceinline__ void chol_diag16_fast(double (&col)[16], int p16, int l, int LP, double tol,
                                                  const double* d0, double* Di, int* bad, double* R, double* Rinv,
-                                                 int* colflag, int* flag, int lane, double ill_tol, int* ill_s) {
+                                                 int* colflag, int* flag, int lane) {
     const int j = lane & 15;
-    int badmask = 0, illm = 0;
+    int badmask = 0;
     double acc[16];
 #pragma unroll
     for (int i = 0; i < 16; ++i) acc[i] = 0.0;
@@ -548,7 +549,6 @@ __device__ __forceinline__ void chol_diag16_fast(double (&col)[16], int p16, int
         const bool pad = gk >= l;
         const bool isbad = !pad && (!(dkk > tol * d0[gk]) || !(d0[gk] > 0.0) || !isfinite(dkk));
         if (isbad) badmask |= 1 << k;
-        if (!pad && !(dkk > ill_tol * d0[gk])) illm = 1;  // (wave-uniform) a pivot too small for the split Gram
         const bool unit = pad || isbad;
         const double y = unit ? 1.0 : rsqrt_nr(dkk);
         const double rk = unit ? 1.0 : dkk * y;
@@ -579,12 +579,27 @@ __device__ __forceinline__ void chol_diag16_fast(double (&col)[16], int p16, int
             *reinterpret_cast<double2*>(Rinv + (int64_t)(p16 + j) * LP + p16 + i) =
                 *reinterpret_cast<const double2*>(Di + j * 16 + i);
     }
-    if (lane == 0 && illm) *ill_s = 1;
     if (lane == 0 && badmask) {
         atomicAdd(flag, __popc(badmask));
         for (int k = 0; k < 16; ++k)
             if (badmask & (1 << k)) colflag[p16 + k] = 1;
     }
+}
+
+// The split-Gram fallback test after a factor (off the pivot chain): ill = some valid pivot broke
+// down or R_kk^2 <= ill_tol G_kk.  Called by the whole workgroup after its last barrier (the R
+// diagonal and colflag stores of the factor are then visible workgroup-wide).
+__device__ __forceinline__ void chol_ill_test(const double* __restrict__ R, int LP, int l, const double* d0,
+                                              const int* __restrict__ colflag, double ill_tol, int* ill,
+                                              int* ill_s, int tid, int nthr) {
+    int mine = 0;
+    for (int k = tid; k < l; k += nthr) {
+        const double rkk = R[(int64_t)k * LP + k];
+        if (colflag[k] || !(rkk * rkk > ill_tol * d0[k])) mine = 1;
+    }
+    if (mine) *ill_s = 1;
+    __syncthreads();
+    if (tid == 0) *ill = *ill_s;
 }
 
 #ifdef RSVD_CHOL_PROF
@@ -754,7 +769,7 @@ __global__ __launch_bounds__(NT) void chol_wide_kernel(const double* __restrict_
                 __builtin_amdgcn_s_waitcnt(0xc07f);
                 __builtin_amdgcn_wave_barrier();
                 chol_diag16_fast(col, 16 * b1, l, LP, tol, d0, Dd + (b1 & 1) * 256, bad + (b1 & 1) * 16, R, Rinv,
-                                 colflag, flag, lane, ill_tol, &ill_s);
+                                 colflag, flag, lane);
             } else if (p >= 0) {
                 // local tile t of the (nt2 x nt2) upper triangle; t = 0 is wave 0's
                 TriWalk tw(wv, nt2);
@@ -801,7 +816,7 @@ __global__ __launch_bounds__(NT) void chol_wide_kernel(const double* __restrict_
         __syncthreads();
         if (p >= 0) CHOL_TS(2 + 2 * p);
     }
-    if (ill && tid == 0) *ill = ill_s;
+    if (ill) chol_ill_test(R, LP, l, d0, colflag, ill_tol, ill, &ill_s, tid, NT);
 }
 
 size_t chol_lds_bytes(int LP) {
@@ -918,12 +933,12 @@ __global__ __launch_bounds__(64 * kCholRegWaves) void chol_reg_kernel(const doub
             __builtin_amdgcn_s_waitcnt(0xc07f);
             __builtin_amdgcn_wave_barrier();
             chol_diag16_fast(col, p16, l, LP, tol, d0, Di + (p & 1) * 256, bad + (p & 1) * 16, R, Rinv,
-                            colflag, flag, lane, ill_tol, &ill_s);
+                            colflag, flag, lane);
         }
         __syncthreads();
         if (p < 32) CHOL_TS(1 + 3 * p);
         if (p == NP - 1) {
-            if (ill && tid == 0) *ill = ill_s;
+            if (ill) chol_ill_test(R, LP, l, d0, colflag, ill_tol, ill, &ill_s, tid, 64 * NW);
             break;
         }
         // (B) strip R[p][jb] = D_p^-T W[p][jb] (0 for rows that broke down or are padding)
@@ -1234,21 +1249,26 @@ __global__ void split_mat_kernel(const float* __restrict__ M, int LP, bf16_t* __
     }
 }
 
+// RT2 row tiles (16 rows each) per wave, CT output columns per workgroup: the workgroup covers
+// 64 RT2 rows x CT columns.  M's next chunk is loaded into registers while the current one is
+// multiplied and written to the free LDS buffer after the MFMAs; the first version loaded and
+// wrote it in one place before the MFMAs, exposing the L2 latency every step, and transposed
+// column-major outputs through LDS.  Same shape (RT2 = 2, CT = 128), same box: C5 m-side product
+// 454 -> 318 us, n side 51 -> 31 us, C4 74 -> 59 us (C5 31.0 -> 30.1 ms, C3 7.90 -> 7.50 ms).
+template <int RT2, int CT>
 __global__ __launch_bounds__(256) void panel_split_kernel(const float* __restrict__ In, int64_t rows, int LP,
                                                           const bf16_t* __restrict__ Mt, int upper,
                                                           float* __restrict__ Out, int64_t ldo, int cols,
                                                           bf16_t* __restrict__ hi, bf16_t* __restrict__ lo, int ncb,
                                                           const int* __restrict__ pred) {
     if (pred && *pred == 0) return;
-    // workgroup tile 128 rows x 128 columns: wave w owns rows 32 w .. + 31 (two 16-row tiles), so
-    // each staged M chunk (24 KiB) feeds 128 rows
-    constexpr int CT = 128, G = CT / 16, RT2 = 2, IMG = CT * 64, STEPB = 3 * IMG;
+    constexpr int G = CT / 16, IMG = CT * 64, STEPB = 3 * IMG, WR = 64 * RT2, NU = 3 * CT / 64;
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int r = lane & 15, h = lane >> 4;
     const int bid = xcd_remap(blockIdx.x, gridDim.x);
     const int cb = bid % ncb;
-    const int64_t row0 = (int64_t)(bid / ncb) * 128;
+    const int64_t row0 = (int64_t)(bid / ncb) * WR;
     const int c0 = cb * CT;
     const int kmax = upper ? ((c0 + CT < LP) ? c0 + CT : LP) : LP;
     const int nk = (kmax + 31) / 32;
@@ -1258,15 +1278,23 @@ __global__ __launch_bounds__(256) void panel_split_kernel(const float* __restric
     for (int t = 0; t < RT2; ++t)
 #pragma unroll
         for (int g = 0; g < G; ++g) acc[t][g] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // M chunk staging: 3 pieces x 128 columns x 64 B = 1536 16-B units, 6 per thread
-    auto stage = [&](int ks, char* img) {
+    // M chunk: 3 pieces x CT columns x 64 B = 12 CT 16-B units, NU per thread
+    uint4 mreg[NU];
+    auto loadM = [&](int ks) {
 #pragma unroll
-        for (int t = 0; t < 6; ++t) {
+        for (int t = 0; t < NU; ++t) {
             const int u = tid + 256 * t;
-            const int x = u / 512, rem = u % 512, c = rem >> 2, un = rem & 3;
-            uint4 v = make_uint4(0u, 0u, 0u, 0u);
-            if (c0 + c < LP) v = *reinterpret_cast<const uint4*>(Mt + x * L2 + (int64_t)(c0 + c) * LP + 32 * ks + 8 * un);
-            *reinterpret_cast<uint4*>(img + x * IMG + c * 64 + 16 * (un ^ ((c >> 1) & 3))) = v;
+            const int x = u / (4 * CT), rem = u % (4 * CT), c = rem >> 2, un = rem & 3;
+            mreg[t] = make_uint4(0u, 0u, 0u, 0u);
+            if (c0 + c < LP) mreg[t] = *reinterpret_cast<const uint4*>(Mt + x * L2 + (int64_t)(c0 + c) * LP + 32 * ks + 8 * un);
+        }
+    };
+    auto writeM = [&](char* img) {
+#pragma unroll
+        for (int t = 0; t < NU; ++t) {
+            const int u = tid + 256 * t;
+            const int x = u / (4 * CT), rem = u % (4 * CT), c = rem >> 2, un = rem & 3;
+            *reinterpret_cast<uint4*>(img + x * IMG + c * 64 + 16 * (un ^ ((c >> 1) & 3))) = mreg[t];
         }
     };
     // In vectors of this / the next k-step (swapped, never indexed at run time)
@@ -1275,7 +1303,7 @@ __global__ __launch_bounds__(256) void panel_split_kernel(const float* __restric
         const int k = 32 * ks + 8 * h;
 #pragma unroll
         for (int t = 0; t < RT2; ++t) {
-            const int64_t row = row0 + 32 * w + 16 * t + r;
+            const int64_t row = row0 + 16 * RT2 * w + 16 * t + r;
             if (row < rows && k < LP) {
                 a[t][0] = *reinterpret_cast<const float4*>(In + row * LP + k);
                 a[t][1] = *reinterpret_cast<const float4*>(In + row * LP + k + 4);
@@ -1287,14 +1315,16 @@ __global__ __launch_bounds__(256) void panel_split_kernel(const float* __restric
     const uint32_t lofs = (uint32_t)(r * 64 + 16 * (h ^ ((r >> 1) & 3)));
     if (nk > 0) {
         loadA(0, cur);
-        stage(0, smem_raw);
+        loadM(0);
+        writeM(smem_raw);
     }
     for (int ks = 0; ks < nk; ++ks) {
-        char* img = smem_raw + (ks & 1) * STEPB;
-        __syncthreads();  // chunk ks staged; chunk ks - 1's readers are done
-        if (ks + 1 < nk) {
+        const char* img = smem_raw + (ks & 1) * STEPB;
+        __syncthreads();  // chunk ks written; the readers of chunk ks - 1 (the other buffer) are done
+        const bool more = ks + 1 < nk;
+        if (more) {
             loadA(ks + 1, nxt);
-            stage(ks + 1, smem_raw + ((ks + 1) & 1) * STEPB);
+            loadM(ks + 1);
         }
         // In fragments of this k-step: three pieces of 8 consecutive k of the lane's row, per row tile
         bf16x8s fa[RT2][3];
@@ -1332,6 +1362,7 @@ __global__ __launch_bounds__(256) void panel_split_kernel(const float* __restric
                 acc[t][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[t][0], bh, c, 0, 0, 0);
             }
         }
+        if (more) writeM(smem_raw + ((ks + 1) & 1) * STEPB);
 #pragma unroll
         for (int t = 0; t < RT2; ++t) {
             cur[t][0] = nxt[t][0];
@@ -1346,7 +1377,7 @@ __global__ __launch_bounds__(256) void panel_split_kernel(const float* __restric
             for (int g = 0; g < G; ++g)
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
-                    const int64_t orow = row0 + 32 * w + 16 * t + 4 * h + j;
+                    const int64_t orow = row0 + 16 * RT2 * w + 16 * t + 4 * h + j;
                     const int c = c0 + 16 * g + r;
                     if (orow < rows && c < LP) {
                         const float v = acc[t][g][j];
@@ -1360,20 +1391,25 @@ __global__ __launch_bounds__(256) void panel_split_kernel(const float* __restric
                 }
         return;
     }
-    // column-major caller output: transpose through LDS, store column segments contiguously
-    __syncthreads();
-    float* Ts = reinterpret_cast<float*>(smem_raw);  // [CT][128 + 1]
+    // column-major caller output: a lane holds 4 consecutive rows of one column -- one 16-B store
+    // when Out and ldo allow it (4 lanes then write 64 contiguous bytes of the column)
+    const bool vec = ((reinterpret_cast<uintptr_t>(Out) | (uintptr_t)(ldo * 4)) & 15) == 0;
 #pragma unroll
     for (int t = 0; t < RT2; ++t)
 #pragma unroll
-        for (int g = 0; g < G; ++g)
+        for (int g = 0; g < G; ++g) {
+            const int64_t orow = row0 + 16 * RT2 * w + 16 * t + 4 * h;
+            const int c = c0 + 16 * g + r;
+            if (c >= cols) continue;
+            float* dst = Out + orow + (int64_t)c * ldo;
+            if (vec && orow + 3 < rows) {
+                *reinterpret_cast<f32x4*>(dst) = acc[t][g];
+            } else {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) Ts[(16 * g + r) * 129 + 32 * w + 16 * t + 4 * h + j] = acc[t][g][j];
-    __syncthreads();
-    for (int e = tid; e < CT * 128; e += 256) {
-        const int c = e / 128, lr = e % 128;
-        if (c0 + c < cols && row0 + lr < rows) Out[row0 + lr + (int64_t)(c0 + c) * ldo] = Ts[c * 129 + lr];
-    }
+                for (int j = 0; j < 4; ++j)
+                    if (orow + j < rows) dst[j] = acc[t][g][j];
+            }
+        }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1695,6 +1731,17 @@ hipError_t launch_chol_wide_2level(const double* G, int l, int LP, double tol, d
 }
 
 
+// panel_split_kernel shape: 0 = 2 row tiles x 128 columns (default), 1 = 4 x 128, 2 = 4 x 64
+// (RSVD_PANEL_SPLIT_SHAPE, for A/B runs; 4 x 128 runs at one wave per SIMD and loses the gain of
+// its halved LDS reads, 4 x 64 ties with 2 x 128 in the bench)
+static int panel_split_variant() {
+    static const int v = [] {
+        const char* e = std::getenv("RSVD_PANEL_SPLIT_SHAPE");
+        return e ? std::atoi(e) : 0;
+    }();
+    return v;
+}
+
 template <typename T>
 hipError_t launch_panel_gemm(const T* In, int64_t rows, int LP, const T* Mm, int upper, T* Out, int64_t ldo,
                              int cols, bf16_t* hi, bf16_t* lo, const int* pred, hipStream_t s, bf16_t* msplit) {
@@ -1705,13 +1752,20 @@ hipError_t launch_panel_gemm(const T* In, int64_t rows, int LP, const T* Mm, int
             const int64_t L2 = (int64_t)LP * LP;
             hipLaunchKernelGGL(split_mat_kernel, dim3((unsigned)std::min<int64_t>((L2 + 255) / 256, 1024)), dim3(256), 0,
                                s, reinterpret_cast<const float*>(Mm), LP, msplit);
-            const int ncb = (LP + 127) / 128;
-            const int64_t rb2 = (rows + 127) / 128;
-            const size_t lds = std::max<size_t>((size_t)2 * 3 * 128 * 64, (size_t)128 * 129 * 4);
-            hipLaunchKernelGGL(panel_split_kernel, dim3((unsigned)(rb2 * ncb)), dim3(256), lds, s,
-                               reinterpret_cast<const float*>(In), rows, LP, msplit, upper,
-                               reinterpret_cast<float*>(Out), ldo, cols, hi, lo, ncb, pred);
-            return hipGetLastError();
+#define PSPLIT(RT2, CT)                                                                                        \
+    {                                                                                                          \
+        const int ncb = (LP + CT - 1) / CT;                                                                    \
+        const int64_t rb2 = (rows + 64 * RT2 - 1) / (64 * RT2);                                                \
+        hipLaunchKernelGGL((panel_split_kernel<RT2, CT>), dim3((unsigned)(rb2 * ncb)), dim3(256),              \
+                           (size_t)2 * 3 * CT * 64, s, reinterpret_cast<const float*>(In), rows, LP, msplit,   \
+                           upper, reinterpret_cast<float*>(Out), ldo, cols, hi, lo, ncb, pred);                \
+        return hipGetLastError();                                                                              \
+    }
+            const int v = panel_split_variant();
+            if (v == 1) PSPLIT(4, 128)
+            if (v == 2) PSPLIT(4, 64)
+            PSPLIT(2, 128)
+#undef PSPLIT
         }
     }
 #define GO(CT)                                                                                                  \
