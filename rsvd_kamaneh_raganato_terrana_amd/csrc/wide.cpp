@@ -291,6 +291,7 @@ struct WideEngine {
     // 128^3 products (14 us each, latency-bound) lose to the one-level 175 us factor (C4 28.63 vs
     // 28.88 ms on the same box)
     int chol2 = 1;
+    int bj_groups = 0;  // block-Jacobi row groups (0: auto; RSVD_BJ_GROUPS, for A/B runs)
     // panel_gemm's operand in the panel precision: fp64 matrices as-is, fp32 copies for fp32 panels
     const T* mat(const double* m64, const float* m32) const {
         if constexpr (sizeof(T) == 8) return m64; else return m32;
@@ -456,8 +457,10 @@ struct WideEngine {
         } else {
             // fp32 results (fp32 / bf16 / e4m3 A): converged at cos <= 1e-6 -- 16 fp32 ulps, far below
             // the 1e-4 bar -- one or two sweeps fewer than the fp64 results' 1e-12
+            const int bjg = bj_groups > 0 && block_jacobi_groups(L.LP, L.LP, bj_groups) ? bj_groups : 0;
             RSVD_CK(launch_block_jacobi<double>(R1, L.l, L.LP, JX, JJ, Uw, Vw, Sd, sync, h->dflags + 1, s,
-                                                sizeof(T) == 4 ? 1e-8 : 1e-16, sizeof(T) == 4 ? kBJTolF32 : kBJTolF64));
+                                                sizeof(T) == 4 ? 1e-8 : 1e-16, sizeof(T) == 4 ? kBJTolF32 : kBJTolF64,
+                                                bjg));
         }
         RSVD_CK(launch_convert_scale<T>(Sd, S, L.l, std::fabs(a_scale(d)), s));
         if (sizeof(T) == 4) {
@@ -527,6 +530,11 @@ int wide_typed(rsvd_handle_t h, const rsvd_desc_t* d, const void* A, const void*
             return v ? std::atoi(v) : 1;
         }();
         E.split_panel = env3 != 0 && sizeof(T) == 4 && L.lowp && L.LP % 32 == 0 && L.LP >= 128;
+        static const int env4 = [] {
+            const char* v = std::getenv("RSVD_BJ_GROUPS");
+            return v ? std::atoi(v) : 0;
+        }();
+        E.bj_groups = env4;
     }
     E.lowp_inter = (d->flags & RSVD_FLAG_LOWP_INTERMEDIATES) != 0;
     E.seed = d->seed;

@@ -38,6 +38,7 @@
 // (an LP x LP fp64 MFMA Gram, every workgroup a 32-column slice) and stops at <= tol_chk -- which
 // saves the confirming sweep the first rule needs.
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.hpp"
 #include "kernels.hpp"
@@ -176,48 +177,40 @@ size_t block_jacobi_lds(int rows) { return ((rows <= 512 ? (size_t)32 * (rows + 
 constexpr int kBJThreads = 512;  // 8 waves: 2 per SIMD for the MFMA phases
 
 // One cyclic sweep of the 32 x 32 pair Gram (round-robin: 16 disjoint rotations per inner round,
-// 31 rounds), two phases per inner round: (a) lanes 0..15 compute the angles of the 16 pairs into
-// LDS; (b) thread (k, k2) < 256 rotates the 2 x 2 block (pair k rows, pair k2 columns) from both
-// sides into the other G buffer, while threads 256.. rotate the columns of Jp (Jp <- Jp J).
-// Returns the buffer holding the final Gram.
-__device__ __forceinline__ double* inner_sweep(double* Ga, double* Gb, double* Jp, double* Ang, int* Rot, int tid,
-                                               double tol2, double negl) {
+// 31 rounds), ONE barrier per inner round: every thread derives the angle of its column pair k2
+// itself (32 threads per pair, identical inputs, so identical c, s); thread (k, k2) < 256 takes
+// the angle of its row pair k from a lane of its wave that computed it (a register shuffle) and
+// rotates the 2 x 2 block (pair k rows, pair k2 columns) from both sides into the other G buffer,
+// while threads 256.. rotate the columns of Jp (Jp <- Jp J).  Returns the buffer holding the final
+// Gram.  (Round 3: replaces 16 lanes writing the angles to LDS behind a barrier of their own --
+// bit-identical outputs, neutral in the bench: C4 27.72 -> 27.59 ms, C5 29.60 -> 29.57 ms, C3 equal;
+// the inner round is bound by neither that barrier nor the angle hand-off.)
+__device__ __forceinline__ double* inner_sweep(double* Ga, double* Gb, double* Jp, int tid, double tol2, double negl) {
     for (int e = tid; e < 32 * 32; e += kBJThreads) Jp[(e / 32) * GS + e % 32] = (e / 32 == e % 32) ? 1.0 : 0.0;
     __syncthreads();
     const int k = (tid >> 4) & 15, k2 = tid & 15;
+    const int src = (tid & 0x30) | k;  // a lane of this wave with k2 == k
     double* cur = Ga;
     double* nxt = Gb;
     for (int ir = 0; ir < 31; ++ir) {
-        if (tid < 16) {
-            int p, q;
-            rr_pair(ir, tid, 32, p, q);
-            double c, sn;
-            bool rt;
-            pair_angle(cur, p, q, tol2, negl, c, sn, rt);
-            Ang[tid] = c;
-            Ang[16 + tid] = sn;
-            Rot[tid] = rt;
-        }
-        __syncthreads();
         int p2, q2;
         rr_pair(ir, k2, 32, p2, q2);
-        const double c2 = Ang[k2], s2 = Ang[16 + k2];
+        double c2, s2;
+        bool rt2;
+        pair_angle(cur, p2, q2, tol2, negl, c2, s2, rt2);
+        const double c1 = __shfl(c2, src, 64), s1 = __shfl(s2, src, 64);
         if (tid < 256) {
             int p, q;
             rr_pair(ir, k, 32, p, q);
-            const double c1 = Ang[k], s1 = Ang[16 + k];
             const double b00 = cur[p * GS + p2], b01 = cur[p * GS + q2];
             const double b10 = cur[q * GS + p2], b11 = cur[q * GS + q2];
-            // left: rows (p, q) <- (c1 row_p - s1 row_q, s1 row_p + c1 row_q)
             const double l00 = c1 * b00 - s1 * b10, l01 = c1 * b01 - s1 * b11;
             const double l10 = s1 * b00 + c1 * b10, l11 = s1 * b01 + c1 * b11;
-            // right: cols (p2, q2) <- (c2 col_p2 - s2 col_q2, s2 col_p2 + c2 col_q2)
             nxt[p * GS + p2] = c2 * l00 - s2 * l01;
             nxt[p * GS + q2] = s2 * l00 + c2 * l01;
             nxt[q * GS + p2] = c2 * l10 - s2 * l11;
             nxt[q * GS + q2] = s2 * l10 + c2 * l11;
-        } else if (Rot[k2]) {
-            // Jp columns (p2, q2) of pair k2, rows k and k + 16 (disjoint per thread)
+        } else if (rt2) {
 #pragma unroll
             for (int rr = 0; rr < 2; ++rr) {
                 const int row = k + 16 * rr;
@@ -418,8 +411,6 @@ __global__ __launch_bounds__(kBJThreads) void block_jacobi_kernel(const double* 
     double* Jp = Gb + 32 * GS;                         // [32][GS] accumulated inner rotation
     __shared__ int flags[8];
     __shared__ double fro;
-    __shared__ double Ang[32];  // c, s of the 16 pairs of an inner round
-    __shared__ int Rot[16];
     __shared__ unsigned long long lmax;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int r = lane & 15, h = lane >> 4;
@@ -558,7 +549,7 @@ __global__ __launch_bounds__(kBJThreads) void block_jacobi_kernel(const double* 
                     if (flags[1]) __hip_atomic_store(sync + 36 + sweep, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
                 // 4. the inner sweep on Gp (in place; Jp from the register wave)
-                inner_sweep(Ga, Gb, Jp, Ang, Rot, tid, tol2, negl);
+                inner_sweep(Ga, Gb, Jp, tid, tol2, negl);
                 BJ_T(3);
                 // 5. X_pair Jp and J_pair Jp -> destination buffer
                 if (staged)
