@@ -69,6 +69,15 @@ __device__ __forceinline__ void rr_pair(int round, int k, int N, int& p, int& q)
     }
 }
 
+// rr_pair for N = 32 without the modulo (round < 31, k < 16): the same pairs
+__device__ __forceinline__ void rr_pair32(int round, int k, int& p, int& q) {
+    int a = round + k, b = round - k;
+    a = a >= 31 ? a - 31 : a;
+    b = b < 0 ? b + 31 : b;
+    p = k == 0 ? round : a;
+    q = k == 0 ? 31 : b;
+}
+
 // Returns false on timeout (then every workgroup bails out through the abort word sync[1]).
 // ctr: the arrival counter (sync[0] for the grid, a group word for a row group).
 __device__ bool grid_barrier(unsigned* sync, unsigned target, unsigned* ctr = nullptr) {
@@ -171,6 +180,26 @@ __device__ __forceinline__ void pair_angle(const double* G, int p, int q, double
     s = rot ? cc * t : 0.0;
 }
 
+// The same rotation with a shorter dependent chain: the operands are scaled by the power of two of
+// max(|d|, |2g|) (exact, v_ldexp) instead of a Newton reciprocal, and with u = ds + sqrt(ds^2 + gs^2)
+// (so t = gs / u) the pair c = (1 + t^2)^-1/2, s = c t is c = u w, s = gs w with
+// w = (u^2 + gs^2)^-1/2 -- one reciprocal square root instead of a reciprocal and a reciprocal square
+// root.  c^2 + s^2 = 1 to rounding as before; the angle differs from pair_angle's in the last bits.
+__device__ __forceinline__ void pair_angle_fast(const double* G, int p, int q, double tol2, double negl, double& c,
+                                                double& s, bool& rot) {
+    const double a = G[p * GS + p], b = G[q * GS + q], g = G[p * GS + q];
+    rot = g != 0.0 && g * g > tol2 * a * b && a > negl && b > negl;
+    const double d = b - a, g2 = 2.0 * g;
+    const int e = __builtin_amdgcn_frexp_exp(fmax(fmax(fabs(d), fabs(g2)), 1e-300));
+    const double ds = __builtin_ldexp(fabs(d), -e), gs = __builtin_ldexp(fabs(g2), -e);  // max in [0.5, 1)
+    const double hyp2 = ds * ds + gs * gs;
+    const double u = ds + hyp2 * rsqrt_nr(hyp2);
+    const double w = rsqrt_nr(u * u + gs * gs);
+    const double sg = ((d >= 0.0) == (g >= 0.0)) ? w : -w;
+    c = rot ? u * w : 1.0;
+    s = rot ? gs * sg : 0.0;
+}
+
 // rows: the rows one workgroup stages (MR / G)
 size_t block_jacobi_lds(int rows) { return ((rows <= 512 ? (size_t)32 * (rows + 1) : 0) + 3 * 32 * GS) * sizeof(double); }
 
@@ -185,6 +214,7 @@ constexpr int kBJThreads = 512;  // 8 waves: 2 per SIMD for the MFMA phases
 // Gram.  (Round 3: replaces 16 lanes writing the angles to LDS behind a barrier of their own --
 // bit-identical outputs, neutral in the bench: C4 27.72 -> 27.59 ms, C5 29.60 -> 29.57 ms, C3 equal;
 // the inner round is bound by neither that barrier nor the angle hand-off.)
+template <bool FAST>
 __device__ __forceinline__ double* inner_sweep(double* Ga, double* Gb, double* Jp, int tid, double tol2, double negl) {
     for (int e = tid; e < 32 * 32; e += kBJThreads) Jp[(e / 32) * GS + e % 32] = (e / 32 == e % 32) ? 1.0 : 0.0;
     __syncthreads();
@@ -194,14 +224,20 @@ __device__ __forceinline__ double* inner_sweep(double* Ga, double* Gb, double* J
     double* nxt = Gb;
     for (int ir = 0; ir < 31; ++ir) {
         int p2, q2;
-        rr_pair(ir, k2, 32, p2, q2);
+        rr_pair32(ir, k2, p2, q2);
         double c2, s2;
         bool rt2;
-        pair_angle(cur, p2, q2, tol2, negl, c2, s2, rt2);
+        if constexpr (FAST)
+            pair_angle_fast(cur, p2, q2, tol2, negl, c2, s2, rt2);
+        else
+            if constexpr (FAST)
+                pair_angle_fast(cur, p2, q2, tol2, negl, c2, s2, rt2);
+            else
+                pair_angle(cur, p2, q2, tol2, negl, c2, s2, rt2);
         const double c1 = __shfl(c2, src, 64), s1 = __shfl(s2, src, 64);
         if (tid < 256) {
             int p, q;
-            rr_pair(ir, k, 32, p, q);
+            rr_pair32(ir, k, p, q);
             const double b00 = cur[p * GS + p2], b01 = cur[p * GS + q2];
             const double b10 = cur[q * GS + p2], b11 = cur[q * GS + q2];
             const double l00 = c1 * b00 - s1 * b10, l01 = c1 * b01 - s1 * b11;
@@ -217,6 +253,59 @@ __device__ __forceinline__ double* inner_sweep(double* Ga, double* Gb, double* J
                 const double jp = Jp[row * GS + p2], jq = Jp[row * GS + q2];
                 Jp[row * GS + p2] = c2 * jp - s2 * jq;
                 Jp[row * GS + q2] = s2 * jp + c2 * jq;
+            }
+        }
+        __syncthreads();
+        double* t = cur;
+        cur = nxt;
+        nxt = t;
+    }
+    return cur;
+}
+
+// The same sweep on the first four waves only (one per SIMD): thread (k, k2) < 256 also rotates
+// rows k and k + 16 of Jp's column pair k2, so the round's VALU work (angle, index arithmetic,
+// 2 x 2 updates) is issued once per SIMD instead of twice; waves 4..7 only meet the barriers.
+// Same arithmetic as inner_sweep up to the compiler's FMA contraction choices.
+template <bool FAST>
+__device__ __forceinline__ double* inner_sweep4(double* Ga, double* Gb, double* Jp, int tid, double tol2, double negl) {
+    for (int e = tid; e < 32 * 32; e += kBJThreads) Jp[(e / 32) * GS + e % 32] = (e / 32 == e % 32) ? 1.0 : 0.0;
+    __syncthreads();
+    const int k = (tid >> 4) & 15, k2 = tid & 15;
+    const int src = (tid & 0x30) | k;
+    double* cur = Ga;
+    double* nxt = Gb;
+    for (int ir = 0; ir < 31; ++ir) {
+        if (tid < 256) {
+            int p2, q2, p, q;
+            rr_pair32(ir, k2, p2, q2);
+            rr_pair32(ir, k, p, q);
+            double c2, s2;
+            bool rt2;
+            if constexpr (FAST)
+            pair_angle_fast(cur, p2, q2, tol2, negl, c2, s2, rt2);
+        else
+            if constexpr (FAST)
+                pair_angle_fast(cur, p2, q2, tol2, negl, c2, s2, rt2);
+            else
+                pair_angle(cur, p2, q2, tol2, negl, c2, s2, rt2);
+            const double c1 = __shfl(c2, src, 64), s1 = __shfl(s2, src, 64);
+            const double b00 = cur[p * GS + p2], b01 = cur[p * GS + q2];
+            const double b10 = cur[q * GS + p2], b11 = cur[q * GS + q2];
+            const double l00 = c1 * b00 - s1 * b10, l01 = c1 * b01 - s1 * b11;
+            const double l10 = s1 * b00 + c1 * b10, l11 = s1 * b01 + c1 * b11;
+            nxt[p * GS + p2] = c2 * l00 - s2 * l01;
+            nxt[p * GS + q2] = s2 * l00 + c2 * l01;
+            nxt[q * GS + p2] = c2 * l10 - s2 * l11;
+            nxt[q * GS + q2] = s2 * l10 + c2 * l11;
+            if (rt2) {
+#pragma unroll
+                for (int rr = 0; rr < 2; ++rr) {
+                    const int row = k + 16 * rr;
+                    const double jp = Jp[row * GS + p2], jq = Jp[row * GS + q2];
+                    Jp[row * GS + p2] = c2 * jp - s2 * jq;
+                    Jp[row * GS + q2] = s2 * jp + c2 * jq;
+                }
             }
         }
         __syncthreads();
@@ -400,7 +489,8 @@ __global__ __launch_bounds__(kBJThreads) void block_jacobi_kernel(const double* 
                                                            int src_rowmajor, int mrv, int l, int MR, int LP, int G,
                                                            double* __restrict__ Xb, double* __restrict__ Jb,
                                                            double* __restrict__ scratch, unsigned* __restrict__ sync,
-                                                           int* __restrict__ info, double quad2, double tol_chk2) {
+                                                           int* __restrict__ info, double quad2, double tol_chk2,
+                                                           int inner_v) {
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
     const int rpg = MR / G, jpg = LP / G;  // rows of X / J per group member
     const bool staged = rpg <= 512;
@@ -549,7 +639,12 @@ __global__ __launch_bounds__(kBJThreads) void block_jacobi_kernel(const double* 
                     if (flags[1]) __hip_atomic_store(sync + 36 + sweep, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
                 // 4. the inner sweep on Gp (in place; Jp from the register wave)
-                inner_sweep(Ga, Gb, Jp, tid, tol2, negl);
+                switch (inner_v) {
+                    case 1: inner_sweep4<false>(Ga, Gb, Jp, tid, tol2, negl); break;
+                    case 2: inner_sweep<true>(Ga, Gb, Jp, tid, tol2, negl); break;
+                    case 3: inner_sweep4<true>(Ga, Gb, Jp, tid, tol2, negl); break;
+                    default: inner_sweep<false>(Ga, Gb, Jp, tid, tol2, negl);
+                }
                 BJ_T(3);
                 // 5. X_pair Jp and J_pair Jp -> destination buffer
                 if (staged)
@@ -783,6 +878,20 @@ __global__ __launch_bounds__(1024) void block_jacobi_complete_kernel(const T* __
 
 }  // namespace
 
+// inner sweep form: bit 0 = the first four waves only (inner_sweep4), bit 1 = pair_angle_fast.
+// Same box A/B (RSVD_BJ_INNER=0/1/2/3): C5 29.77 / 29.25 / 29.48 / 29.14 ms, C3 7.15 / 6.99 / 7.04 /
+// 6.99 ms, C4 28.02 / 28.05 / 28.06 / 27.92 ms (8 sweeps in every case).  Default: 3 for the
+// fp32-result tolerance; the fp64-result runs (tol_chk <= 1e-9: the standalone fp64 SVD, fp64 A)
+// keep 0, whose V is orthogonal to the 1e-12 the fp64 SVD tests hold (3 gave 1.6e-12 on a
+// 1200 x 900 SVD).
+static int bj_inner_variant(double tol_chk) {
+    static const int v = [] {
+        const char* e = std::getenv("RSVD_BJ_INNER");
+        return e ? std::atoi(e) : -1;
+    }();
+    return v >= 0 ? v : (tol_chk > 1e-9 ? 3 : 0);
+}
+
 int block_jacobi_groups(int MR, int LP, int G) {
     // scratch (U_w, MR x LP doubles) must hold nwg + 1024 nwg doubles; members split MR and LP rows
     // into whole 32- / 16-row tiles
@@ -807,7 +916,8 @@ hipError_t launch_block_jacobi_ex(const double* src, int64_t lds, int src_rowmaj
     hipError_t e = hipMemsetAsync(sync, 0, kSyncWords * sizeof(unsigned), s);
     if (e != hipSuccess) return e;
     e = launch_coresident(block_jacobi_kernel, dim3(LP / 32 * G), dim3(kBJThreads), block_jacobi_lds(MR / G), s, src,
-                          lds, src_rowmajor, mrv, l, MR, LP, G, X, J, Uw, sync, info, quad2, tol_chk * tol_chk);
+                          lds, src_rowmajor, mrv, l, MR, LP, G, X, J, Uw, sync, info, quad2, tol_chk * tol_chk,
+                          bj_inner_variant(tol_chk));
     if (e != hipSuccess) return e;
     const size_t lds_fin = (size_t)LP * 8 * 2 + (size_t)LP * 4 + 64;
     hipLaunchKernelGGL((block_jacobi_finish_kernel<T>), dim3(1), dim3(1024), lds_fin, s, X, l, MR, LP, sync, S);
