@@ -316,6 +316,67 @@ __device__ __forceinline__ double* inner_sweep4(double* Ga, double* Gb, double* 
     return cur;
 }
 
+// inner_sweep4 with the rotation of Jp moved to the idle waves 4..7, one round behind: wave 0's
+// k == 0 lanes leave each round's (c, s) in a two-slot LDS table, and in round ir + 1 threads 256..
+// apply round ir's rotations to rows k, k + 16 of Jp (c = 1, s = 0 for a skipped pair: the
+// identity).  The first four waves' round is then the angle and the 2 x 2 Gram update only.
+template <bool FAST>
+__device__ __forceinline__ double* inner_sweep4j(double* Ga, double* Gb, double* Jp, double* AngB, int tid, double tol2,
+                                                 double negl) {
+    for (int e = tid; e < 32 * 32; e += kBJThreads) Jp[(e / 32) * GS + e % 32] = (e / 32 == e % 32) ? 1.0 : 0.0;
+    __syncthreads();
+    const int k = (tid >> 4) & 15, k2 = tid & 15;
+    const int src = (tid & 0x30) | k;
+    double* cur = Ga;
+    double* nxt = Gb;
+    for (int ir = 0; ir < 32; ++ir) {
+        if (tid < 256) {
+            if (ir < 31) {
+                int p2, q2, p, q;
+                rr_pair32(ir, k2, p2, q2);
+                rr_pair32(ir, k, p, q);
+                double c2, s2;
+                bool rt2;
+                if constexpr (FAST)
+                    pair_angle_fast(cur, p2, q2, tol2, negl, c2, s2, rt2);
+                else
+                    pair_angle(cur, p2, q2, tol2, negl, c2, s2, rt2);
+                const double c1 = __shfl(c2, src, 64), s1 = __shfl(s2, src, 64);
+                const double b00 = cur[p * GS + p2], b01 = cur[p * GS + q2];
+                const double b10 = cur[q * GS + p2], b11 = cur[q * GS + q2];
+                const double l00 = c1 * b00 - s1 * b10, l01 = c1 * b01 - s1 * b11;
+                const double l10 = s1 * b00 + c1 * b10, l11 = s1 * b01 + c1 * b11;
+                nxt[p * GS + p2] = c2 * l00 - s2 * l01;
+                nxt[p * GS + q2] = s2 * l00 + c2 * l01;
+                nxt[q * GS + p2] = c2 * l10 - s2 * l11;
+                nxt[q * GS + q2] = s2 * l10 + c2 * l11;
+                if (tid < 16) {
+                    AngB[(ir & 1) * 32 + k2] = c2;
+                    AngB[(ir & 1) * 32 + 16 + k2] = s2;
+                }
+            }
+        } else if (ir > 0) {
+            int p2, q2;
+            rr_pair32(ir - 1, k2, p2, q2);
+            const double c2 = AngB[((ir - 1) & 1) * 32 + k2], s2 = AngB[((ir - 1) & 1) * 32 + 16 + k2];
+#pragma unroll
+            for (int rr = 0; rr < 2; ++rr) {
+                const int row = k + 16 * rr;
+                const double jp = Jp[row * GS + p2], jq = Jp[row * GS + q2];
+                Jp[row * GS + p2] = c2 * jp - s2 * jq;
+                Jp[row * GS + q2] = s2 * jp + c2 * jq;
+            }
+        }
+        __syncthreads();
+        if (ir < 31) {
+            double* t = cur;
+            cur = nxt;
+            nxt = t;
+        }
+    }
+    return cur;
+}
+
 // Stage rows [row0, row0 + nr) of the 32 columns col(0..31) of a column-major matrix (ld rows per
 // column) into LDS rows of pitch nr + 1; 32 nr / 2 double2, each thread keeping up to 4 loads in flight.
 template <typename F>
@@ -500,6 +561,7 @@ __global__ __launch_bounds__(kBJThreads) void block_jacobi_kernel(const double* 
     double* Gb = Ga + 32 * GS;
     double* Jp = Gb + 32 * GS;                         // [32][GS] accumulated inner rotation
     __shared__ int flags[8];
+    __shared__ double AngB[64];  // inner_sweep4j: (c, s) of two inner rounds
     __shared__ double fro;
     __shared__ unsigned long long lmax;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -643,6 +705,8 @@ __global__ __launch_bounds__(kBJThreads) void block_jacobi_kernel(const double* 
                     case 1: inner_sweep4<false>(Ga, Gb, Jp, tid, tol2, negl); break;
                     case 2: inner_sweep<true>(Ga, Gb, Jp, tid, tol2, negl); break;
                     case 3: inner_sweep4<true>(Ga, Gb, Jp, tid, tol2, negl); break;
+                    case 5: inner_sweep4j<false>(Ga, Gb, Jp, AngB, tid, tol2, negl); break;
+                    case 7: inner_sweep4j<true>(Ga, Gb, Jp, AngB, tid, tol2, negl); break;
                     default: inner_sweep<false>(Ga, Gb, Jp, tid, tol2, negl);
                 }
                 BJ_T(3);
@@ -878,9 +942,11 @@ __global__ __launch_bounds__(1024) void block_jacobi_complete_kernel(const T* __
 
 }  // namespace
 
-// inner sweep form: bit 0 = the first four waves only (inner_sweep4), bit 1 = pair_angle_fast.
+// inner sweep form: bit 0 = the first four waves only (inner_sweep4), bit 1 = pair_angle_fast,
+// bit 2 (with bit 0) = Jp rotated by waves 4..7 one round behind (inner_sweep4j).
 // Same box A/B (RSVD_BJ_INNER=0/1/2/3): C5 29.77 / 29.25 / 29.48 / 29.14 ms, C3 7.15 / 6.99 / 7.04 /
-// 6.99 ms, C4 28.02 / 28.05 / 28.06 / 27.92 ms (8 sweeps in every case).  Default: 3 for the
+// 6.99 ms, C4 28.02 / 28.05 / 28.06 / 27.92 ms (8 sweeps in every case); another box, 3 / 5 / 7:
+// C5 28.91 / 28.51 / 28.34, C4 27.67 / 27.35 / 27.27, C3 6.96 / 6.92 / 6.88.  Default: 7 for the
 // fp32-result tolerance; the fp64-result runs (tol_chk <= 1e-9: the standalone fp64 SVD, fp64 A)
 // keep 0, whose V is orthogonal to the 1e-12 the fp64 SVD tests hold (3 gave 1.6e-12 on a
 // 1200 x 900 SVD).
@@ -889,7 +955,7 @@ static int bj_inner_variant(double tol_chk) {
         const char* e = std::getenv("RSVD_BJ_INNER");
         return e ? std::atoi(e) : -1;
     }();
-    return v >= 0 ? v : (tol_chk > 1e-9 ? 3 : 0);
+    return v >= 0 ? v : (tol_chk > 1e-9 ? 7 : 0);
 }
 
 int block_jacobi_groups(int MR, int LP, int G) {
