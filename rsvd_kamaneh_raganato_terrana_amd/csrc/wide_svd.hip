@@ -341,6 +341,8 @@ __device__ __forceinline__ double* inner_sweep4j(double* Ga, double* Gb, double*
                     pair_angle_fast(cur, p2, q2, tol2, negl, c2, s2, rt2);
                 else
                     pair_angle(cur, p2, q2, tol2, negl, c2, s2, rt2);
+                // (evaluating the row pair's angle here too instead of the shuffle: C5 28.5 -> 29.3 ms,
+                // the round is VALU-issue-bound)
                 const double c1 = __shfl(c2, src, 64), s1 = __shfl(s2, src, 64);
                 const double b00 = cur[p * GS + p2], b01 = cur[p * GS + q2];
                 const double b10 = cur[q * GS + p2], b11 = cur[q * GS + q2];
