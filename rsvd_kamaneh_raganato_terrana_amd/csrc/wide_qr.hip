@@ -1369,26 +1369,52 @@ __global__ __launch_bounds__(256) void panel_split_kernel(const float* __restric
             cur[t][1] = nxt[t][1];
         }
     }
-    // epilogue.  bf16 MFMA D: col = r (output column c0 + 16 g + r), row = 4 h + j within the 16-row tile
+    // epilogue.  bf16 MFMA D: col = r (output column c0 + 16 g + r), row = 4 h + j within the 16-row tile.
+    // Row-major outputs go through LDS, 64 rows at a time (in the M buffers): a lane then owns 8
+    // consecutive columns of one row and stores them as 32 B of fp32 and 16 B each of hi / lo --
+    // from the accumulators a lane's values sit in 4 different rows, i.e. 2-byte hi / lo stores.
     if (ldo == 0) {
+        constexpr int TP = CT + 4;  // fp32 pitch of the staged rows
+        static_assert(64 * TP * 4 <= 2 * STEPB, "epilogue tile fits the M buffers");
+        float* Ts = reinterpret_cast<float*>(smem_raw);
 #pragma unroll
-        for (int t = 0; t < RT2; ++t)
+        for (int ch = 0; ch < RT2; ++ch) {  // 64-row chunks of the 64 RT2-row tile
+            __syncthreads();                // the M buffers / the previous chunk are free
 #pragma unroll
-            for (int g = 0; g < G; ++g)
+            for (int t = 0; t < RT2; ++t) {
+                const int rt = 16 * RT2 * w + 16 * t;  // this row tile's first row in the workgroup
+                if (rt / 64 != ch) continue;
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int64_t orow = row0 + 16 * RT2 * w + 16 * t + 4 * h + j;
-                    const int c = c0 + 16 * g + r;
-                    if (orow < rows && c < LP) {
-                        const float v = acc[t][g][j];
-                        if (Out) Out[orow * LP + c] = v;
-                        if (hi) {
-                            const bf16_t bh = f2bf(v);
-                            hi[orow * LP + c] = bh;
-                            if (lo) lo[orow * LP + c] = f2bf(v - bf2f(bh));
-                        }
-                    }
+                for (int g = 0; g < G; ++g)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) Ts[(rt % 64 + 4 * h + j) * TP + 16 * g + r] = acc[t][g][j];
+            }
+            __syncthreads();
+            for (int e = tid; e < 64 * (CT / 8); e += 256) {
+                const int lr = e / (CT / 8), c8 = 8 * (e % (CT / 8));
+                const int64_t orow = row0 + 64 * ch + lr;
+                const int c = c0 + c8;
+                if (orow >= rows || c >= LP) continue;
+                const float4 v0 = *reinterpret_cast<const float4*>(Ts + lr * TP + c8);
+                const float4 v1 = *reinterpret_cast<const float4*>(Ts + lr * TP + c8 + 4);
+                if (Out) {
+                    *reinterpret_cast<float4*>(Out + orow * LP + c) = v0;
+                    *reinterpret_cast<float4*>(Out + orow * LP + c + 4) = v1;
                 }
+                if (hi) {
+                    const float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+                    uint32_t ph[4], pl[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const bf16_t h0 = f2bf(v[2 * q]), h1 = f2bf(v[2 * q + 1]);
+                        ph[q] = (uint32_t)h0 | ((uint32_t)h1 << 16);
+                        pl[q] = (uint32_t)f2bf(v[2 * q] - bf2f(h0)) | ((uint32_t)f2bf(v[2 * q + 1] - bf2f(h1)) << 16);
+                    }
+                    *reinterpret_cast<uint4*>(hi + orow * LP + c) = make_uint4(ph[0], ph[1], ph[2], ph[3]);
+                    if (lo) *reinterpret_cast<uint4*>(lo + orow * LP + c) = make_uint4(pl[0], pl[1], pl[2], pl[3]);
+                }
+            }
+        }
         return;
     }
     // column-major caller output: a lane holds 4 consecutive rows of one column -- one 16-B store
