@@ -66,10 +66,11 @@ def algorithmic_flops(m, n, l, q):
     return f_proj, f_qr, f_small
 
 
-def make_A(torch, m_local, n, row0, dtype, rank_cols=128, seed=0x5EED0002):
+def make_A(torch, m_local, n, row0, dtype, rank_cols=128, seed=0x5EED0002, amax_reduce=None):
     """Column-major rows [row0, row0 + m_local) of the synthetic A, built on the GPU in row
     chunks (A^T chunks, n x rows) so the fp32 temporaries stay small.  fp8: A / scale in e4m3 with
-    scale = max|A| / 448 (per tensor), returned with the scale."""
+    scale = max|A| / 448 (per tensor: the max over every rank's rows via amax_reduce, so that all
+    shards share one scale), returned with the scale."""
     dev = torch.device("cuda")
     gY = torch.Generator(device=dev).manual_seed(seed)
     sig = 0.9 ** torch.arange(rank_cols, device=dev, dtype=torch.float32)
@@ -88,6 +89,8 @@ def make_A(torch, m_local, n, row0, dtype, rank_cols=128, seed=0x5EED0002):
     # column-major m x n: store A^T row-major
     if dtype == "fp8":
         amax = float(At.abs().max())
+        if amax_reduce is not None:
+            amax = amax_reduce(amax)
         scale = amax / 448.0
         Acm = (At / scale).t().contiguous().to(store).t()
         del At
@@ -247,6 +250,20 @@ def self_check(torch, dist, A, a_scale, U, S, V, world, k_top=32):
     return {"top_k": k, "max_ritz_residual": rel, "V_orth_err": vo, "ok": bool(rel < 1e-2 and vo < 1e-2)}
 
 
+def launch_ranks(n):
+    """Run this script as N ranks under torch.distributed.run (a child process: nothing in this
+    process has initialised the GPU, and it is never replaced by exec)."""
+    import socket
+    import subprocess
+
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -261,7 +278,16 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU-oracle work (0 = skip)")
     ap.add_argument("--comm", default="library", choices=["library", "torch"],
                     help="N > 1: the handle's own RCCL communicator (rsvd_comm_init) or torch.distributed hooks")
+    ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                    help="N > 1: torch.distributed backend (nccl = RCCL; gloo with --comm torch runs the whole "
+                         "multi-rank path with every rank on one GPU, for the one-GPU test box)")
     args = ap.parse_args()
+
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # `python bench.py --gpus N` without torchrun: start the N ranks as child processes (one per
+        # GPU, torch.distributed.run on 127.0.0.1) before this process touches the GPU, and exit
+        # with their status; rank 0 prints the JSON line
+        raise SystemExit(launch_ranks(args.gpus))
 
     import torch
     import torch.distributed as dist
@@ -278,11 +304,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world == 1 and args.gpus > 1:
-        raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one rank per GPU)")
-    torch.cuda.set_device(local_rank)
+    # one rank per GPU; with --backend gloo several ranks may share the box's GPUs (test mode)
+    ndev = max(1, torch.cuda.device_count())
+    dev = local_rank % ndev
+    if args.backend == "nccl" and world > ndev:
+        raise SystemExit(f"{world} ranks over RCCL need {world} GPUs ({ndev} visible)")
+    if args.backend == "gloo" and args.comm != "torch" and world > 1:
+        raise SystemExit("--backend gloo needs --comm torch (the library communicator is RCCL)")
+    torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{dev}"))
+        else:
+            dist.init_process_group("gloo")
 
     if strong:  # global m x n, rows partitioned (src/rSVD.cpp:20-23)
         m_global = m_cfg
@@ -293,8 +327,15 @@ def main():
     if args.config == "c1":  # I_100, exactly the reference's input/sparse_matrix100.mtx
         A, a_scale = torch.eye(m_local, n, dtype=torch.float64, device="cuda").t().contiguous().t(), 1.0
     else:
-        A, a_scale = make_A(torch, m_local, n, row0, dt)
-    eng = R.Engine(local_rank)
+        def amax_all(x):  # one per-tensor e4m3 scale for the global A
+            if world == 1:
+                return x
+            t = torch.tensor([x], device="cuda", dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            return float(t.item())
+
+        A, a_scale = make_A(torch, m_local, n, row0, dt, amax_reduce=amax_all)
+    eng = R.Engine(dev)
     if world > 1:
         if args.comm == "library":  # rsvd_comm_init: RCCL owned by the C ABI, rank 0's id broadcast
             uid = [R.Engine.comm_unique_id() if rank == 0 else None]
@@ -467,7 +508,8 @@ def main():
         if world > 1 and info.get("n_shard_rows"):
             par += f", n side sharded ({info['n_shard_rows']} rows/GPU)"
         if world > 1:
-            par += ", RCCL " + ("owned by the C ABI (rsvd_comm_init)" if args.comm == "library" else "via torch.distributed hooks")
+            par += (", gloo via torch.distributed hooks (test mode)" if args.backend == "gloo" else
+                    ", RCCL " + ("owned by the C ABI (rsvd_comm_init)" if args.comm == "library" else "via torch.distributed hooks"))
         line = {
             "metric": "rSVD wall-clock + achieved TFLOP/s, dense m x n rank-k",
             "value": value,

@@ -234,8 +234,10 @@ class Engine:
         if len(uid) != _capi.COMM_ID_BYTES:
             raise ValueError("bad RCCL unique id")
         buf = ctypes.create_string_buffer(uid, _capi.COMM_ID_BYTES)
-        self._hook = self._coll = None
+        # the handle may still hold set_comm's trampolines if the call fails (librccl missing):
+        # drop the Python references only once the library owns the collectives
         check(lib().rsvd_comm_init(self.h, buf, rank, world, int(shard_n)), self.h)
+        self._hook = self._coll = None
 
     def comm_destroy(self):
         check(lib().rsvd_comm_destroy(self.h), self.h)

@@ -188,6 +188,9 @@ int qr_big_typed(rsvd_handle_t h, int64_t m, int64_t n, const T* A, int64_t lda,
         const int w = (int)std::min<int64_t>(kQrBlock, K - c0);
         // the basis columns c0 .. c0 + w: A's (j < n), then the identity completion e_j (j >= n)
         const int na = (int)std::max<int64_t>(0, std::min<int64_t>(n, c0 + w) - c0);
+        // this block's breakdown word (as orth_cols): an earlier block's breakdown must not predicate
+        // this block's repair pass
+        RSVD_CK(hipMemsetAsync(h->dflags + 4, 0, sizeof(int), s));
         if (na > 0)
             RSVD_CK(hipMemcpy2DAsync(E.Y, sizeof(T) * m, A + c0 * lda, sizeof(T) * lda, sizeof(T) * m, na,
                                      hipMemcpyDeviceToDevice, s));

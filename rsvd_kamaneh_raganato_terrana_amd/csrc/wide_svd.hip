@@ -230,10 +230,7 @@ __device__ __forceinline__ double* inner_sweep(double* Ga, double* Gb, double* J
         if constexpr (FAST)
             pair_angle_fast(cur, p2, q2, tol2, negl, c2, s2, rt2);
         else
-            if constexpr (FAST)
-                pair_angle_fast(cur, p2, q2, tol2, negl, c2, s2, rt2);
-            else
-                pair_angle(cur, p2, q2, tol2, negl, c2, s2, rt2);
+            pair_angle(cur, p2, q2, tol2, negl, c2, s2, rt2);
         const double c1 = __shfl(c2, src, 64), s1 = __shfl(s2, src, 64);
         if (tid < 256) {
             int p, q;
@@ -282,9 +279,6 @@ __device__ __forceinline__ double* inner_sweep4(double* Ga, double* Gb, double* 
             rr_pair32(ir, k, p, q);
             double c2, s2;
             bool rt2;
-            if constexpr (FAST)
-            pair_angle_fast(cur, p2, q2, tol2, negl, c2, s2, rt2);
-        else
             if constexpr (FAST)
                 pair_angle_fast(cur, p2, q2, tol2, negl, c2, s2, rt2);
             else
@@ -887,8 +881,12 @@ __global__ __launch_bounds__(256) void block_jacobi_scatter_kernel(const double*
 template <typename T>
 __global__ __launch_bounds__(1024) void block_jacobi_complete_kernel(const T* __restrict__ S, int l, int rows_valid,
                                                                      int LP, double* __restrict__ Uw) {
+    // LDS is sized by LP, not by rows (the standalone SVD<Jacobi> has rows = max(m, n), unbounded):
+    // v[j] (j < LP) holds the CGS2 coefficients; the least-covered row is a block argmin reduction
+    // of per-thread (coverage, row) minima over the rows in global memory
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-    double* v = reinterpret_cast<double*>(smem_raw);  // [max(rows_valid, LP)]
+    double* v = reinterpret_cast<double*>(smem_raw);  // [max(LP, 1024)]
+    int* vi = reinterpret_cast<int*>(v + (LP > 1024 ? LP : 1024));  // [1024]
     __shared__ int misc[2];
     const int tid = threadIdx.x, nt = blockDim.x;
     if (tid == 0) misc[1] = 0;
@@ -900,20 +898,26 @@ __global__ __launch_bounds__(1024) void block_jacobi_complete_kernel(const T* __
     const int nz = misc[1];
     // complete U_w for zero singular values (as jacobi.hip): least-covered unit vector, CGS2
     for (int k = nz; k < l; ++k) {
+        double best_c = 1e300;
+        int best_i = 0x7fffffff;
         for (int i = tid; i < rows_valid; i += nt) {
             double cov = 0.0;
             for (int j = 0; j < k; ++j) cov += Uw[(int64_t)i * LP + j] * Uw[(int64_t)i * LP + j];
-            v[i] = cov;
+            if (cov < best_c) best_c = cov, best_i = i;  // rows visited in ascending order: first minimum
         }
+        v[tid] = best_c;
+        vi[tid] = best_i;
         __syncthreads();
-        if (tid == 0) {
-            int best = 0;
-            for (int i = 1; i < rows_valid; ++i)
-                if (v[i] < v[best]) best = i;
-            misc[0] = best;
+        for (int o = nt / 2; o > 0; o >>= 1) {
+            if (tid < o) {
+                const double c2 = v[tid + o];
+                const int i2 = vi[tid + o];
+                if (c2 < v[tid] || (c2 == v[tid] && i2 < vi[tid])) v[tid] = c2, vi[tid] = i2;
+            }
+            __syncthreads();
         }
+        const int cand = vi[0];
         __syncthreads();
-        const int cand = misc[0];
         for (int i = tid; i < rows_valid; i += nt) Uw[(int64_t)i * LP + k] = (i == cand) ? 1.0 : 0.0;
         __syncthreads();
         for (int pass = 0; pass < 2; ++pass) {
@@ -995,8 +999,8 @@ hipError_t launch_block_jacobi_ex(const double* src, int64_t lds, int src_rowmaj
                        l, LP, sync, 0, Vw);
     hipLaunchKernelGGL(block_jacobi_scatter_kernel, dim3(nbk * ((MR + 63) / 64)), dim3(256), 0, s, X, sx, X, sx, mrv, MR,
                        l, LP, sync, 1, Uw);
-    hipLaunchKernelGGL((block_jacobi_complete_kernel<T>), dim3(1), dim3(1024), (size_t)std::max(mrv, LP) * 8 + 64, s, S, l,
-                       mrv, LP, Uw);
+    hipLaunchKernelGGL((block_jacobi_complete_kernel<T>), dim3(1), dim3(1024), (size_t)std::max(LP, 1024) * 8 + 1024 * 4,
+                       s, S, l, mrv, LP, Uw);
     return hipGetLastError();
 }
 
