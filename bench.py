@@ -260,8 +260,11 @@ def launch_ranks(n):
         so.bind(("127.0.0.1", 0))
         port = so.getsockname()[1]
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
-           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
-    return subprocess.call(cmd)
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)]
+    # the bench's own flags travel in the environment: torch.distributed.run's parser would take
+    # abbreviations such as --m / --n placed after the script for its own options
+    env = dict(os.environ, RSVD_BENCH_ARGV=json.dumps(sys.argv[1:]))
+    return subprocess.call(cmd, env=env)
 
 
 def main():
@@ -281,7 +284,8 @@ def main():
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="N > 1: torch.distributed backend (nccl = RCCL; gloo with --comm torch runs the whole "
                          "multi-rank path with every rank on one GPU, for the one-GPU test box)")
-    args = ap.parse_args()
+    argv = json.loads(os.environ["RSVD_BENCH_ARGV"]) if "RSVD_BENCH_ARGV" in os.environ and "WORLD_SIZE" in os.environ else None
+    args = ap.parse_args(argv)
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # `python bench.py --gpus N` without torchrun: start the N ranks as child processes (one per
