@@ -57,7 +57,7 @@ struct WideLayout {
     GramPlan gm, gn, gx;
     size_t off_Xn, off_Zn, off_Ym, off_Qm, off_T1, off_Xh, off_Xl, off_Qh, off_Ql, off_X8, off_pslab, off_gslab;
     size_t off_G, off_R, off_Rinv, off_W, off_R1, off_Uw, off_Vw, off_JX, off_JJ, off_M32, off_MS, off_colflag, off_sync,
-        total;
+        off_E, total;
 
     int64_t mpad, npad;  // bf16 panel rows, zero-padded to a multiple of 32 (wproj2 reads whole k-steps)
     bool s8 = false;     // the sketch runs e4m3 x e4m3 on the fp8 MFMA
@@ -134,6 +134,8 @@ struct WideLayout {
         off_MS = take(sizeof(T) == 4 ? sizeof(bf16_t) * 3 * L2 : 0);  // the three bf16 pieces of panel_gemm's M
         off_colflag = take(sizeof(int) * LP);
         off_sync = take(sizeof(unsigned) * kBJSyncWords);
+        // the eigensolver's small SVD (fp32 results, 128 <= LP <= 512: wide_eig.hip)
+        off_E = take(sizeof(T) == 4 && LP >= 128 && LP <= 512 ? sizeof(double) * eig_svd_ws_doubles(LP) : 0);
         total = o;
     }
 };
@@ -292,6 +294,7 @@ struct WideEngine {
     // 28.88 ms on the same box)
     int chol2 = 1;
     int bj_groups = 0;  // block-Jacobi row groups (0: auto; RSVD_BJ_GROUPS, for A/B runs)
+    bool eig_svd = true;  // fp32 results: the small SVD through the eigensolver (RSVD_SMALL_SVD=jacobi: block Jacobi)
     // panel_gemm's operand in the panel precision: fp64 matrices as-is, fp32 copies for fp32 panels
     const T* mat(const double* m64, const float* m32) const {
         if constexpr (sizeof(T) == 8) return m64; else return m32;
@@ -454,6 +457,12 @@ struct WideEngine {
         double* Sd = G;  // free scratch by now
         if (L.LP <= 64) {
             RSVD_CK(launch_small_svd<double>(R1, L.l, L.LP, Uw, Vw, Sd, h->dflags + 1, s));
+        } else if (sizeof(T) == 4 && eig_svd && L.l >= 3 && L.LP >= 128 && L.LP <= 512) {
+            // fp32 results: G = W^T W, tridiagonalisation, multisection + inverse iteration, the
+            // back-transformation, X = W V_w, then the block Jacobi's orthogonality check at the same
+            // cos <= 1e-6 (wide_eig.hip; sweeps run only if the check fails)
+            double* E = reinterpret_cast<double*>(h->ws + L.off_E);
+            RSVD_CK(launch_eig_svd<double>(R1, L.l, L.LP, E, JX, JJ, Uw, Vw, Sd, sync, h->dflags + 1, s, kBJTolF32));
         } else {
             // fp32 results (fp32 / bf16 / e4m3 A): converged at cos <= 1e-6 -- 16 fp32 ulps, far below
             // the 1e-4 bar -- one or two sweeps fewer than the fp64 results' 1e-12
@@ -535,6 +544,11 @@ int wide_typed(rsvd_handle_t h, const rsvd_desc_t* d, const void* A, const void*
             return v ? std::atoi(v) : 0;
         }();
         E.bj_groups = env4;
+        static const bool env5 = [] {
+            const char* v = std::getenv("RSVD_SMALL_SVD");
+            return !(v && std::string(v) == "jacobi");
+        }();
+        E.eig_svd = env5;
     }
     E.lowp_inter = (d->flags & RSVD_FLAG_LOWP_INTERMEDIATES) != 0;
     E.seed = d->seed;

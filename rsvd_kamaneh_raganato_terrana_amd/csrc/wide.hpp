@@ -154,6 +154,22 @@ hipError_t launch_block_jacobi_ex(const double* src, int64_t lds, int src_rowmaj
                                   hipStream_t s, double quad2 = 1e-16, double tol_chk = kBJTolF64, int G = 0);
 // The row-group count launch_block_jacobi_ex uses for G (0: auto), or 0 when G does not fit.
 int block_jacobi_groups(int MR, int LP, int G);
+// "Given" mode (LP <= 512): X = W V_w and J = V_w are already in buffer 0 of X / J (column-major,
+// zero-padded); the kernel measures the largest cosine between the columns of X first and runs
+// sweeps only while it exceeds tol_chk; then the same finish (S, U_w, V_w).
+template <typename T>
+hipError_t launch_block_jacobi_given(int l, int LP, double* X, double* J, double* Uw, double* Vw, T* S, unsigned* sync,
+                                     int* info, hipStream_t s, double tol_chk);
+
+// ---- wide_eig.hip ------------------------------------------------------------------------------
+// The small SVD through the symmetric eigensolver (3 <= l <= 512, LP in {128, 256, 512}): G = W^T W,
+// Householder tridiagonalisation, multisection eigenvalues, inverse-iteration eigenvectors, the
+// compact-WY back-transformation, X = W V_w; then launch_block_jacobi_given's check (and polish if
+// it fails) and finish.  ews: eig_svd_ws_doubles(LP) doubles; sync: kBJSyncWords words.
+size_t eig_svd_ws_doubles(int LP);
+template <typename T>
+hipError_t launch_eig_svd(const double* R, int l, int LP, double* ews, double* X, double* J, double* Uw, double* Vw,
+                          T* S, unsigned* sync, int* info, hipStream_t s, double tol_chk);
 
 // ---- wide.cpp: the host pipeline ------------------------------------------------------------------
 // True when `d` runs on the wide engine (bf16 / fp8 A, or l > 64).

@@ -547,7 +547,7 @@ __global__ __launch_bounds__(kBJThreads) void block_jacobi_kernel(const double* 
                                                            double* __restrict__ Xb, double* __restrict__ Jb,
                                                            double* __restrict__ scratch, unsigned* __restrict__ sync,
                                                            int* __restrict__ info, double quad2, double tol_chk2,
-                                                           int inner_v) {
+                                                           int inner_v, int given) {
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
     const int rpg = MR / G, jpg = LP / G;  // rows of X / J per group member
     const bool staged = rpg <= 512;
@@ -579,15 +579,22 @@ __global__ __launch_bounds__(kBJThreads) void block_jacobi_kernel(const double* 
 
     // X (column-major, X[c][i] = W[i][c] = R[c][i]) and J = I into buffer 0: columns of this
     // workgroup; this workgroup's part of ||W||_F^2 to scratch[wg]
+    // (given: X and J are already in buffer 0 -- wide_eig.hip's X = W V_w, J = V_w -- and |X|_F = |W|_F)
     {
         double part = 0.0;
         for (int c = wg; c < LP; c += nwg) {
             for (int i = tid; i < MR; i += kBJThreads) {
-                const double v = (c < l && i < mrv) ? (src_rowmajor ? R[(int64_t)i * lds + c] : R[(int64_t)c * lds + i]) : 0.0;
-                Xb[(int64_t)c * MR + i] = v;
+                double v;
+                if (given) {
+                    v = Xb[(int64_t)c * MR + i];
+                } else {
+                    v = (c < l && i < mrv) ? (src_rowmajor ? R[(int64_t)i * lds + c] : R[(int64_t)c * lds + i]) : 0.0;
+                    Xb[(int64_t)c * MR + i] = v;
+                }
                 part += v * v;
             }
-            for (int i = tid; i < LP; i += kBJThreads) Jb[(int64_t)c * LP + i] = (c == i && c < l) ? 1.0 : 0.0;
+            if (!given)
+                for (int i = tid; i < LP; i += kBJThreads) Jb[(int64_t)c * LP + i] = (c == i && c < l) ? 1.0 : 0.0;
         }
         if (tid == 0) fro = 0.0;
         __syncthreads();
@@ -608,7 +615,22 @@ __global__ __launch_bounds__(kBJThreads) void block_jacobi_kernel(const double* 
 
     BJ_T(0);
     int par = 0, sweeps = 0;
-    for (int sweep = 0; sweep < kMaxSweeps; ++sweep) {
+    bool done = false;
+    if (given && tol_chk2 > 0.0) {
+        // the given X may already be orthogonal to the tolerance: the global check first (slot 31)
+        const double mx = slice_max_cos2(Xb, MR, LP, pr, g, G, w, lane, negl);
+        if (tid == 0) lmax = 0ull;
+        __syncthreads();
+        atomicMax(&lmax, (unsigned long long)__double_as_longlong(mx));
+        __syncthreads();
+        if (tid == 0) atomicMax(cmax + 31, lmax);
+        if (!grid_barrier(sync, (unsigned)nwg * ++bar)) {
+            if (tid == 0) info[2] = 1;
+            return;
+        }
+        done = u64_as_double(__hip_atomic_load(cmax + 31, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) <= tol_chk2;
+    }
+    for (int sweep = 0; sweep < kMaxSweeps && !done; ++sweep) {
         for (int round = 0; round < NB - 1; ++round) {
             int P, Q;
             rr_pair(round, pr, NB, P, Q);
@@ -979,9 +1001,9 @@ int block_jacobi_groups(int MR, int LP, int G) {
 }
 
 template <typename T>
-hipError_t launch_block_jacobi_ex(const double* src, int64_t lds, int src_rowmajor, int mrv, int l, int MR, int LP,
-                                  double* X, double* J, double* Uw, double* Vw, T* S, unsigned* sync, int* info,
-                                  hipStream_t s, double quad2, double tol_chk, int G) {
+hipError_t bj_launch(const double* src, int64_t lds, int src_rowmajor, int mrv, int l, int MR, int LP, double* X,
+                     double* J, double* Uw, double* Vw, T* S, unsigned* sync, int* info, hipStream_t s, double quad2,
+                     double tol_chk, int G, int given) {
     if (LP % 32 || LP < 64 || LP > 4096 || MR % 32 || MR < 32 || l > LP || mrv > MR) return hipErrorInvalidValue;
     G = block_jacobi_groups(MR, LP, G);
     if (G < 1) return hipErrorInvalidValue;
@@ -989,7 +1011,7 @@ hipError_t launch_block_jacobi_ex(const double* src, int64_t lds, int src_rowmaj
     if (e != hipSuccess) return e;
     e = launch_coresident(block_jacobi_kernel, dim3(LP / 32 * G), dim3(kBJThreads), block_jacobi_lds(MR / G), s, src,
                           lds, src_rowmajor, mrv, l, MR, LP, G, X, J, Uw, sync, info, quad2, tol_chk * tol_chk,
-                          bj_inner_variant(tol_chk));
+                          bj_inner_variant(tol_chk), given);
     if (e != hipSuccess) return e;
     const size_t lds_fin = (size_t)LP * 8 * 2 + (size_t)LP * 4 + 64;
     hipLaunchKernelGGL((block_jacobi_finish_kernel<T>), dim3(1), dim3(1024), lds_fin, s, X, l, MR, LP, sync, S);
@@ -1003,6 +1025,25 @@ hipError_t launch_block_jacobi_ex(const double* src, int64_t lds, int src_rowmaj
                        s, S, l, mrv, LP, Uw);
     return hipGetLastError();
 }
+
+template <typename T>
+hipError_t launch_block_jacobi_ex(const double* src, int64_t lds, int src_rowmajor, int mrv, int l, int MR, int LP,
+                                  double* X, double* J, double* Uw, double* Vw, T* S, unsigned* sync, int* info,
+                                  hipStream_t s, double quad2, double tol_chk, int G) {
+    return bj_launch<T>(src, lds, src_rowmajor, mrv, l, MR, LP, X, J, Uw, Vw, S, sync, info, s, quad2, tol_chk, G, 0);
+}
+
+template <typename T>
+hipError_t launch_block_jacobi_given(int l, int LP, double* X, double* J, double* Uw, double* Vw, T* S, unsigned* sync,
+                                     int* info, hipStream_t s, double tol_chk) {
+    if (LP > 512) return hipErrorInvalidValue;
+    return bj_launch<T>(nullptr, LP, 0, l, l, LP, LP, X, J, Uw, Vw, S, sync, info, s,
+                        tol_chk > 1e-9 ? 1e-8 : 1e-16, tol_chk, 0, 1);
+}
+template hipError_t launch_block_jacobi_given<float>(int, int, double*, double*, double*, double*, float*, unsigned*,
+                                                     int*, hipStream_t, double);
+template hipError_t launch_block_jacobi_given<double>(int, int, double*, double*, double*, double*, double*,
+                                                      unsigned*, int*, hipStream_t, double);
 
 template <typename T>
 hipError_t launch_block_jacobi(const double* R, int l, int LP, double* X, double* J, double* Uw, double* Vw, T* S,
