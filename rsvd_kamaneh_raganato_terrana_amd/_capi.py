@@ -80,7 +80,7 @@ COLL_REDUCE_SCATTER, COLL_ALL_GATHER = 1, 2
 
 def _sources():
     """The files librsvd_hip.so is built from, in the order the Makefile hashes them."""
-    hip = "util.hip proj.hip qr.hip jacobi.hip wide_proj.hip wide_qr.hip wide_svd.hip dense.hip gemm.hip".split()
+    hip = "util.hip proj.hip qr.hip jacobi.hip wide_proj.hip wide_qr.hip wide_svd.hip wide_eig.hip dense.hip gemm.hip".split()
     cpp = "driver.cpp wide.cpp dense_api.cpp comm.cpp dense_big.cpp".split()
     hdr = "common.hpp kernels.hpp wide.hpp dense.hpp handle.hpp".split()
     return ([os.path.join(CSRC, f) for f in hip + cpp + hdr] + [os.path.join(REPO, "include", "rsvd_c.h")]
