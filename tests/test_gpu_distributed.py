@@ -40,7 +40,7 @@ def _matrix(case):
     return gapped_matrix(m, n, 2 * l, decay=0.93 if l < 256 else 0.985, seed=5).astype(np.float64)
 
 
-def _worker(rank, port, case, q, shard_n, lowp=False):
+def _worker(rank, port, case, q, shard_n, lowp=False, world=WORLD):
     try:
         sys.path.insert(0, REPO)
         sys.path.insert(0, os.path.join(REPO, "tests"))
@@ -52,22 +52,22 @@ def _worker(rank, port, case, q, shard_n, lowp=False):
 
         os.environ["MASTER_ADDR"] = "127.0.0.1"
         os.environ["MASTER_PORT"] = str(port)
-        dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
         torch.cuda.set_device(0)
         m, n, l, qq, dt = case[:5]
         A = _matrix(case)
-        rows, off = R.row_partition(m, WORLD, rank)
+        rows, off = R.row_partition(m, world, rank)
         tdt = {"f64": torch.float64, "f32": torch.float32, "bf16": torch.bfloat16,
                "e4m3": torch.float8_e4m3fn}[dt]
         # e4m3: one per-tensor scale of the GLOBAL A (every rank the same a_scale)
         scale = float(np.abs(A).max()) / 448.0 if dt == "e4m3" else 1.0
         Ag = torch.from_numpy(np.ascontiguousarray(A[off:off + rows].T / scale)).cuda().to(tdt).t()
         eng = R.Engine(0)
-        eng.set_comm(rank, WORLD, shard_n=shard_n)
+        eng.set_comm(rank, world, shard_n=shard_n)
         U, S, V = eng.rsvd(Ag, l, q=qq, seed=4242, a_scale=scale, lowp_intermediates=lowp)
         torch.cuda.synchronize()
         nsh = eng.info()["n_shard_rows"]
-        assert (nsh == -(-(-(-n // WORLD)) // 32) * 32) if shard_n else nsh == 0, nsh
+        assert (nsh == -(-(-(-n // world)) // 32) * 32) if shard_n else nsh == 0, nsh
         q.put((rank, off, U.cpu().double().numpy(), S.cpu().double().numpy(), V.cpu().double().numpy(),
                Ag.float().cpu().double().numpy() * scale))
         eng.close()
@@ -78,16 +78,16 @@ def _worker(rank, port, case, q, shard_n, lowp=False):
         q.put((rank, None, traceback.format_exc(), None, None, None))
 
 
-def _run_world2(case, shard_n=True, lowp=False):
+def _run_world2(case, shard_n=True, lowp=False, world=WORLD):
     import torch.multiprocessing as mp
 
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, port, case, q, shard_n, lowp)) for r in range(WORLD)]
+    procs = [ctx.Process(target=_worker, args=(r, port, case, q, shard_n, lowp, world)) for r in range(world)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=300) for _ in range(WORLD)]
+    res = [q.get(timeout=300) for _ in range(world)]
     for p in procs:
         p.join(timeout=60)
     for r in res:
@@ -115,17 +115,19 @@ def test_row_sharded_rank_deficient_is_orthonormal(dt, shard_n):
     assert np.all(S[2:] < (1e-9 if dt == "f64" else 1e-5) * S[0])
 
 
-def _check_world2(case, shard_n, lowp=False):
+def _check_world2(case, shard_n, lowp=False, world=WORLD):
     import oracle
     from conftest import rel_fro, sign_align
 
     m, n, l, qq, dt = case
-    res = _run_world2(case, shard_n, lowp)
+    res = _run_world2(case, shard_n, lowp, world)
     U = np.vstack([r[2] for r in res])
     A = np.vstack([r[5] for r in res])  # the values the GPU saw (bf16 / fp32 rounded)
+    assert A.shape[0] == m
     S0, V0 = res[0][3], res[0][4]
     # every rank holds the same S and V
-    assert np.array_equal(S0, res[1][3]) and np.array_equal(V0, res[1][4])
+    for r in res[1:]:
+        assert np.array_equal(S0, r[3]) and np.array_equal(V0, r[4])
     # the same Omega the engine drew (Philox; rounded to bf16 for bf16 A)
     import torch
 
@@ -166,3 +168,17 @@ def test_row_sharded_world2_lowp_intermediates_sharded_n():
     only the bf16 hi/lo panels (no fp32 Out), which are what the all-gather moves -- the combination
     the opt-in bench variant runs at N > 1.  0.985^i spectrum (decays across the sketch), 1e-4 bar."""
     _check_world2((4096, 2048, 256, 2, "bf16"), True, lowp=True)
+
+
+@pytest.mark.parametrize("case", [(1501, 700, 96, 2, "f64"), (4099, 3000, 128, 2, "bf16"), (3002, 2000, 256, 2, "e4m3")])
+def test_row_sharded_world3_uneven_matches_oracle(case):
+    """Three ranks: m % 3 != 0, so rank 0 holds one row more than the others
+    by the reference's remainder rule (src/rSVD.cpp:20-23, rsvd_row_partition); n is not a
+    multiple of 3 x 32, so the last n shard carries zero padding rows; the e4m3 case's shards
+    (1001, 1001, 1000 rows) are not multiples of 16, which takes the sketch off the fp8 x fp8
+    kernel onto the widening one.  Against the oracle on the same A and Omega."""
+    import rsvd_kamaneh_raganato_terrana_amd as R
+
+    m = case[0]
+    assert [R.row_partition(m, 3, r)[0] for r in range(3)] == [m // 3 + (r < m % 3) for r in range(3)]
+    _check_world2(case, True, world=3)
