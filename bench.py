@@ -545,6 +545,9 @@ def main():
     eng.close()  # releases the handle's RCCL communicator (rsvd_destroy)
     if world > 1:
         dist.destroy_process_group()
+    if os.environ.get("RSVD_MAPS_OUT"):  # diagnostics: the process's mappings, to symbolise an exit-time fault
+        with open("/proc/self/maps") as f, open(os.environ["RSVD_MAPS_OUT"], "w") as g:
+            g.write(f.read())
 
 
 if __name__ == "__main__":

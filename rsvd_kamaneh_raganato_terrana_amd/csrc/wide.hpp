@@ -35,6 +35,7 @@ struct WProjPlan {
     bool tn2 = false; // v3 TN at LP = 256 with two k-steps per A slot (128-B A lines)
     bool half = false; // e4m3 A at LP = 512: two LP = 256 column-half launches (256-row tiles)
     bool tn4 = false;  // e4m3 TN at LP 256 / 512: four k-steps per A slot (128-B A lines, wproj3tn4_kernel)
+    bool merge = false; // LP = 512 halves (half / tn4) in ONE launch, twin blocks adjacent (A from HBM once)
     int abl = 0;      // lab-only ablations of the v3 kernel (tools/wide_lab.cpp), never set by the engine
     int kn = -1;      // lab-only knob override of the LP = 256 v3 kernels (-1: the engine's choice)
 };

@@ -391,7 +391,7 @@ __global__ __launch_bounds__(512) void wproj2_kernel(const void* __restrict__ Av
                                                      int64_t K, int64_t arows, const bf16_t* __restrict__ Shi,
                                                      const bf16_t* __restrict__ Slo, float* __restrict__ out,
                                                      int64_t slab_stride, int64_t kchunk, int nrowblk, int s_pitch,
-                                                     int o_pitch) {
+                                                     int o_pitch, int halves) {
     typedef W2Shape<LP, SPLIT, FP8, DS, S8, SC> SH;
     static_assert(!SC || S8, "scaled fp8 MFMA: e4m3 x e4m3 sketch only");
     static_assert(!DS || (!NN && !FP8), "double-step stages: bf16 TN only");
@@ -404,7 +404,15 @@ __global__ __launch_bounds__(512) void wproj2_kernel(const void* __restrict__ Av
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int r = lane & 15, h = lane >> 4, q = r >> 2, p = r & 3;
     const int wr = w % WR, wc = w / WR;
-    const int bid = xcd_remap(blockIdx.x, gridDim.x);
+    // halves = 2: the two 256-column halves of an LP = 512 product in one launch, as neighbouring
+    // logical blocks (same XCD, dispatched together), so the twin's A reads hit the L2
+    const int bid2 = xcd_remap(blockIdx.x, gridDim.x);
+    const int hf = bid2 % halves, bid = bid2 / halves;
+    if (hf) {
+        Shi = S8 ? reinterpret_cast<const bf16_t*>(reinterpret_cast<const uint8_t*>(Shi) + 256 * hf) : Shi + 256 * hf;
+        if (Slo) Slo += 256 * hf;
+        out += 256 * hf;
+    }
     const int rb = bid % nrowblk, sp = bid / nrowblk;
     const int64_t row0 = (int64_t)rb * WI;
     const int64_t kbeg = (int64_t)sp * kchunk;
@@ -1256,7 +1264,7 @@ __global__ __launch_bounds__(512) void wproj3tn4_kernel(const uint8_t* __restric
                                                         int64_t K, int64_t arows, const bf16_t* __restrict__ Shi,
                                                         const bf16_t* __restrict__ Slo, float* __restrict__ out,
                                                         int64_t slab_stride, int64_t kchunk, int nrowblk, int s_pitch,
-                                                        int o_pitch) {
+                                                        int o_pitch, int halves) {
     constexpr int LP = 256;
     typedef W3Shape<LP, false, SPLIT, 1> SH;
     typedef typename SH::SImg SImg;
@@ -1268,7 +1276,13 @@ __global__ __launch_bounds__(512) void wproj3tn4_kernel(const uint8_t* __restric
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int r = lane & 15, h = lane >> 4, q = r >> 2, p = r & 3;
     const int wr = w % WR, wc = w / WR;
-    const int bid = xcd_remap(blockIdx.x, gridDim.x);
+    const int bid2 = xcd_remap(blockIdx.x, gridDim.x);  // halves: as wproj2_kernel
+    const int hf = bid2 % halves, bid = bid2 / halves;
+    if (hf) {
+        Shi += 256 * hf;
+        if (Slo) Slo += 256 * hf;
+        out += 256 * hf;
+    }
     const int rb = bid % nrowblk, sp = bid / nrowblk;
     const int64_t row0 = (int64_t)rb * WI;
     const int64_t kbeg = (int64_t)sp * kchunk;
@@ -1417,12 +1431,20 @@ hipError_t wproj3tn4_go(const void* A, int64_t lda, int64_t m, int64_t n, const 
     const int64_t rows_out = n, K = m;
     float* o = p.splits == 1 ? Out : slabs;
     const int64_t stride = rows_out * LP;
-    for (int hf = 0; hf < LP / 256; ++hf) {
-        hipLaunchKernelGGL((wproj3tn4_kernel<SPLIT>), dim3(p.blocks * p.splits), dim3(512), lds, s,
-                           reinterpret_cast<const uint8_t*>(A), lda, rows_out, K, m, Shi + 256 * hf,
-                           Slo ? Slo + 256 * hf : nullptr, o + 256 * hf, stride, p.chunk, p.blocks, LP, LP);
+    if (LP == 512 && p.merge) {  // both halves in one launch (A read once, the twin from L2)
+        hipLaunchKernelGGL((wproj3tn4_kernel<SPLIT>), dim3(2 * p.blocks * p.splits), dim3(512), lds, s,
+                           reinterpret_cast<const uint8_t*>(A), lda, rows_out, K, m, Shi, Slo, o, stride, p.chunk,
+                           p.blocks, LP, LP, 2);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
+    } else {
+        for (int hf = 0; hf < LP / 256; ++hf) {
+            hipLaunchKernelGGL((wproj3tn4_kernel<SPLIT>), dim3(p.blocks * p.splits), dim3(512), lds, s,
+                               reinterpret_cast<const uint8_t*>(A), lda, rows_out, K, m, Shi + 256 * hf,
+                               Slo ? Slo + 256 * hf : nullptr, o + 256 * hf, stride, p.chunk, p.blocks, LP, LP, 1);
+            hipError_t e = hipGetLastError();
+            if (e != hipSuccess) return e;
+        }
     }
     hipError_t e = hipSuccess;
     if (done) e = hipEventRecord(done, s);
@@ -1475,7 +1497,7 @@ hipError_t wproj2_go(const void* A, int64_t lda, int64_t m, int64_t n, const bf1
     // (profiles/r02_wide_lab_knobs.txt).
     constexpr int KN = NN ? 3 : 0;
     hipLaunchKernelGGL((wproj2_kernel<FP8, NN, LP, SPLIT, DS, KN, S8, SC>), dim3(p.blocks * p.splits), dim3(512), SH::LDS,
-                       s, A, lda, rows_out, K, m, Shi, Slo, o, stride, p.chunk, p.blocks, LP, LP);
+                       s, A, lda, rows_out, K, m, Shi, Slo, o, stride, p.chunk, p.blocks, LP, LP, 1);
     hipError_t e = hipGetLastError();
     if (e == hipSuccess && done) e = hipEventRecord(done, s);
     if (e != hipSuccess || p.splits == 1) return e;
@@ -1496,15 +1518,24 @@ hipError_t wproj2_half_go(const void* A, int64_t lda, int64_t m, int64_t n, cons
     float* o = p.splits == 1 ? Out : slabs;
     const int64_t stride = rows_out * 512;
     constexpr int KN = NN ? 3 : 0;
-    for (int hf = 0; hf < 2; ++hf) {
-        // S column offset: 256 bf16 elements, or 256 bytes of an e4m3 panel (S8)
-        const bf16_t* sh = S8 ? reinterpret_cast<const bf16_t*>(reinterpret_cast<const uint8_t*>(Shi) + 256 * hf)
-                              : Shi + 256 * hf;
-        const bf16_t* sl = Slo ? Slo + 256 * hf : nullptr;
-        hipLaunchKernelGGL((wproj2_kernel<FP8, NN, 256, SPLIT, false, KN, S8, SC>), dim3(p.blocks * p.splits), dim3(512),
-                           SH::LDS, s, A, lda, rows_out, K, m, sh, sl, o + 256 * hf, stride, p.chunk, p.blocks, 512, 512);
+    if (p.merge) {  // both halves in one launch: neighbouring blocks share the A tile through the L2
+        hipLaunchKernelGGL((wproj2_kernel<FP8, NN, 256, SPLIT, false, KN, S8, SC>), dim3(2 * p.blocks * p.splits),
+                           dim3(512), SH::LDS, s, A, lda, rows_out, K, m, Shi, Slo, o, stride, p.chunk, p.blocks, 512,
+                           512, 2);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
+    } else {
+        for (int hf = 0; hf < 2; ++hf) {
+            // S column offset: 256 bf16 elements, or 256 bytes of an e4m3 panel (S8)
+            const bf16_t* sh = S8 ? reinterpret_cast<const bf16_t*>(reinterpret_cast<const uint8_t*>(Shi) + 256 * hf)
+                                  : Shi + 256 * hf;
+            const bf16_t* sl = Slo ? Slo + 256 * hf : nullptr;
+            hipLaunchKernelGGL((wproj2_kernel<FP8, NN, 256, SPLIT, false, KN, S8, SC>), dim3(p.blocks * p.splits),
+                               dim3(512), SH::LDS, s, A, lda, rows_out, K, m, sh, sl, o + 256 * hf, stride, p.chunk,
+                               p.blocks, 512, 512, 1);
+            hipError_t e = hipGetLastError();
+            if (e != hipSuccess) return e;
+        }
     }
     hipError_t e = hipSuccess;
     if (done) e = hipEventRecord(done, s);
@@ -1621,6 +1652,14 @@ static bool tn4_enabled() {  // RSVD_FP8_TN4=0 in the environment: the wproj2 e4
     return env != 0;
 }
 
+static bool half_merge_enabled() {
+    static const int env = [] {
+        const char* v = std::getenv("RSVD_HALF_MERGE");
+        return v ? std::atoi(v) : 1;
+    }();
+    return env != 0;
+}
+
 WProjPlan plan_wproj(int64_t rows_out, int64_t K, int LP, bool v2, bool nn, bool fp8) {
     WProjPlan p;
     p.v2 = v2 && LP >= 128;
@@ -1633,7 +1672,10 @@ WProjPlan plan_wproj(int64_t rows_out, int64_t K, int LP, bool v2, bool nn, bool
     const int WI = p.v2 ? (LP == 128 ? (p.ds ? 256 : 512) : ((LP == 256 || p.half) ? 256 : 128))
                         : wproj_rows_per_block(LP);
     p.blocks = (int)((rows_out + WI - 1) / WI);
-    const int target = (p.v2 || LP >= 512) ? 256 : 512;  // one workgroup per CU (LDS ring / registers)
+    // LP = 512 e4m3 products as two 256-column halves in one launch (RSVD_HALF_MERGE=0: two launches)
+    p.merge = (p.half || (p.tn4 && LP == 512)) && half_merge_enabled();
+    // one workgroup per CU (LDS ring / registers); merged halves: two workgroups per (row block, split)
+    const int target = p.merge ? 128 : ((p.v2 || LP >= 512) ? 256 : 512);
     int64_t splits = (target + p.blocks - 1) / p.blocks;
     const int64_t max_by_work = K / (KS * 8);
     if (splits > max_by_work) splits = max_by_work;
