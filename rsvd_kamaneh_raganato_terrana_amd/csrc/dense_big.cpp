@@ -118,13 +118,29 @@ struct QrBig {
 
     double tol() const { return sizeof(T) == 4 ? 1e-13 : 1e-28; }
 
+    // Row-sharded panels (rSVD() past 512 columns at world > 1): this rank holds rows of a global
+    // panel; the Grams and the block projections Qp^T Y are summed over the ranks (the all-reduce hook,
+    // src/rSVD.cpp:20-23's row partition), and repair draws use disjoint stream rows per rank.
+    bool shard = false;
+    int64_t row_off = 0, rows_total = 0, norm_rows = 0, rows_global = 0;
+    int allreduce(void* buf, int64_t count, int32_t dt) {
+        if (!shard || h->world <= 1 || !h->allreduce) return RSVD_OK;
+        if (h->allreduce(buf, count, dt, (void*)s, h->ar_user) != 0) {
+            h->err = "all-reduce hook failed";
+            return RSVD_ERR_COMM;
+        }
+        return RSVD_OK;
+    }
+
     // one CholeskyQR pass on a k-column panel (forward substitution: backward stable)
     int pass(const T* In, int k, T* Out, bool shift, const int* pred) {
         const int64_t rows = L.bo.rows;
         const int LP = L.bo.LP;
         int* flag = h->dflags + 4;
         RSVD_CK(launch_gram_wide<T>(In, nullptr, rows, LP, L.bo.gp, gslab, G, pred, s));
-        if (shift) RSVD_CK(launch_shift_diag(G, LP, k, rows, sizeof(T) == 4 ? 0x1p-24 : 0x1p-53, s));
+        RSVD_TRY(allreduce(G, (int64_t)LP * LP, RSVD_F64));
+        if (shift)
+            RSVD_CK(launch_shift_diag(G, LP, k, shard ? rows_global : rows, sizeof(T) == 4 ? 0x1p-24 : 0x1p-53, s));
         RSVD_CK(launch_chol_wide(G, k, LP, tol(), R, Rinv, sizeof(T) == 4 ? R32 : nullptr, colflag, flag, W, pred, s));
         RSVD_CK(launch_trsm_rows<T>(In, rows, k, LP, R, Out, pred, s));
         return RSVD_OK;
@@ -135,7 +151,11 @@ struct QrBig {
         RSVD_TRY(pass(P, k, T1, true, nullptr));
         RSVD_TRY(pass(T1, k, T2, false, nullptr));
         RSVD_TRY(pass(T2, k, Q, false, nullptr));
-        RSVD_CK(launch_repair_panel<T>(Q, rows, k, L.bo.LP, colflag, h->dflags + 4, seed, 0, rows, rows, T1, s));
+        if (shard)
+            RSVD_CK(launch_repair_panel<T>(Q, rows, k, L.bo.LP, colflag, h->dflags + 4, seed, row_off, rows_total,
+                                           norm_rows, T1, s));
+        else
+            RSVD_CK(launch_repair_panel<T>(Q, rows, k, L.bo.LP, colflag, h->dflags + 4, seed, 0, rows, rows, T1, s));
         RSVD_TRY(pass(T1, k, Q, false, h->dflags + 4));
         return RSVD_OK;
     }
@@ -143,6 +163,7 @@ struct QrBig {
     int project(const T* Qp, int64_t ldq, int64_t m, int64_t c0, int w) {
         if (c0 == 0) return RSVD_OK;
         RSVD_CK(launch_gemm<T>(1, 0, c0, w, m, T(1), Qp, ldq, Y, m, T(0), C, c0, s));
+        RSVD_TRY(allreduce(C, c0 * w, sizeof(T) == 8 ? RSVD_F64 : RSVD_F32));
         RSVD_CK(launch_gemm<T>(0, 0, m, w, c0, T(-1), Qp, ldq, C, c0, T(1), Y, m, s));
         return RSVD_OK;
     }
@@ -383,11 +404,30 @@ int big_rsvd_typed(rsvd_handle_t h, const rsvd_desc_t* d, const void* Av, const 
         RSVD_CK(launch_panel_to_colmajor<T>(X, n, (int)l, LPo, Om, n, s));
     }
     const uint64_t sd = d->seed ^ 0xB16Full;
+    // world > 1: this rank's rows of A (src/rSVD.cpp:20-23); the m-side panels stay row-sharded
+    // (their Grams and block projections all-reduced), A^T Q is all-reduced, the n side replicated
+    const int32_t tdt = sizeof(T) == 8 ? RSVD_F64 : RSVD_F32;
+    if (h->world > 1) {
+        Em.shard = true;
+        Em.row_off = (int64_t)h->rank << 40;
+        Em.rows_total = (int64_t)h->world << 40;
+        Em.norm_rows = (int64_t)h->world * m;
+        Em.rows_global = (int64_t)h->world * m;
+    }
+    auto reduce_z = [&]() -> int {
+        if (h->world <= 1 || !h->allreduce) return RSVD_OK;
+        if (h->allreduce(Z, n * l, tdt, (void*)s, h->ar_user) != 0) {
+            h->err = "all-reduce hook failed";
+            return RSVD_ERR_COMM;
+        }
+        return RSVD_OK;
+    };
     // intermediate_step (src/rSVD.cpp:57-70)
     RSVD_CK(launch_gemm<T>(0, 0, m, l, n, T(1), A, lda, Om, n, T(0), Y, m, s));  // Y = A Omega
     RSVD_TRY(Em.orth_cols(Y, m, l, Q, sd));
     for (int i = 0; i < d->q; ++i) {
         RSVD_CK(launch_gemm<T>(1, 0, n, l, m, T(1), A, lda, Q, m, T(0), Z, n, s));  // Z = A^T Q
+        RSVD_TRY(reduce_z());
         RSVD_TRY(En.orth_cols(Z, n, l, X, sd + 1000003ull * (2 * i + 1)));
         RSVD_CK(launch_gemm<T>(0, 0, m, l, n, T(1), A, lda, X, n, T(0), Y, m, s));  // Y = A X
         RSVD_TRY(Em.orth_cols(Y, m, l, Q, sd + 1000003ull * (2 * i + 2)));
@@ -398,6 +438,7 @@ int big_rsvd_typed(rsvd_handle_t h, const rsvd_desc_t* d, const void* Av, const 
     }
     // B^T = A^T Q, Q_B = orth(B^T), R = Q_B^T B^T (src/rSVD.cpp:89, SVD_class.hpp:116-123)
     RSVD_CK(launch_gemm<T>(1, 0, n, l, m, T(1), A, lda, Q, m, T(0), Z, n, s));
+    RSVD_TRY(reduce_z());
     RSVD_TRY(En.orth_cols(Z, n, l, X, sd + 7));
     RSVD_CK(launch_gemm<T>(1, 0, l, l, n, T(1), X, n, Z, n, T(0), R, l, s));
     const double* R64 = reinterpret_cast<const double*>(R);
@@ -477,9 +518,9 @@ int big_rsvd_run(rsvd_handle_t h, const rsvd_desc_t* d, const void* A, const voi
         h->err = "l > 4096 not supported (the block Jacobi small SVD is built for l <= 4096)";
         return RSVD_ERR_UNSUPPORTED;
     }
-    if (h->world > 1 || (d->flags & RSVD_FLAG_FORCE_NSHARD)) {
-        h->err = "l > 512 runs on one GPU (no row sharding past the wide engine's panels)";
-        return RSVD_ERR_UNSUPPORTED;
+    if (h->world > 1 && !h->allreduce) {
+        h->err = "a row-sharded rSVD needs the all-reduce hook (rsvd_set_comm / rsvd_comm_init)";
+        return RSVD_ERR_INVALID_ARG;
     }
     if (!Qout && (d->method == RSVD_SVD_POWER || d->method == RSVD_SVD_POWER_IC)) {
         h->err = "SVDMethod::Power is built for l <= 512";

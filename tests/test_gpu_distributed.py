@@ -182,3 +182,12 @@ def test_row_sharded_world3_uneven_matches_oracle(case):
     m = case[0]
     assert [R.row_partition(m, 3, r)[0] for r in range(3)] == [m // 3 + (r < m % 3) for r in range(3)]
     _check_world2(case, True, world=3)
+
+
+@pytest.mark.parametrize("case", [(1600, 1000, 768, 1, "f32"), (2001, 1200, 640, 1, "bf16")])
+def test_row_sharded_world2_l_past_512(case):
+    """rSVD() past the wide engine's 512 sketch columns on two ranks: the
+    dense_big.cpp path with its m-side panels row-sharded (Grams and block projections all-reduced,
+    disjoint repair rows) and A^T Q all-reduced (the n side replicated); the reference has no cap on
+    l (src/rSVD.cpp:72).  Uneven 2001-row split in the bf16 case.  Against the oracle, 1e-4."""
+    _check_world2(case, False)
