@@ -434,6 +434,7 @@ def main():
     key = f"{args.config}_{dt}_{m_local}x{n}_l{l}_q{q}"
     lowp = dt in ("bf16", "fp8")
     per_op = 1  # kernel dispatches per timed projection (the HIP events bracket the whole product)
+    merged_off = os.environ.get("RSVD_HALF_MERGE") == "0"  # LP = 512 e4m3 halves as two dispatches
     if lowp:  # the LDS-DMA kernels (hi/lo split skinny operand): wproj3 (bf16, LP 256 / 512; TN at
         # LP 256 with two-step A slots: wproj3tn2), wproj3tn4 (e4m3 TN, four-step A slots),
         # wproj2<FP8, NN, LP, SPLIT> otherwise
@@ -443,12 +444,12 @@ def main():
             kpref = "wproj3tn2_kernel<true"
         elif dt == "fp8" and LPk in (256, 512) and not nn and os.environ.get("RSVD_FP8_TN4") != "0":
             kpref = "wproj3tn4_kernel<true"  # e4m3 TN, 128-B A lines; LP = 512 as two column halves
-            per_op = LPk // 256
+            per_op = LPk // 256 if merged_off else 1  # (both halves in one dispatch by default)
         elif dt == "bf16" and LPk in (256, 512):
             kpref = f"wproj3_kernel<{'true' if nn else 'false'}, {LPk}, true"
-        elif dt == "fp8" and LPk == 512:  # two 256-column half launches per product (WProjPlan::half)
+        elif dt == "fp8" and LPk == 512:  # two 256-column halves per product (WProjPlan::half), one dispatch
             kpref = f"wproj2_kernel<true, {'true' if nn else 'false'}, 256, true"
-            per_op = 2
+            per_op = 2 if merged_off else 1
         else:
             kpref = f"wproj2_kernel<{'true' if dt == 'fp8' else 'false'}, {'true' if nn else 'false'}, {LPk}, true"
     else:
