@@ -14,7 +14,8 @@
 //   4. the eigenvectors of T by inverse iteration (tridiag_invit_kernel: one thread per vector,
 //      LU with partial pivoting of T - lambda I, LAPACK dlagtf/dlagts semantics); vectors whose
 //      eigenvalues are closer than kClusterTol |lambda|_max are re-orthogonalised (CGS2,
-//      cluster_orth_kernel) -- inverse iteration only needs that inside clusters;
+//      cluster_orth_kernel), then one Newton-Schulz step over all of Z (two GEMMs) removes the
+//      eps / gap_rel non-orthogonality of close but separated pairs;
 //   5. V_w = Q_H Z: compact-WY blocks of 32 reflectors (wy_t_kernel builds T_b, wy_apply_kernel
 //      applies them to 16-column blocks of Z held in LDS, fp64 MFMA);
 //   6. X = W V_w (fp64 MFMA GEMM); then wide_svd.hip's block Jacobi runs in "given" mode: it
@@ -47,8 +48,13 @@ typedef Mfma<double> MD;
 constexpr double kEpsE = 2.220446049250313e-16;
 constexpr int kEigThreads = 512;
 constexpr int kEigMaxN = 512;
-// eigenvalues within kClusterTol * max|lambda| of their neighbour: re-orthogonalised vectors
-constexpr double kClusterTol = 1e-9;
+// eigenvalues within kClusterTol * max|lambda| of their neighbour (exact or near-exact
+// degeneracies, where inverse iteration from random starts returns random vectors of the
+// eigenspace): CGS2 of the cluster's vectors, in order.  Every other pair is orthogonal to
+// ~eps / gap_rel <= 2e-4 after inverse iteration, and one Newton-Schulz step Z (3 I - Z^T Z) / 2 over
+// the whole Z squares that (its mixing of a pair i, j is ~eps |G| / |lam_i - lam_j|, so the eigen
+// residuals stay at eps |G|).
+constexpr double kClusterTol = 1e-12;
 // sync words (in the block-Jacobi sync block, past its own 384): hand-off counter, abort
 constexpr int kTriCtr = 448, kTriAbort = 449;
 
@@ -101,219 +107,320 @@ __device__ bool tri_barrier(unsigned* sync, unsigned target) {
     return ok != 0;
 }
 
-// Householder reflector of the row `row` (LDS, this row of the current matrix) for column k:
-// x = row[k+1 .. n), H = I - tau v v^T with v[k+1] = 1, H x = beta e_{k+1} (LAPACK dlarfg: tau = 0
-// when x[k+2 ..] = 0).  Writes v into vout[0 .. n) (zeros up to k); returns tau, beta.
-__device__ __forceinline__ void house(const double* row, int k, int n, double* vout, double* red, int& tog,
-                                      double& tau, double& beta) {
-    const int tid = threadIdx.x;
-    double xj = 0.0;
-    for (int j = tid; j < n; j += kEigThreads)
-        if (j > k + 1) xj += row[j] * row[j];
-    const double xn2 = block_sum512(xj, red, tog);
-    const double a0 = row[k + 1];
-    double scal = 0.0;
-    if (xn2 == 0.0) {
-        tau = 0.0;
-        beta = a0;
-    } else {
-        const double nr = sqrt(a0 * a0 + xn2);
-        beta = a0 >= 0.0 ? -nr : nr;
-        tau = (beta - a0) / beta;
-        scal = 1.0 / (a0 - beta);
-    }
-    for (int j = tid; j < kEigMaxN; j += kEigThreads)
-        vout[j] = (j == k + 1) ? 1.0 : ((j > k + 1 && j < n) ? row[j] * scal : 0.0);
+// Sum over the LPR lanes of a lane group (lanes g LPR .. g LPR + LPR - 1), every lane gets the total.
+template <int LPR>
+__device__ __forceinline__ double group_sum(double v) {
+#pragma unroll
+    for (int o = LPR / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
 }
 
-// Householder tridiagonalisation of the symmetric n x n G (column-major, ld; n <= 512) by NW
-// workgroups.  Row i belongs to workgroup i % NW (cyclic: every member keeps active rows to the
-// end), local row li = i / NW held by wave li % 8 in register slot li / 8; lane holds columns
-// lane + 64 u.  Step k (A_k -> A_{k+1} = H_k A_k H_k):
-//   p = tau_k A_k v_k       each member its rows, published (row-group hand-off, double-buffered by
-//                           step parity) with the pivot row k + 1 of A_k by its owner;
-//   K = tau_k / 2 v_k.p, w = p - K v_k, row k+1 of A_{k+1} = row - w - w_{k+1} v_k;
-//   v_{k+1}, tau_{k+1}      from that row, identical on every member (fixed-order sums);
-//   A_{k+1} = A_k - v w^T - w v^T on the registers, fused with the next partial product.
-// Out: d (n), e (n - 1), tau (n - 2) and the reflectors as columns of Y (ld; v_k[k+1] = 1).
-template <int RT, int CT, int NW>
-__global__ __launch_bounds__(kEigThreads) void tridiag_kernel(const double* __restrict__ G, int ld, int n,
-                                                              double* __restrict__ Y, double* __restrict__ dvec,
-                                                              double* __restrict__ evec, double* __restrict__ taus,
+// Householder tridiagonalisation of the symmetric G (LAPACK dsytd2's reflectors, v_k[k+1] = 1), in
+// one or two launches:
+//   phase 1: NW workgroups hold the rows of G in registers (row i on workgroup i % NW: every member
+//            keeps active rows to the end) and run steps 0 .. kend - 1 with ONE hand-off per step,
+//            then dump the trailing block (rows / columns >= kend + 1) of A_kend;
+//   phase 2: one workgroup loads that block (t <= 192 rows: it fits the registers) and finishes the
+//            steps kend .. n - 3 with workgroup barriers only.
+// Register layout: a wave is G = 64 / LPR groups of LPR lanes (lane = g LPR + c); lane (g, c) holds
+// RPL rows -- local row q (8 G) + w G + g of the workgroup -- at the CPL columns c + LPR u.  Local row
+// li of workgroup wg is row off + li NW + wg of the matrix, local column j is column off + j.
+// Step k (A_k -> A_{k+1} = H_k A_k H_k, LAPACK dsytd2 / dlatrd without the blocking):
+//   [A] p = tau_k A_k v_k (each member its rows: a reduction over LPR lanes per row), the per-wave
+//       partials of v_k . p, and the pivot row k + 1 of A_k by its owner -- to LDS (one workgroup) or
+//       published (sc1 stores, the row-group hand-off, double-buffered by step parity);
+//   [C] K = tau_k / 2 v_k . p (the partials summed in one fixed order: bit-identical on every
+//       member), w = p - K v_k, the pivot row of A_{k+1} = row - w - w_{k+1} v_k, |row[k+3 ..]|^2;
+//   [E] v_{k+1}, tau_{k+1}, beta (= e_{k+1}) from that row, identical on every member;
+//   [D] A_{k+1} = A_k - v w^T - w v^T on the registers, fused with the next partial products.
+// Out: d (n), e (n - 1), tau (n - 2) and the reflectors as the columns of Y (ldy; v_k[k+1] = 1).
+template <int RPL, int CPL, int LPR, int NW>
+__global__ __launch_bounds__(kEigThreads) void tridiag_kernel(const double* __restrict__ src, int lds, int n, int off,
+                                                              int kend, double* __restrict__ Y, int ldy,
+                                                              double* __restrict__ dvec, double* __restrict__ evec,
+                                                              double* __restrict__ taus, double* __restrict__ dump,
                                                               double* __restrict__ xch, unsigned* __restrict__ sync,
                                                               int* __restrict__ info) {
-    constexpr int RPW = 8 * RT;                  // rows per member
-    constexpr int XS = NW * RPW + kEigMaxN;      // one parity's exchange slots: p, then the pivot row
+    constexpr int G = 64 / LPR;
+    constexpr int RPW = 8 * G * RPL;                     // rows per member
+    constexpr int XS = NW * RPW + 8 * NW + kEigMaxN;     // one parity's exchange slots: p, v.p partials, row
     __shared__ double vb[2][kEigMaxN];
     __shared__ double ps[kEigMaxN], ws[kEigMaxN], rs[kEigMaxN];
-    __shared__ double red[16];
+    __shared__ double vpw[8 * NW];
+    __shared__ double red[8];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int g = blockIdx.x;
-    int tog = 0;
+    const int g = lane / LPR, c = lane % LPR;
+    const int wg = blockIdx.x;
+    const int t = n - off;  // local size
     if (n <= 2) {
-        if (g == 0 && tid == 0) {
-            dvec[0] = G[0];
+        if (wg == 0 && tid == 0) {
+            dvec[0] = src[0];
             if (n == 2) {
-                dvec[1] = G[(int64_t)ld + 1];
-                evec[0] = G[1];
+                dvec[1] = src[(int64_t)lds + 1];
+                evec[0] = src[1];
             }
         }
         return;
     }
-    double a[RT][CT];
+    auto lrow = [&](int q) { return (q * (8 * G) + w * G + g) * NW + wg; };  // local row of slot q
+    double a[RPL][CPL];
 #pragma unroll
-    for (int t = 0; t < RT; ++t) {
-        const int i = (w + 8 * t) * NW + g;
+    for (int q = 0; q < RPL; ++q) {
+        const int i = lrow(q);
 #pragma unroll
-        for (int u = 0; u < CT; ++u) {
-            const int j = lane + 64 * u;
-            a[t][u] = (i < n && j < n) ? G[(int64_t)i * ld + j] : 0.0;  // G(j, i) = G(i, j)
+        for (int u = 0; u < CPL; ++u) {
+            const int j = c + LPR * u;
+            a[q][u] = (i < t && j < t) ? src[(int64_t)i * lds + j] : 0.0;  // symmetric: row i = column i
         }
     }
-    for (int j = tid; j < kEigMaxN; j += kEigThreads) rs[j] = j < n ? G[j] : 0.0;  // row 0
-    __syncthreads();
-    double tau, beta;
-    house(rs, 0, n, vb[0], red, tog, tau, beta);
-    if (g == 0) {
-        for (int j = tid; j < ld; j += kEigThreads) Y[j] = j < n ? vb[0][j] : 0.0;
-        if (tid == 0) {
+    const int kbeg = off == 0 ? 0 : off - 1;
+    double tau;
+    if (off == 0) {
+        // v_0 from row 0 (LAPACK dlarfg: tau = 0 when the column below the subdiagonal is zero)
+        for (int j = tid; j < kEigMaxN; j += kEigThreads) rs[j] = j < n ? src[j] : 0.0;
+        __syncthreads();
+        double xj = 0.0;
+        for (int j = tid; j < n; j += kEigThreads)
+            if (j > 1) xj += rs[j] * rs[j];
+        xj = warp_sum(xj);
+        if (lane == 0) red[w] = xj;
+        __syncthreads();
+        double xn2 = 0.0;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) xn2 += red[q];
+        const double a0 = rs[1];
+        double beta = a0, scal = 0.0;
+        tau = 0.0;
+        if (xn2 != 0.0) {
+            const double nr = sqrt(a0 * a0 + xn2);
+            beta = a0 >= 0.0 ? -nr : nr;
+            tau = (beta - a0) / beta;
+            scal = 1.0 / (a0 - beta);
+        }
+        for (int j = tid; j < kEigMaxN; j += kEigThreads) {
+            const double v = (j == 1) ? 1.0 : ((j > 1 && j < n) ? rs[j] * scal : 0.0);
+            vb[0][j] = v;
+            if (wg == 0 && j < n) Y[j] = v;
+        }
+        if (wg == 0 && tid == 0) {
             dvec[0] = rs[0];
             evec[0] = beta;
             taus[0] = tau;
         }
+    } else {
+        // phase 2: v_kbeg (written to Y by phase 1) in local coordinates
+        for (int j = tid; j < kEigMaxN; j += kEigThreads) vb[0][j] = j < t ? Y[(int64_t)kbeg * ldy + off + j] : 0.0;
+        tau = taus[kbeg];
     }
     __syncthreads();
-    double s[RT];
+    double s[RPL];
 #pragma unroll
-    for (int t = 0; t < RT; ++t) {
+    for (int q = 0; q < RPL; ++q) {
         double acc = 0.0;
 #pragma unroll
-        for (int u = 0; u < CT; ++u) acc += a[t][u] * vb[0][lane + 64 * u];
-        s[t] = acc;
+        for (int u = 0; u < CPL; ++u) acc += a[q][u] * vb[0][c + LPR * u];
+        s[q] = acc;
     }
     int cur = 0;
-    for (int k = 0; k <= n - 3; ++k) {
+    for (int k = kbeg; k < kend; ++k) {
         const double* vc = vb[cur];
         double* vn = vb[cur ^ 1];
-        double* xp = xch + (int64_t)(k & 1) * XS;  // this step's slots
-        // A. publish p = tau A_k v_k (rows > k; zero for rows <= k) and the pivot row k + 1
+        const int l1 = k + 1 - off;  // local index of the pivot row k + 1
+        double* xp = xch + (int64_t)((k - kbeg) & 1) * XS;
+        // [A] p, the v.p partials and the pivot row
+        double pv = 0.0;
 #pragma unroll
-        for (int t = 0; t < RT; ++t) {
-            const double tot = warp_sum(s[t]);
-            const int li = w + 8 * t, i = li * NW + g;
-            if (lane == 0 && i < n) {
-                const double pv = i > k ? tau * tot : 0.0;
-                if constexpr (NW == 1) ps[i] = pv;
-                else st_wt(xp + g * RPW + li, pv);
+        for (int q = 0; q < RPL; ++q) {
+            const double tot = group_sum<LPR>(s[q]);
+            const int li = lrow(q);
+            const double p = (li < t && li > l1 - 1) ? tau * tot : 0.0;  // rows > k
+            pv += vc[li < kEigMaxN ? li : 0] * p;
+            if (c == 0 && li < t) {
+                if constexpr (NW == 1) ps[li] = p;
+                else st_wt(xp + wg * RPW + (li - wg) / NW, p);
             }
         }
-        if ((k + 1) % NW == g) {
-            const int li1 = (k + 1) / NW;
-            if (w == (li1 & 7)) {
+        // wave partial of v.p over the group leaders (fixed butterfly: identical on every member)
+        pv = c == 0 ? pv : 0.0;
+        pv = warp_sum(pv);
+        if (lane == 0) {
+            if constexpr (NW == 1) vpw[w] = pv;
+            else st_wt(xp + NW * RPW + wg * 8 + w, pv);
+        }
+        if (l1 % NW == wg) {
+            const int li1 = l1 / NW;
+            const int q1 = li1 / (8 * G), rem = li1 % (8 * G);
+            if (w == rem / G && g == rem % G) {
 #pragma unroll
-                for (int t = 0; t < RT; ++t) {
-                    if (t == (li1 >> 3)) {
+                for (int q = 0; q < RPL; ++q)
+                    if (q == q1) {
 #pragma unroll
-                        for (int u = 0; u < CT; ++u) {
-                            const int j = lane + 64 * u;
-                            if (j < n) {
-                                if constexpr (NW == 1) rs[j] = a[t][u];
-                                else st_wt(xp + NW * RPW + j, a[t][u]);
+                        for (int u = 0; u < CPL; ++u) {
+                            const int j = c + LPR * u;
+                            if (j < t) {
+                                if constexpr (NW == 1) rs[j] = a[q][u];
+                                else st_wt(xp + NW * RPW + 8 * NW + j, a[q][u]);
                             }
                         }
                     }
-                }
             }
         }
-        // B. the hand-off
+        // [B] the hand-off
         if constexpr (NW > 1) {
-            if (!tri_barrier(sync, (unsigned)NW * (unsigned)(k + 1))) {
+            if (!tri_barrier(sync, (unsigned)NW * (unsigned)(k - kbeg + 1))) {
                 if (tid == 0) info[2] = 1;
                 return;
             }
-            for (int j = tid; j < n; j += kEigThreads) {
+            for (int j = tid; j < t; j += kEigThreads) {
                 ps[j] = ld_wt(xp + (j % NW) * RPW + j / NW);
-                rs[j] = ld_wt(xp + NW * RPW + j);
+                rs[j] = ld_wt(xp + NW * RPW + 8 * NW + j);
+            }
+            if (tid < 8 * NW) vpw[tid] = ld_wt(xp + NW * RPW + tid);
+        }
+        __syncthreads();
+        // [C] K, w, the pivot row of A_{k+1}, |row[k+3 ..]|^2
+        double kk = lane < 8 * NW ? vpw[lane] : 0.0;
+        kk = warp_sum(kk);
+        const double K = 0.5 * tau * kk;
+        const double wk1 = ps[l1] - K * vc[l1];
+        double xq = 0.0;
+        for (int j = tid; j < kEigMaxN; j += kEigThreads) {
+            const double wj = j < t ? ps[j] - K * vc[j] : 0.0;
+            ws[j] = wj;
+            if (j >= l1 && j < t) {
+                const double rj = rs[j] - wj - wk1 * vc[j];
+                rs[j] = rj;
+                if (j > l1 + 1) xq += rj * rj;
             }
         }
+        xq = warp_sum(xq);
+        if (lane == 0) red[w] = xq;
         __syncthreads();
-        // C. K, w, the pivot row of A_{k+1}, the next reflector
-        double dv = 0.0;
-        for (int j = tid; j < n; j += kEigThreads) dv += vc[j] * ps[j];
-        const double K = 0.5 * tau * block_sum512(dv, red, tog);
-        const double wk1 = ps[k + 1] - K * vc[k + 1];
-        for (int j = tid; j < kEigMaxN; j += kEigThreads) {
-            const double wj = j < n ? ps[j] - K * vc[j] : 0.0;
-            ws[j] = wj;
-            if (j > k && j < n) rs[j] = rs[j] - wj - wk1 * vc[j];  // row k + 1 of A_{k+1} (own j only)
-        }
-        __syncthreads();
-        double taun = 0.0, betan = 0.0;
+        // [E] the next reflector
+        double taun = 0.0;
         if (k + 1 <= n - 3) {
-            house(rs, k + 1, n, vn, red, tog, taun, betan);
-            if (g == 0) {
-                for (int j = tid; j < ld; j += kEigThreads) Y[(int64_t)(k + 1) * ld + j] = j < n ? vn[j] : 0.0;
-                if (tid == 0) {
-                    dvec[k + 1] = rs[k + 1];
-                    evec[k + 1] = betan;
-                    taus[k + 1] = taun;
-                }
+            double xn2 = 0.0;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) xn2 += red[q];
+            const double a0 = rs[l1 + 1];
+            double beta = a0, scal = 0.0;
+            if (xn2 != 0.0) {
+                const double nr = sqrt(a0 * a0 + xn2);
+                beta = a0 >= 0.0 ? -nr : nr;
+                taun = (beta - a0) / beta;
+                scal = 1.0 / (a0 - beta);
+            }
+            for (int j = tid; j < kEigMaxN; j += kEigThreads) {
+                const double v = (j == l1 + 1) ? 1.0 : ((j > l1 + 1 && j < t) ? rs[j] * scal : 0.0);
+                vn[j] = v;
+                if (wg == 0 && j < t) Y[(int64_t)(k + 1) * ldy + off + j] = v;
+            }
+            if (wg == 0 && tid == 0) {
+                dvec[k + 1] = rs[l1];
+                evec[k + 1] = beta;
+                taus[k + 1] = taun;
             }
         } else {
             for (int j = tid; j < kEigMaxN; j += kEigThreads) vn[j] = 0.0;
-            if (g == 0 && tid == 0) {
-                dvec[n - 2] = rs[n - 2];
-                evec[n - 2] = rs[n - 1];
+            if (wg == 0 && tid == 0) {
+                dvec[n - 2] = rs[l1];
+                evec[n - 2] = rs[l1 + 1];
             }
         }
         __syncthreads();
-        // D. A_{k+1} = A_k - v w^T - w v^T on the registers, and the next partial product
-        double vj[CT], wj[CT], vnj[CT];
+        // [D] A_{k+1} = A_k - v w^T - w v^T on the registers, and the next partial products; columns
+        // in groups of 4 with a compiler memory barrier between groups, so the LDS reads of v, w, v'
+        // are not all hoisted ahead (that kept 3 CPL extra doubles live and spilled)
+        double vi[RPL], wi[RPL];
 #pragma unroll
-        for (int u = 0; u < CT; ++u) {
-            vj[u] = vc[lane + 64 * u];
-            wj[u] = ws[lane + 64 * u];
-            vnj[u] = vn[lane + 64 * u];
+        for (int q = 0; q < RPL; ++q) {
+            const int li = lrow(q);
+            const int lc = li < kEigMaxN ? li : kEigMaxN - 1;
+            vi[q] = li < t ? vc[lc] : 0.0;
+            wi[q] = li < t ? ws[lc] : 0.0;
+            s[q] = 0.0;
         }
 #pragma unroll
-        for (int t = 0; t < RT; ++t) {
-            const int i = (w + 8 * t) * NW + g;
-            const int ii = i < kEigMaxN ? i : kEigMaxN - 1;
-            const double vi = i < n ? vc[ii] : 0.0, wi = i < n ? ws[ii] : 0.0;
-            double acc = 0.0;
+        for (int u0 = 0; u0 < CPL; u0 += 4) {
 #pragma unroll
-            for (int u = 0; u < CT; ++u) {
-                a[t][u] -= vi * wj[u] + wi * vj[u];
-                acc += a[t][u] * vnj[u];
-            }
-            s[t] = acc;
-            if (k == n - 3 && i == n - 1) {  // the last diagonal entry, from its owner
+            for (int u = u0; u < (u0 + 4 < CPL ? u0 + 4 : CPL); ++u) {
+                const int j = c + LPR * u;
+                const double wj = ws[j], vj = vc[j], vnj = vn[j];
 #pragma unroll
-                for (int u = 0; u < CT; ++u)
-                    if (lane + 64 * u == n - 1) dvec[n - 1] = a[t][u];
+                for (int q = 0; q < RPL; ++q) {
+                    a[q][u] -= vi[q] * wj + wi[q] * vj;
+                    s[q] += a[q][u] * vnj;
+                }
             }
+            asm volatile("" ::: "memory");
+        }
+        if (k == n - 3) {  // the last diagonal entry, from its owner
+#pragma unroll
+            for (int q = 0; q < RPL; ++q)
+                if (lrow(q) == t - 1) {
+#pragma unroll
+                    for (int u = 0; u < CPL; ++u)
+                        if (c + LPR * u == t - 1) dvec[n - 1] = a[q][u];
+                }
         }
         tau = taun;
         cur ^= 1;
+    }
+    if (kend < n - 2) {  // phase 1 ends: the trailing block of A_kend (rows / columns >= kend + 1)
+        const int o2 = kend + 1 - off;
+#pragma unroll
+        for (int q = 0; q < RPL; ++q) {
+            const int li = lrow(q);
+            if (li >= o2 && li < t) {
+#pragma unroll
+                for (int u = 0; u < CPL; ++u) {
+                    const int j = c + LPR * u;
+                    if (j >= o2 && j < t) dump[(int64_t)(li - o2) * lds + (j - o2)] = a[q][u];
+                }
+            }
+        }
     }
 }
 
 // Number of eigenvalues of T (d, e2 = e^2, both LDS) below x: sign changes of the leading principal
 // minors p_i = (d_i - x) p_{i-1} - e2_{i-1} p_{i-2} (Sturm sequence; an exact zero counts as a change),
 // with a power-of-two rescale every 8 steps (the ratios -- all the count uses -- are unchanged).
+// The chain is one dependent FMA per step; the LDS operands of the next 8 steps are read into
+// registers (ds_read_b128 pairs) while the current 8 run, so no step waits on an LDS round trip.
+// d[i], e2[i] must be readable (any value) up to index n + 8.
 __device__ __forceinline__ int sturm_count(const double* d, const double* e2, int n, double x) {
     double p0 = 1.0, p1 = d[0] - x;
     if (p1 == 0.0) p1 = -1e-300;
     int c = p1 < 0.0;
-    int i = 1;
-    while (i < n) {
-        const int iend = min(n, i + 8);
-        for (; i < iend; ++i) {
-            double p2 = (d[i] - x) * p1 - e2[i - 1] * p0;
-            if (p2 == 0.0) p2 = p1 < 0.0 ? 1e-300 : -1e-300;
-            c += (p2 < 0.0) != (p1 < 0.0);
-            p0 = p1;
-            p1 = p2;
+    // chunk i0 = 1 + 8 q covers steps i0 .. i0 + 7 (d[i], e2[i - 1])
+    double dn[8], en[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+        dn[u] = d[1 + u];
+        en[u] = e2[u];
+    }
+    for (int i0 = 1; i0 < n; i0 += 8) {
+        double dc[8], ec[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            dc[u] = dn[u] - x;
+            ec[u] = en[u];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            dn[u] = d[i0 + 8 + u];
+            en[u] = e2[i0 + 7 + u];
+        }
+        const int m = n - i0 < 8 ? n - i0 : 8;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            if (u < m) {
+                double p2 = fma(dc[u], p1, -ec[u] * p0);
+                if (p2 == 0.0) p2 = p1 < 0.0 ? 1e-300 : -1e-300;
+                c += (p2 < 0.0) != (p1 < 0.0);
+                p0 = p1;
+                p1 = p2;
+            }
         }
         const int ex = __builtin_amdgcn_frexp_exp(fmax(fabs(p0), fabs(p1)));
         p0 = __builtin_ldexp(p0, -ex);
@@ -327,7 +434,7 @@ __device__ __forceinline__ int sturm_count(const double* d, const double* e2, in
 // T is scaled by its Gershgorin bound first; tnorm[0] = that bound (inverse iteration's scale).
 __global__ __launch_bounds__(256) void tridiag_bisect_kernel(const double* __restrict__ dg, const double* __restrict__ eg,
                                                              int n, double* __restrict__ lam, double* __restrict__ tnorm) {
-    __shared__ double d[kEigMaxN], e2[kEigMaxN];
+    __shared__ double d[kEigMaxN + 16], e2[kEigMaxN + 16];  // + the prefetch overrun of sturm_count
     __shared__ double rlo[4], rhi[4];
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     double lo = 1e300, hi = -1e300;
@@ -347,8 +454,8 @@ __global__ __launch_bounds__(256) void tridiag_bisect_kernel(const double* __res
     hi = fmax(fmax(rhi[0], rhi[1]), fmax(rhi[2], rhi[3]));
     const double nrm = fmax(fabs(lo), fabs(hi));
     const double inv = nrm > 0.0 ? 1.0 / nrm : 0.0;
-    for (int i = tid; i < n; i += 256) {
-        d[i] = dg[i] * inv;
+    for (int i = tid; i < kEigMaxN + 16; i += 256) {
+        d[i] = i < n ? dg[i] * inv : 0.0;
         const double es = i + 1 < n ? eg[i] * inv : 0.0;
         e2[i] = es * es;
     }
@@ -386,9 +493,12 @@ __device__ __forceinline__ double unit_hash(uint64_t x) {
 }
 
 // Inverse iteration for every eigenvalue: thread k factors T - lam_k I = P L U (partial pivoting,
-// LAPACK dlagtf; |u_ii| below eps |T| is replaced by +-eps |T|) and runs three solves from a
-// pseudo-random start, rescaling by the largest entry between solves; the unit vector goes to
-// row-major Z (Z[i][k], ld ldz).  Scratch: six n x ldz arrays laid out [i][k] (coalesced over k).
+// LAPACK dlagtf; |u_ii| below eps |T| is replaced by +-eps |T|) and runs two solves from a
+// pseudo-random start -- the first forward elimination fused into the factorisation, the second
+// solve rescaled by the first's largest entry -- and writes the unit vector to row-major Z
+// (Z[i][k], ld ldz).  Scratch: six n x ldz arrays laid out [i][k] (a wave's 64 vectors read and
+// write 512 contiguous bytes per step).  The serial chains never wait on memory: each loop reads
+// the operands of its next 8 steps into registers while the current 8 run.
 __global__ __launch_bounds__(64) void tridiag_invit_kernel(const double* __restrict__ dg, const double* __restrict__ eg,
                                                            const double* __restrict__ lam, const double* __restrict__ tnorm,
                                                            int n, int ldz, double* __restrict__ Z,
@@ -396,12 +506,12 @@ __global__ __launch_bounds__(64) void tridiag_invit_kernel(const double* __restr
     const int k = blockIdx.x * 64 + threadIdx.x;
     if (k >= n) return;
     const int64_t S = (int64_t)n * ldz;
-    double* U0i = scr;
-    double* U1 = scr + S;
-    double* U2 = scr + 2 * S;
-    double* Lm = scr + 3 * S;
-    double* Pv = scr + 4 * S;
-    double* X = scr + 5 * S;
+    double* __restrict__ U0i = scr;
+    double* __restrict__ U1 = scr + S;
+    double* __restrict__ U2 = scr + 2 * S;
+    double* __restrict__ Lm = scr + 3 * S;
+    double* __restrict__ Pv = scr + 4 * S;
+    double* __restrict__ X = scr + 5 * S;
     auto at = [&](int i) { return (int64_t)i * ldz + k; };
     const double lk = lam[k];
     const double tol = kEpsE * fmax(tnorm[0], 1e-300);
@@ -409,10 +519,11 @@ __global__ __launch_bounds__(64) void tridiag_invit_kernel(const double* __restr
         if (fabs(u) < tol) u = u < 0.0 ? -tol : tol;
         return 1.0 / u;
     };
-    // factor
-    double cd = dg[0] - lk, cu = n > 1 ? eg[0] : 0.0;
+    auto rnd = [&](int i) { return unit_hash(((uint64_t)k << 32) ^ (uint64_t)i ^ 0x5EED5EEDull); };
+    // pass 1: factor, forward elimination of the random right-hand side on the fly (y into X)
+    double cd = dg[0] - lk, cu = n > 1 ? eg[0] : 0.0, yc = rnd(0);
     for (int i = 0; i < n - 1; ++i) {
-        const double bi = eg[i], an = dg[i + 1] - lk, cn = i + 1 < n - 1 ? eg[i + 1] : 0.0;
+        const double bi = eg[i], an = dg[i + 1] - lk, cn = i + 1 < n - 1 ? eg[i + 1] : 0.0, yn = rnd(i + 1);
         if (fabs(bi) > fabs(cd)) {
             const double m = cd / bi;
             U0i[at(i)] = pivot_inv(bi);
@@ -420,6 +531,8 @@ __global__ __launch_bounds__(64) void tridiag_invit_kernel(const double* __restr
             U2[at(i)] = cn;
             Lm[at(i)] = m;
             Pv[at(i)] = 1.0;
+            X[at(i)] = yn;
+            yc = yc - m * yn;
             cd = cu - m * an;
             cu = -m * cn;
         } else {
@@ -429,45 +542,88 @@ __global__ __launch_bounds__(64) void tridiag_invit_kernel(const double* __restr
             U2[at(i)] = 0.0;
             Lm[at(i)] = m;
             Pv[at(i)] = 0.0;
+            X[at(i)] = yc;
+            yc = yn - m * yc;
             cd = an - m * cu;
             cu = cn;
         }
     }
     U0i[at(n - 1)] = pivot_inv(cd);
-    for (int i = 0; i < n; ++i) X[at(i)] = unit_hash(((uint64_t)k << 32) ^ (uint64_t)i ^ 0x5EED5EEDull);
-    double sc = 1.0;
-    for (int it = 0; it < 3; ++it) {
-        // forward: y = L^-1 P x (in place)
-        double yc = X[at(0)] * sc;
-        for (int i = 0; i < n - 1; ++i) {
-            const double yn = X[at(i + 1)] * sc, m = Lm[at(i)];
-            if (Pv[at(i)] != 0.0) {
-                X[at(i)] = yn;
-                yc = yc - m * yn;
-            } else {
-                X[at(i)] = yc;
-                yc = yn - m * yc;
-            }
+    X[at(n - 1)] = yc;
+    // back substitution U z = y (z into X); returns max |z| (with norm2: the sum of squares too)
+    auto back = [&](double& norm2) {
+        double z1 = 0.0, z2 = 0.0, zmax = 0.0, nn = 0.0;
+        int i = n - 1;
+        while (i >= 0) {
+            const int c = i + 1 < 8 ? i + 1 : 8;  // steps i, i-1, .., i-c+1
+            double xv[8], u1[8], u2[8], ui[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (u < c) {
+                    xv[u] = X[at(i - u)];
+                    u1[u] = U1[at(i - u)];
+                    u2[u] = U2[at(i - u)];
+                    ui[u] = U0i[at(i - u)];
+                }
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (u < c) {
+                    const double z = (xv[u] - u1[u] * z1 - u2[u] * z2) * ui[u];
+                    X[at(i - u)] = z;
+                    zmax = fmax(zmax, fabs(z));
+                    nn += z * z;
+                    z2 = z1;
+                    z1 = z;
+                }
+            i -= c;
         }
-        X[at(n - 1)] = yc;
-        // back: U z = y (z into X), tracking max |z|
-        double z1 = 0.0, z2 = 0.0, zmax = 0.0;
-        for (int i = n - 1; i >= 0; --i) {
-            const double z = (X[at(i)] - U1[at(i)] * z1 - U2[at(i)] * z2) * U0i[at(i)];
-            X[at(i)] = z;
-            zmax = fmax(zmax, fabs(z));
-            z2 = z1;
-            z1 = z;
+        norm2 = nn;
+        return zmax;
+    };
+    double nn;
+    const double zmax = back(nn);
+    // pass 3: forward elimination of sc x (in place), sc = 1 / max |x|
+    const double sc = zmax > 0.0 ? 1.0 / zmax : 1.0;
+    {
+        double ycur = X[at(0)] * sc;
+        int i = 0;
+        while (i < n - 1) {
+            const int c = n - 1 - i < 8 ? n - 1 - i : 8;  // steps i .. i + c - 1
+            double xn[8], lm[8], pv[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (u < c) {
+                    xn[u] = X[at(i + u + 1)];
+                    lm[u] = Lm[at(i + u)];
+                    pv[u] = Pv[at(i + u)];
+                }
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (u < c) {
+                    const double yn = xn[u] * sc;
+                    if (pv[u] != 0.0) {
+                        X[at(i + u)] = yn;
+                        ycur = ycur - lm[u] * yn;
+                    } else {
+                        X[at(i + u)] = ycur;
+                        ycur = yn - lm[u] * ycur;
+                    }
+                }
+            i += c;
         }
-        sc = zmax > 0.0 ? 1.0 / zmax : 1.0;
+        X[at(n - 1)] = ycur;
     }
-    double nn = 0.0;
-    for (int i = 0; i < n; ++i) {
-        const double z = X[at(i)] * sc;
-        nn += z * z;
+    back(nn);
+    const double f = nn > 0.0 ? 1.0 / sqrt(nn) : 0.0;
+    for (int i = 0; i < n; i += 8) {
+        double xv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (i + u < n) xv[u] = X[at(i + u)];
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (i + u < n) Z[at(i + u)] = xv[u] * f;
     }
-    const double f = sc / sqrt(nn);
-    for (int i = 0; i < n; ++i) Z[at(i)] = X[at(i)] * f;
 }
 
 // Re-orthogonalise the vectors of eigenvalue clusters (neighbours within kClusterTol max|lam|):
@@ -524,37 +680,71 @@ __global__ __launch_bounds__(1024) void cluster_orth_kernel(const double* __rest
     }
 }
 
-constexpr int kWY = 32;  // reflectors per compact-WY block
+constexpr int kWY = 32;     // reflectors per compact-WY block
+constexpr int kWYRows = 128;  // Y rows staged in LDS per chunk
+
+// Y rows [r0, r0 + kWYRows) of the block's 32 reflector columns (column-major Y, ld) -> Ys[row][refl]
+// (pitch 33), zero past n / nref; 16 values per thread, consecutive threads along the rows.
+__device__ __forceinline__ void wy_stage(const double* __restrict__ Y, int ld, int n, int nref, int k0, int r0,
+                                         double (&v)[kWYRows * kWY / 256]) {
+#pragma unroll
+    for (int q = 0; q < kWYRows * kWY / 256; ++q) {
+        const int e = threadIdx.x + 256 * q, rr = e % kWYRows, c = e / kWYRows;
+        const int row = r0 + rr;
+        v[q] = (row < n && k0 + c < nref) ? Y[(int64_t)(k0 + c) * ld + row] : 0.0;
+    }
+}
+__device__ __forceinline__ void wy_put(double* Ys, const double (&v)[kWYRows * kWY / 256]) {
+#pragma unroll
+    for (int q = 0; q < kWYRows * kWY / 256; ++q) {
+        const int e = threadIdx.x + 256 * q, rr = e % kWYRows, c = e / kWYRows;
+        Ys[rr * (kWY + 1) + c] = v[q];
+    }
+}
 
 // T_b of block b (reflectors 32 b .. 32 b + 31; tau = 0 past the last one): the upper triangular
-// factor of H_{32b} ... H_{32b+31} = I - Y_b T_b Y_b^T (LAPACK dlarft, forward, columnwise).
+// factor of H_{32b} ... H_{32b+31} = I - Y_b T_b Y_b^T (LAPACK dlarft, forward, columnwise).  The
+// Gram Y_b^T Y_b over coalesced 128-row chunks staged in LDS.
 __global__ __launch_bounds__(256) void wy_t_kernel(const double* __restrict__ Y, int ld, int n, int nref,
                                                    const double* __restrict__ taus, double* __restrict__ Tg) {
+    __shared__ double Ys[kWYRows * (kWY + 1)];
     __shared__ double Sg[kWY][kWY + 1], T[kWY][kWY + 1];
     const int b = blockIdx.x, tid = threadIdx.x;
     const int k0 = kWY * b;
-    for (int e = tid; e < kWY * kWY; e += 256) {
-        const int p = e / kWY, q = e % kWY;
-        double sdot = 0.0;
-        if (p <= q && k0 + q < nref) {
-            const double* yp = Y + (int64_t)(k0 + p) * ld;
-            const double* yq = Y + (int64_t)(k0 + q) * ld;
-            for (int j = k0 + q + 1; j < n; ++j) sdot += yp[j] * yq[j];  // v_q is zero above q + 1
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    double v[kWYRows * kWY / 256];
+    for (int r0 = k0 + 1; r0 < n; r0 += kWYRows) {
+        wy_stage(Y, ld, n, nref, k0, r0, v);
+        __syncthreads();
+        wy_put(Ys, v);
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int e = tid + 256 * q, pp = e / kWY, qq = e % kWY;
+            if (pp <= qq) {
+                double a = 0.0;
+                for (int rr = 0; rr < kWYRows; ++rr) a += Ys[rr * (kWY + 1) + pp] * Ys[rr * (kWY + 1) + qq];
+                acc[q] += a;
+            }
         }
-        Sg[p][q] = sdot;
-        T[p][q] = 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int e = tid + 256 * q;
+        Sg[e / kWY][e % kWY] = acc[q];
+        T[e / kWY][e % kWY] = 0.0;
     }
     __syncthreads();
     if (tid == 0) T[0][0] = k0 < nref ? taus[k0] : 0.0;
     __syncthreads();
     for (int i = 1; i < kWY; ++i) {
         const double ti = k0 + i < nref ? taus[k0 + i] : 0.0;
-        double acc = 0.0;
+        double a = 0.0;
         if (tid < i) {
-            for (int q = tid; q < i; ++q) acc += T[tid][q] * Sg[q][i];
+            for (int q = tid; q < i; ++q) a += T[tid][q] * Sg[q][i];
         }
         __syncthreads();
-        if (tid < i) T[tid][i] = -ti * acc;
+        if (tid < i) T[tid][i] = -ti * a;
         if (tid == i) T[i][i] = ti;
         __syncthreads();
     }
@@ -562,16 +752,18 @@ __global__ __launch_bounds__(256) void wy_t_kernel(const double* __restrict__ Y,
 }
 
 // V = Q_H Z for one 16-column block of the row-major Z (ld ldz), held in LDS: blocks of 32
-// reflectors from the last to the first, Z <- Z - Y_b (T_b (Y_b^T Z)) on the fp64 MFMA; then V
-// into the column-major Vout (ld ldv; rows >= n written as zero).  256 threads.
+// reflectors from the last to the first, Z <- Z - Y_b (T_b (Y_b^T Z)) on the fp64 MFMA, Y_b staged
+// through LDS in coalesced 128-row chunks (the next chunk read into registers while the current one
+// is multiplied); then V into the column-major Vout (ld ldv; rows >= n written as zero).
 __global__ __launch_bounds__(256) void wy_apply_kernel(const double* __restrict__ Y, int ld, int n, int nref,
                                                        const double* __restrict__ Tg, const double* __restrict__ Z,
                                                        int ldz, double* __restrict__ Vout, int ldv) {
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    constexpr int ZP = 17, YP = kWY + 1;
     double* Zs = reinterpret_cast<double*>(smem_raw);  // [n][17]
+    __shared__ double Ys[kWYRows * YP];
     __shared__ double Ms[2][kWY][17];
     __shared__ double Ts[kWY][kWY + 1];
-    constexpr int ZP = 17;
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int r = lane & 15, h = lane >> 4;
     const int c0 = 16 * blockIdx.x;
@@ -580,38 +772,39 @@ __global__ __launch_bounds__(256) void wy_apply_kernel(const double* __restrict_
         Zs[i * ZP + c] = c0 + c < n ? Z[(int64_t)i * ldz + c0 + c] : 0.0;
     }
     const int nb = (nref + kWY - 1) / kWY;
+    double v[kWYRows * kWY / 256];
     for (int b = nb - 1; b >= 0; --b) {
         const int k0 = kWY * b;
         const int j0 = k0 + 1;  // first row any reflector of the block touches
         for (int e = tid; e < kWY * kWY; e += 256) Ts[e / kWY][e % kWY] = Tg[(int64_t)b * kWY * kWY + e];
-        __syncthreads();
-        // M = Y_b^T Z (32 x 16): wave w -> tile rows (w & 1), k (row) quarter... halves (w >> 1)
-        {
-            const int rt = w & 1, half = w >> 1;
-            const int len = n - j0;
-            const int q0 = j0 + ((len + 7) / 8 * 4) * half;  // 4-aligned split of [j0, n)
-            const int q1 = half ? n : min(n, q0 + (len + 7) / 8 * 4);
-            f64x4 acc = MD::zero();
-            const int col = k0 + 16 * rt + r;  // reflector of this lane's A row
-            const double* yc = Y + (int64_t)col * ld;
-            for (int j = q0; j < q1; j += 4) {
-                const int jj = j + h;
-                const double av = (jj < q1 && col < nref) ? yc[jj] : 0.0;
-                const double bv = jj < q1 ? Zs[jj * ZP + r] : 0.0;
+        // M = Y_b^T Z (32 x 16): per chunk, wave w -> reflector tile (w & 1), chunk rows half (w >> 1)
+        f64x4 acc = MD::zero();
+        const int rt = w & 1, half = w >> 1;
+        wy_stage(Y, ld, n, nref, k0, j0, v);
+        for (int r0 = j0; r0 < n; r0 += kWYRows) {
+            __syncthreads();
+            wy_put(Ys, v);
+            __syncthreads();
+            if (r0 + kWYRows < n) wy_stage(Y, ld, n, nref, k0, r0 + kWYRows, v);
+#pragma unroll 4
+            for (int j = 64 * half; j < 64 * half + 64; j += 4) {
+                const int row = r0 + j + h;
+                const double av = Ys[(j + h) * YP + 16 * rt + r];
+                const double bv = row < n ? Zs[row * ZP + r] : 0.0;
                 acc = MD::mma(av, bv, acc);
             }
-#pragma unroll
-            for (int q = 0; q < 4; ++q) Ms[half][16 * rt + MD::row(h, q)][r] = acc[q];
         }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) Ms[half][16 * rt + MD::row(h, q)][r] = acc[q];
         __syncthreads();
         // M2 = T_b M (upper triangular T), into Ms[0]
         double m2[2];
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
             const int e = tid + 256 * q, rr = e >> 4, cc = e & 15;
-            double acc = 0.0;
-            for (int p = rr; p < kWY; ++p) acc += Ts[rr][p] * (Ms[0][p][cc] + Ms[1][p][cc]);
-            m2[q] = acc;
+            double a = 0.0;
+            for (int p = rr; p < kWY; ++p) a += Ts[rr][p] * (Ms[0][p][cc] + Ms[1][p][cc]);
+            m2[q] = a;
         }
         __syncthreads();
 #pragma unroll
@@ -619,22 +812,24 @@ __global__ __launch_bounds__(256) void wy_apply_kernel(const double* __restrict_
             const int e = tid + 256 * q;
             Ms[0][e >> 4][e & 15] = m2[q];
         }
-        __syncthreads();
-        // Z -= Y_b M2: 16-row tiles of rows [j0, n), wave w -> tiles w, w + 4, ...
-        const int t0 = j0 & ~15;
-        for (int ti = t0 + 16 * w; ti < n; ti += 64) {
-            f64x4 acc = MD::zero();
-            const int row = ti + r;
+        // Z -= Y_b M2: per chunk, wave w -> 16-row tiles w, w + 4 of the 128 chunk rows
+        wy_stage(Y, ld, n, nref, k0, j0, v);
+        for (int r0 = j0; r0 < n; r0 += kWYRows) {
+            __syncthreads();
+            wy_put(Ys, v);
+            __syncthreads();
+            if (r0 + kWYRows < n) wy_stage(Y, ld, n, nref, k0, r0 + kWYRows, v);
 #pragma unroll
-            for (int s = 0; s < kWY / 4; ++s) {
-                const int kk = 4 * s + h;
-                const double av = (row < n && row >= j0 && k0 + kk < nref) ? Y[(int64_t)(k0 + kk) * ld + row] : 0.0;
-                acc = MD::mma(av, Ms[0][kk][r], acc);
-            }
+            for (int t = 0; t < 2; ++t) {
+                const int tr = 16 * (w + 4 * t);
+                f64x4 a = MD::zero();
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int rr = ti + MD::row(h, q);
-                if (rr < n) Zs[rr * ZP + r] -= acc[q];
+                for (int s = 0; s < kWY / 4; ++s) a = MD::mma(Ys[(tr + r) * YP + 4 * s + h], Ms[0][4 * s + h][r], a);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int row = r0 + tr + MD::row(h, q);
+                    if (row < n) Zs[row * ZP + r] -= a[q];
+                }
             }
         }
         __syncthreads();
@@ -645,12 +840,84 @@ __global__ __launch_bounds__(256) void wy_apply_kernel(const double* __restrict_
     }
 }
 
-template <int RT, int CT, int NW>
-hipError_t launch_tridiag(const double* G, int ld, int n, double* Y, double* d, double* e, double* taus, double* xch,
-                          unsigned* sync, int* info, hipStream_t s) {
-    return launch_coresident(tridiag_kernel<RT, CT, NW>, dim3(NW), dim3(kEigThreads), 0, s, G, ld, n, Y, d, e, taus,
-                             xch, sync, info);
+// C = alpha op(A) op(B) + beta C for the eigensolver's small fp64 products (column-major, M, N,
+// K <= a few hundred): one wave per 16 x 16 tile of C (1024 waves at 512^2 -- gemm.hip's 64 x 64
+// tiles gave 64 workgroups there and ran 55 / 100 us at 256^3 / 512^3).  Within a 16-deep k chunk
+// the MFMA k order is k0 + 4 h + s (step s, lane half h): the A and B operands only have to agree on
+// it, and then a transposed operand (op = T: contiguous along k) is read as 32-B runs per lane,
+// a plain one (contiguous along i / j) as 128-B rows per 16 lanes.
+template <int TA, int TB>
+__global__ __launch_bounds__(64) void sqgemm_f64_kernel(int M, int N, int K, double alpha, const double* __restrict__ A,
+                                                        int lda, const double* __restrict__ B, int ldb, double beta,
+                                                        double* __restrict__ C, int ldc) {
+    const int lane = threadIdx.x, r = lane & 15, h = lane >> 4;
+    const int tm = (M + 15) / 16;
+    const int bi = blockIdx.x % tm, bj = blockIdx.x / tm;
+    const int i = 16 * bi + r, j = 16 * bj + r;
+    const bool iv = i < M, jv = j < N;
+    auto ld_a = [&](int k) -> double {  // op(A)(i, k)
+        if (!iv || k >= K) return 0.0;
+        return TA ? A[(int64_t)i * lda + k] : A[(int64_t)k * lda + i];
+    };
+    auto ld_b = [&](int k) -> double {  // op(B)(k, j)
+        if (!jv || k >= K) return 0.0;
+        return TB ? B[(int64_t)k * ldb + j] : B[(int64_t)j * ldb + k];
+    };
+    f64x4 acc0 = MD::zero(), acc1 = MD::zero();
+    int k0 = 0;
+    for (; k0 + 32 <= K; k0 += 32) {
+        double a[8], b[8];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            a[s] = ld_a(k0 + 4 * h + s);
+            b[s] = ld_b(k0 + 4 * h + s);
+            a[4 + s] = ld_a(k0 + 16 + 4 * h + s);
+            b[4 + s] = ld_b(k0 + 16 + 4 * h + s);
+        }
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            acc0 = MD::mma(a[s], b[s], acc0);
+            acc1 = MD::mma(a[4 + s], b[4 + s], acc1);
+        }
+    }
+    for (; k0 < K; k0 += 16) {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) acc0 = MD::mma(ld_a(k0 + 4 * h + s), ld_b(k0 + 4 * h + s), acc0);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int ii = 16 * bi + MD::row(h, q);
+        if (ii < M && jv) {
+            double* c = C + (int64_t)j * ldc + ii;
+            const double v = alpha * (acc0[q] + acc1[q]);
+            *c = beta != 0.0 ? v + beta * *c : v;
+        }
+    }
 }
+
+hipError_t launch_sqgemm(int ta, int tb, int M, int N, int K, double alpha, const double* A, int lda, const double* B,
+                         int ldb, double beta, double* C, int ldc, hipStream_t s) {
+    const dim3 grid(((M + 15) / 16) * ((N + 15) / 16));
+#define SQG(X, Y)                                                                                                    \
+    if (ta == X && tb == Y) {                                                                                        \
+        hipLaunchKernelGGL((sqgemm_f64_kernel<X, Y>), grid, dim3(64), 0, s, M, N, K, alpha, A, lda, B, ldb, beta, C, \
+                           ldc);                                                                                     \
+        return hipGetLastError();                                                                                    \
+    }
+    SQG(0, 0) SQG(0, 1) SQG(1, 0) SQG(1, 1)
+#undef SQG
+    return hipErrorInvalidValue;
+}
+
+template <int RPL, int CPL, int LPR, int NW>
+hipError_t launch_tridiag(const double* src, int lds, int n, int off, int kend, double* Y, int ldy, double* d, double* e,
+                          double* taus, double* dump, double* xch, unsigned* sync, int* info, hipStream_t s) {
+    static_assert(8 * (64 / LPR) * RPL * NW <= kEigMaxN && LPR * CPL <= kEigMaxN, "tridiag layout");
+    return launch_coresident(tridiag_kernel<RPL, CPL, LPR, NW>, dim3(NW), dim3(kEigThreads), 0, s, src, lds, n, off,
+                             kend, Y, ldy, d, e, taus, dump, xch, sync, info);
+}
+
+constexpr int kTailRows = 192;  // phase 2 (one workgroup) takes the last kTailRows rows
 
 }  // namespace
 
@@ -680,22 +947,39 @@ hipError_t launch_eig_svd(const double* R, int l, int LP, double* ews, double* X
     const int n = l, nref = n - 2;
     hipError_t er;
     // 1. G = W^T W, W = the column-major view of R (ld LP)
-    if ((er = launch_gemm<double>(1, 0, n, n, n, 1.0, R, LP, R, LP, 0.0, G, LP, s)) != hipSuccess) return er;
+    if ((er = launch_sqgemm(1, 0, n, n, n, 1.0, R, LP, R, LP, 0.0, G, LP, s)) != hipSuccess) return er;
     // 2. tridiagonalisation
     if ((er = hipMemsetAsync(Y, 0, L2 * sizeof(double), s)) != hipSuccess) return er;
     if ((er = hipMemsetAsync(taus, 0, LP * sizeof(double), s)) != hipSuccess) return er;
     if ((er = hipMemsetAsync(sync + kTriCtr, 0, 2 * sizeof(unsigned), s)) != hipSuccess) return er;
-    if (LP <= 128)
-        er = launch_tridiag<16, 2, 1>(G, LP, n, Y, d, e, taus, xch, sync, info, s);
-    else if (LP <= 256)
-        er = launch_tridiag<8, 4, 4>(G, LP, n, Y, d, e, taus, xch, sync, info, s);
-    else
-        er = launch_tridiag<4, 8, 16>(G, LP, n, Y, d, e, taus, xch, sync, info, s);
+    if (n <= 128) {
+        er = launch_tridiag<2, 16, 8, 1>(G, LP, n, 0, n - 2, Y, LP, d, e, taus, nullptr, xch, sync, info, s);
+    } else if (n <= kTailRows) {
+        er = launch_tridiag<3, 24, 8, 1>(G, LP, n, 0, n - 2, Y, LP, d, e, taus, nullptr, xch, sync, info, s);
+    } else {
+        // phase 1 on NW workgroups up to the step that leaves kTailRows trailing rows, phase 2 on one
+        double* dump = scr;  // free until the inverse iteration
+        const int kend = n - kTailRows - 1;
+        if (n <= 256)
+            er = launch_tridiag<2, 16, 16, 4>(G, LP, n, 0, kend, Y, LP, d, e, taus, dump, xch, sync, info, s);
+        else
+            er = launch_tridiag<2, 16, 32, 16>(G, LP, n, 0, kend, Y, LP, d, e, taus, dump, xch, sync, info, s);
+        if (er != hipSuccess) return er;
+        er = launch_tridiag<3, 24, 8, 1>(dump, LP, n, kend + 1, n - 2, Y, LP, d, e, taus, nullptr, xch, sync, info, s);
+    }
     if (er != hipSuccess) return er;
     // 3. eigenvalues (descending), 4. eigenvectors of T (row-major Z), cluster re-orthogonalisation
     hipLaunchKernelGGL(tridiag_bisect_kernel, dim3((n + 3) / 4), dim3(256), 0, s, d, e, n, lam, tnorm);
     hipLaunchKernelGGL(tridiag_invit_kernel, dim3((n + 63) / 64), dim3(64), 0, s, d, e, lam, tnorm, n, LP, Z, scr);
     hipLaunchKernelGGL(cluster_orth_kernel, dim3(1), dim3(1024), 0, s, lam, n, LP, Z);
+    // one Newton-Schulz step: Z' = Z (3 I - Z^T Z) / 2.  Row-major Z read column-major (ld LP) is
+    // Zc = Z^T, so M = Z^T Z = Zc Zc^T and Zc' = 1.5 Zc - 0.5 M Zc (M symmetric); Zc' into Z2 (scratch)
+    double* M = scr;
+    double* Z2 = scr + L2;
+    if ((er = launch_sqgemm(0, 1, n, n, n, 1.0, Z, LP, Z, LP, 0.0, M, LP, s)) != hipSuccess) return er;
+    if ((er = hipMemcpyAsync(Z2, Z, L2 * sizeof(double), hipMemcpyDeviceToDevice, s)) != hipSuccess) return er;
+    if ((er = launch_sqgemm(0, 0, n, n, n, -0.5, M, LP, Z, LP, 1.5, Z2, LP, s)) != hipSuccess) return er;
+    Z = Z2;
     // 5. V_w = Q_H Z into J (buffer 0, column-major LP x LP; columns >= n zero)
     if ((er = hipMemsetAsync(J, 0, L2 * sizeof(double), s)) != hipSuccess) return er;
     if (nref > 0) hipLaunchKernelGGL(wy_t_kernel, dim3((nref + kWY - 1) / kWY), dim3(256), 0, s, Y, LP, n, nref, taus, Tg);
@@ -704,7 +988,7 @@ hipError_t launch_eig_svd(const double* R, int l, int LP, double* ews, double* X
     if ((er = hipGetLastError()) != hipSuccess) return er;
     // 6. X = W V_w into X (buffer 0, column-major), then the checked block-Jacobi finish
     if ((er = hipMemsetAsync(X, 0, L2 * sizeof(double), s)) != hipSuccess) return er;
-    if ((er = launch_gemm<double>(0, 0, n, n, n, 1.0, R, LP, J, LP, 0.0, X, LP, s)) != hipSuccess) return er;
+    if ((er = launch_sqgemm(0, 0, n, n, n, 1.0, R, LP, J, LP, 0.0, X, LP, s)) != hipSuccess) return er;
     return launch_block_jacobi_given<T>(l, LP, X, J, Uw, Vw, S, sync, info, s, tol_chk);
 }
 

@@ -4,13 +4,14 @@ W (l x l) -> G = W^T W -> Householder tridiagonalisation (tridiag_kernel's per-c
 p = tau G v, K = tau/2 v.p, w = p - K v, G -= v w^T + w v^T) -> eigenvalues by Sturm-count
 multisection on the scaled T with the three-term recurrence and power-of-two rescaling every 8
 steps (tridiag_bisect_kernel) -> inverse iteration with partial pivoting, three solves
-(tridiag_invit_kernel) -> CGS2 inside clusters (cluster_orth_kernel) -> V = Q_H Z -> X = W V.
+(tridiag_invit_kernel) -> CGS2 inside tight clusters (cluster_orth_kernel) -> one Newton-Schulz step
+Z (3 I - Z^T Z) / 2 -> V = Q_H Z -> X = W V.
 Used by tests/test_eig_model.py (CPU) and to size the design.
 """
 import numpy as np
 
 EPS = np.finfo(float).eps
-CLUSTER_TOL = 1e-9
+CLUSTER_TOL = 1e-12
 
 
 def tridiag(G):
@@ -87,7 +88,7 @@ def eigvals_desc(d, e):
     return lam, nrm
 
 
-def invit(d, e, lam, tnorm, seed=0x5EED5EED):
+def invit(d, e, lam, tnorm, seed=0x5EED5EED, solves=2):
     n = len(d)
     tol = EPS * max(tnorm, 1e-300)
     Z = np.zeros((n, n))
@@ -109,7 +110,7 @@ def invit(d, e, lam, tnorm, seed=0x5EED5EED):
         small = np.abs(U0) < tol
         U0[small] = np.where(U0[small] < 0.0, -tol, tol)
         x = rng.uniform(-1.0, 1.0, n)
-        for _ in range(3):
+        for _ in range(solves):
             y = x.copy()
             for i in range(n - 1):
                 if P[i]:
@@ -139,13 +140,18 @@ def cluster_cgs2(Z, lam):
     return Z
 
 
+def newton_schulz(Z):
+    """One step Z (3 I - Z^T Z) / 2: squares the non-orthogonality of nearly orthonormal columns."""
+    return 1.5 * Z - 0.5 * Z @ (Z.T @ Z)
+
+
 def small_svd(W):
     """X = W V_w (columns orthogonal), V_w orthogonal, lambda (descending) -- what the GPU hands to
     the block Jacobi's check and finish."""
     G = W.T @ W
     d, e, Y, taus = tridiag(G)
     lam, tn = eigvals_desc(d, e)
-    Z = cluster_cgs2(invit(d, e, lam, tn), lam)
+    Z = newton_schulz(cluster_cgs2(invit(d, e, lam, tn), lam))
     V = Z.copy()
     for k in range(len(d) - 3, -1, -1):
         V -= taus[k] * np.outer(Y[:, k], Y[:, k] @ V)
