@@ -107,12 +107,36 @@ __device__ bool tri_barrier(unsigned* sync, unsigned target) {
     return ok != 0;
 }
 
-// Sum over the LPR lanes of a lane group (lanes g LPR .. g LPR + LPR - 1), every lane gets the total.
+// Cross-lane fp64 sums on DPP (two v_mov_dpp per step, no LDS round trip -- a __shfl_xor is a
+// ds_bpermute pair, ~100 cycles of latency per step, and a 6-step wave sum of those sat on the
+// tridiagonalisation's critical path three times per column).
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+    const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xf, 0xf, true);
+    const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xf, 0xf, true);
+    return __hiloint2double(hi, lo);
+}
+constexpr int kDppXor1 = 0xB1, kDppXor2 = 0x4E, kDppHalfMirror = 0x141, kDppMirror = 0x140;
+__device__ __forceinline__ double readlane_f64(double v, int lane) {
+    const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
+    const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
+    return __hiloint2double(hi, lo);
+}
+// Sum over the LPR lanes of an aligned lane group (LPR in {8, 16, 32}); every lane of the group gets
+// the same total (each step adds two partial sums: commutative, so all lanes agree bit for bit).
 template <int LPR>
 __device__ __forceinline__ double group_sum(double v) {
-#pragma unroll
-    for (int o = LPR / 2; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    v += dpp_f64<kDppXor1>(v);
+    v += dpp_f64<kDppXor2>(v);
+    v += dpp_f64<kDppHalfMirror>(v);
+    if constexpr (LPR >= 16) v += dpp_f64<kDppMirror>(v);
+    if constexpr (LPR >= 32) v += __shfl_xor(v, 16, 64);
     return v;
+}
+// Sum over the whole wave, wave-uniform (the four 16-lane row totals read back in a fixed order).
+__device__ __forceinline__ double wave_total(double v) {
+    v = group_sum<16>(v);
+    return (readlane_f64(v, 0) + readlane_f64(v, 16)) + (readlane_f64(v, 32) + readlane_f64(v, 48));
 }
 
 // Householder tridiagonalisation of the symmetric G (LAPACK dsytd2's reflectors, v_k[k+1] = 1), in
@@ -240,9 +264,8 @@ __global__ __launch_bounds__(kEigThreads) void tridiag_kernel(const double* __re
                 else st_wt(xp + wg * RPW + (li - wg) / NW, p);
             }
         }
-        // wave partial of v.p over the group leaders (fixed butterfly: identical on every member)
-        pv = c == 0 ? pv : 0.0;
-        pv = warp_sum(pv);
+        // wave partial of v.p over the group leaders (fixed order: identical on every member)
+        pv = wave_total(c == 0 ? pv : 0.0);
         if (lane == 0) {
             if constexpr (NW == 1) vpw[w] = pv;
             else st_wt(xp + NW * RPW + wg * 8 + w, pv);
@@ -279,8 +302,9 @@ __global__ __launch_bounds__(kEigThreads) void tridiag_kernel(const double* __re
         }
         __syncthreads();
         // [C] K, w, the pivot row of A_{k+1}, |row[k+3 ..]|^2
-        double kk = lane < 8 * NW ? vpw[lane] : 0.0;
-        kk = warp_sum(kk);
+        double kk = 0.0;
+#pragma unroll
+        for (int q = 0; q < 8 * NW; ++q) kk += vpw[q];  // same order on every thread and member
         const double K = 0.5 * tau * kk;
         const double wk1 = ps[l1] - K * vc[l1];
         double xq = 0.0;
@@ -293,7 +317,7 @@ __global__ __launch_bounds__(kEigThreads) void tridiag_kernel(const double* __re
                 if (j > l1 + 1) xq += rj * rj;
             }
         }
-        xq = warp_sum(xq);
+        xq = wave_total(xq);
         if (lane == 0) red[w] = xq;
         __syncthreads();
         // [E] the next reflector
