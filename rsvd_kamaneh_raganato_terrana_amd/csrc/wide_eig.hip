@@ -107,6 +107,46 @@ __device__ bool tri_barrier(unsigned* sync, unsigned target) {
     return ok != 0;
 }
 
+// fp64 reciprocal / reciprocal square root from the hardware estimates (two Newton steps each)
+__device__ __forceinline__ double rcp_f64(double d) {
+    double y = __builtin_amdgcn_rcp(d);
+    y = y * fma(-d, y, 2.0);
+    return y * fma(-d, y, 2.0);
+}
+__device__ __forceinline__ double rsqrt_f64(double d) {
+    double y = __builtin_amdgcn_rsq(d);
+    y = y * fma(-0.5 * d * y, y, 1.5);
+    return y * fma(-0.5 * d * y, y, 1.5);
+}
+
+// RSVD_TRI_PROF (lab builds only): shader-cycle totals of the step phases of tridiag_kernel,
+// workgroup 0 thread 0, read back by tri_prof_read (tools/eig_lab.cpp)
+#ifdef RSVD_TRI_PROF
+__device__ long long g_tri_prof[8];
+#define TRI_INIT() long long tri_last_ = __builtin_amdgcn_s_memtime()
+#define TRI_TS(i)                                                        \
+    do {                                                                 \
+        if (blockIdx.x == 0 && threadIdx.x == 0) {                       \
+            const long long now_ = __builtin_amdgcn_s_memtime();         \
+            g_tri_prof[(i)] += now_ - tri_last_;                         \
+            tri_last_ = now_;                                            \
+        }                                                                \
+    } while (0)
+#define TRI_DONE() \
+    do {           \
+    } while (0)
+#else
+#define TRI_INIT() \
+    do {           \
+    } while (0)
+#define TRI_TS(i) \
+    do {          \
+    } while (0)
+#define TRI_DONE() \
+    do {           \
+    } while (0)
+#endif
+
 // Cross-lane fp64 sums on DPP (two v_mov_dpp per step, no LDS round trip -- a __shfl_xor is a
 // ds_bpermute pair, ~100 cycles of latency per step, and a 6-step wave sum of those sat on the
 // tridiagonalisation's critical path three times per column).
@@ -169,7 +209,7 @@ __global__ __launch_bounds__(kEigThreads) void tridiag_kernel(const double* __re
     constexpr int RPW = 8 * G * RPL;                     // rows per member
     constexpr int XS = NW * RPW + 8 * NW + kEigMaxN;     // one parity's exchange slots: p, v.p partials, row
     __shared__ double vb[2][kEigMaxN];
-    __shared__ double ps[kEigMaxN], ws[kEigMaxN], rs[kEigMaxN];
+    __shared__ double ps[kEigMaxN], ws[kEigMaxN], rs[kEigMaxN], rb[kEigMaxN];
     __shared__ double vpw[8 * NW];
     __shared__ double red[8];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -246,19 +286,25 @@ __global__ __launch_bounds__(kEigThreads) void tridiag_kernel(const double* __re
         s[q] = acc;
     }
     int cur = 0;
+    double scal = 0.0;  // v_k = scal * rb past its leading 1 (rb: row k of A_k, from the previous step)
+    TRI_INIT();
     for (int k = kbeg; k < kend; ++k) {
-        const double* vc = vb[cur];
+        double* vc = vb[cur];
         double* vn = vb[cur ^ 1];
         const int l1 = k + 1 - off;  // local index of the pivot row k + 1
         double* xp = xch + (int64_t)((k - kbeg) & 1) * XS;
-        // [A] p, the v.p partials and the pivot row
+        // [A] p, the v.p partials and the pivot row.  v_k[li] of other threads' rows: from LDS in the
+        // first step, afterwards re-formed from rb (the previous pivot row) -- its vb copy is written
+        // without a barrier before this point
         double pv = 0.0;
 #pragma unroll
         for (int q = 0; q < RPL; ++q) {
             const double tot = group_sum<LPR>(s[q]);
             const int li = lrow(q);
             const double p = (li < t && li > l1 - 1) ? tau * tot : 0.0;  // rows > k
-            pv += vc[li < kEigMaxN ? li : 0] * p;
+            const double vli = k == kbeg ? vc[li < kEigMaxN ? li : 0]
+                                         : (li == l1 ? 1.0 : ((li > l1 && li < t) ? rb[li] * scal : 0.0));
+            pv += vli * p;
             if (c == 0 && li < t) {
                 if constexpr (NW == 1) ps[li] = p;
                 else st_wt(xp + wg * RPW + (li - wg) / NW, p);
@@ -288,74 +334,95 @@ __global__ __launch_bounds__(kEigThreads) void tridiag_kernel(const double* __re
                     }
             }
         }
-        // [B] the hand-off
+        TRI_TS(0);
+        // [B] the hand-off; thread j takes p_j and the pivot row's entry j
+        double pj = 0.0, rj = 0.0, pl1, kk = 0.0;
+        const int j = tid;  // t <= 512 = kEigThreads
         if constexpr (NW > 1) {
             if (!tri_barrier(sync, (unsigned)NW * (unsigned)(k - kbeg + 1))) {
                 if (tid == 0) info[2] = 1;
                 return;
             }
-            for (int j = tid; j < t; j += kEigThreads) {
-                ps[j] = ld_wt(xp + (j % NW) * RPW + j / NW);
-                rs[j] = ld_wt(xp + NW * RPW + 8 * NW + j);
+            if (j < t) {
+                pj = ld_wt(xp + (j % NW) * RPW + j / NW);
+                rj = ld_wt(xp + NW * RPW + 8 * NW + j);
             }
-            if (tid < 8 * NW) vpw[tid] = ld_wt(xp + NW * RPW + tid);
-        }
-        __syncthreads();
-        // [C] K, w, the pivot row of A_{k+1}, |row[k+3 ..]|^2
-        double kk = 0.0;
+            pl1 = ld_wt(xp + (l1 % NW) * RPW + l1 / NW);
 #pragma unroll
-        for (int q = 0; q < 8 * NW; ++q) kk += vpw[q];  // same order on every thread and member
-        const double K = 0.5 * tau * kk;
-        const double wk1 = ps[l1] - K * vc[l1];
-        double xq = 0.0;
-        for (int j = tid; j < kEigMaxN; j += kEigThreads) {
-            const double wj = j < t ? ps[j] - K * vc[j] : 0.0;
-            ws[j] = wj;
-            if (j >= l1 && j < t) {
-                const double rj = rs[j] - wj - wk1 * vc[j];
-                rs[j] = rj;
-                if (j > l1 + 1) xq += rj * rj;
+            for (int q = 0; q < 8 * NW; q += 64) kk += lane + q < 8 * NW ? ld_wt(xp + NW * RPW + lane + q) : 0.0;
+            kk = wave_total(kk);  // the same order in every wave and member
+        } else {
+            __syncthreads();
+            if (j < t) {
+                pj = ps[j];
+                rj = rs[j];
             }
+            pl1 = ps[l1];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) kk += vpw[q];
+        }
+        TRI_TS(1);
+        // [C] K, w, the pivot row of A_{k+1} (into rb), |row[k+3 ..]|^2
+        const double K = 0.5 * tau * kk;
+        const double wk1 = pl1 - K;  // v_k[k+1] = 1
+        double xq = 0.0;
+        if (j < kEigMaxN) {
+            const double wjv = j < t ? pj - K * vc[j] : 0.0;
+            ws[j] = wjv;
+            double rn = 0.0;
+            if (j >= l1 && j < t) {
+                rn = rj - wjv - wk1 * vc[j];
+                if (j > l1 + 1) xq = rn * rn;
+            }
+            rb[j] = rn;
         }
         xq = wave_total(xq);
         if (lane == 0) red[w] = xq;
         __syncthreads();
-        // [E] the next reflector
+        TRI_TS(2);
+        // [E] the next reflector (every thread; v_{k+1} is formed where it is used)
         double taun = 0.0;
-        if (k + 1 <= n - 3) {
+        const bool more = k + 1 <= n - 3;
+        {
             double xn2 = 0.0;
 #pragma unroll
             for (int q = 0; q < 8; ++q) xn2 += red[q];
-            const double a0 = rs[l1 + 1];
-            double beta = a0, scal = 0.0;
-            if (xn2 != 0.0) {
-                const double nr = sqrt(a0 * a0 + xn2);
+            const double a0 = rb[l1 + 1];
+            double beta = a0;
+            scal = 0.0;
+            if (more && xn2 != 0.0) {
+                const double x2 = a0 * a0 + xn2;
+                const double nr = x2 * rsqrt_f64(x2);
                 beta = a0 >= 0.0 ? -nr : nr;
-                taun = (beta - a0) / beta;
-                scal = 1.0 / (a0 - beta);
-            }
-            for (int j = tid; j < kEigMaxN; j += kEigThreads) {
-                const double v = (j == l1 + 1) ? 1.0 : ((j > l1 + 1 && j < t) ? rs[j] * scal : 0.0);
-                vn[j] = v;
-                if (wg == 0 && j < t) Y[(int64_t)(k + 1) * ldy + off + j] = v;
+                taun = (beta - a0) * rcp_f64(beta);
+                scal = rcp_f64(a0 - beta);
             }
             if (wg == 0 && tid == 0) {
-                dvec[k + 1] = rs[l1];
-                evec[k + 1] = beta;
-                taus[k + 1] = taun;
-            }
-        } else {
-            for (int j = tid; j < kEigMaxN; j += kEigThreads) vn[j] = 0.0;
-            if (wg == 0 && tid == 0) {
-                dvec[n - 2] = rs[l1];
-                evec[n - 2] = rs[l1 + 1];
+                if (more) {
+                    dvec[k + 1] = rb[l1];
+                    evec[k + 1] = beta;
+                    taus[k + 1] = taun;
+                } else {
+                    dvec[n - 2] = rb[l1];
+                    evec[n - 2] = rb[l1 + 1];
+                }
             }
         }
-        __syncthreads();
-        // [D] A_{k+1} = A_k - v w^T - w v^T on the registers, and the next partial products; columns
-        // in groups of 4 with a compiler memory barrier between groups, so the LDS reads of v, w, v'
-        // are not all hoisted ahead (that kept 3 CPL extra doubles live and spilled)
+        auto vnext = [&](int jj) -> double {  // v_{k+1}[jj]
+            if (!more) return 0.0;
+            return jj == l1 + 1 ? 1.0 : ((jj > l1 + 1 && jj < t) ? rb[jj] * scal : 0.0);
+        };
+        if (j < kEigMaxN) {
+            const double v = vnext(j);
+            vn[j] = v;  // own entry: read back by this thread only until the next barrier
+            if (more && wg == 0 && j < t) Y[(int64_t)(k + 1) * ldy + off + j] = v;
+        }
+        // [D] A_{k+1} = A_k - v w^T - w v^T on the registers, and the next partial products; column
+        // groups of 4 whose columns are all <= k + 1 (dead from here on) are skipped, as are row slots
+        // whose rows on this wave are all dead; a compiler memory barrier between column groups keeps
+        // their LDS reads from being hoisted together (that kept 3 CPL extra doubles live and spilled)
         double vi[RPL], wi[RPL];
+        bool live[RPL];
 #pragma unroll
         for (int q = 0; q < RPL; ++q) {
             const int li = lrow(q);
@@ -363,17 +430,26 @@ __global__ __launch_bounds__(kEigThreads) void tridiag_kernel(const double* __re
             vi[q] = li < t ? vc[lc] : 0.0;
             wi[q] = li < t ? ws[lc] : 0.0;
             s[q] = 0.0;
+            // the wave's last row of slot q: (q 8G + w G + G - 1) NW + NW - 1
+            live[q] = ((q * 8 * G + w * G + G - 1) * NW + NW - 1) > l1;
         }
 #pragma unroll
         for (int u0 = 0; u0 < CPL; u0 += 4) {
+            constexpr int dummy = 0;
+            (void)dummy;
+            const int u1 = u0 + 4 < CPL ? u0 + 4 : CPL;
+            if (LPR * (u1 - 1) + LPR - 1 > l1) {
 #pragma unroll
-            for (int u = u0; u < (u0 + 4 < CPL ? u0 + 4 : CPL); ++u) {
-                const int j = c + LPR * u;
-                const double wj = ws[j], vj = vc[j], vnj = vn[j];
+                for (int u = u0; u < u1; ++u) {
+                    const int jj = c + LPR * u;
+                    const double wj = ws[jj], vj = vc[jj], vnj = vnext(jj);
 #pragma unroll
-                for (int q = 0; q < RPL; ++q) {
-                    a[q][u] -= vi[q] * wj + wi[q] * vj;
-                    s[q] += a[q][u] * vnj;
+                    for (int q = 0; q < RPL; ++q) {
+                        if (live[q]) {
+                            a[q][u] -= vi[q] * wj + wi[q] * vj;
+                            s[q] += a[q][u] * vnj;
+                        }
+                    }
                 }
             }
             asm volatile("" ::: "memory");
@@ -387,9 +463,11 @@ __global__ __launch_bounds__(kEigThreads) void tridiag_kernel(const double* __re
                         if (c + LPR * u == t - 1) dvec[n - 1] = a[q][u];
                 }
         }
+        TRI_TS(3);
         tau = taun;
         cur ^= 1;
     }
+    TRI_DONE();
     if (kend < n - 2) {  // phase 1 ends: the trailing block of A_kend (rows / columns >= kend + 1)
         const int o2 = kend + 1 - off;
 #pragma unroll
@@ -521,8 +599,10 @@ __device__ __forceinline__ double unit_hash(uint64_t x) {
 // pseudo-random start -- the first forward elimination fused into the factorisation, the second
 // solve rescaled by the first's largest entry -- and writes the unit vector to row-major Z
 // (Z[i][k], ld ldz).  Scratch: six n x ldz arrays laid out [i][k] (a wave's 64 vectors read and
-// write 512 contiguous bytes per step).  The serial chains never wait on memory: each loop reads
-// the operands of its next 8 steps into registers while the current 8 run.
+// write 512 contiguous bytes per step).  Stores and loads share vmcnt, so a load issued after a
+// store waits for it: the solve loops read the operands of the NEXT 8 steps before storing the
+// current 8, and the factorisation's multipliers come from a Newton reciprocal, not a division.
+
 __global__ __launch_bounds__(64) void tridiag_invit_kernel(const double* __restrict__ dg, const double* __restrict__ eg,
                                                            const double* __restrict__ lam, const double* __restrict__ tnorm,
                                                            int n, int ldz, double* __restrict__ Z,
@@ -548,58 +628,63 @@ __global__ __launch_bounds__(64) void tridiag_invit_kernel(const double* __restr
     double cd = dg[0] - lk, cu = n > 1 ? eg[0] : 0.0, yc = rnd(0);
     for (int i = 0; i < n - 1; ++i) {
         const double bi = eg[i], an = dg[i + 1] - lk, cn = i + 1 < n - 1 ? eg[i + 1] : 0.0, yn = rnd(i + 1);
-        if (fabs(bi) > fabs(cd)) {
-            const double m = cd / bi;
-            U0i[at(i)] = pivot_inv(bi);
-            U1[at(i)] = an;
-            U2[at(i)] = cn;
-            Lm[at(i)] = m;
-            Pv[at(i)] = 1.0;
-            X[at(i)] = yn;
-            yc = yc - m * yn;
-            cd = cu - m * an;
-            cu = -m * cn;
-        } else {
-            const double m = cd != 0.0 ? bi / cd : 0.0;
-            U0i[at(i)] = pivot_inv(cd);
-            U1[at(i)] = cu;
-            U2[at(i)] = 0.0;
-            Lm[at(i)] = m;
-            Pv[at(i)] = 0.0;
-            X[at(i)] = yc;
-            yc = yn - m * yc;
-            cd = an - m * cu;
-            cu = cn;
-        }
+        const bool piv = fabs(bi) > fabs(cd);
+        const double m = piv ? cd * rcp_f64(bi) : (cd != 0.0 ? bi * rcp_f64(cd) : 0.0);
+        U0i[at(i)] = pivot_inv(piv ? bi : cd);
+        U1[at(i)] = piv ? an : cu;
+        U2[at(i)] = piv ? cn : 0.0;
+        Lm[at(i)] = m;
+        Pv[at(i)] = piv ? 1.0 : 0.0;
+        X[at(i)] = piv ? yn : yc;
+        const double ycn = piv ? yc - m * yn : yn - m * yc;
+        const double cdn = piv ? cu - m * an : an - m * cu;
+        cu = piv ? -m * cn : cn;
+        cd = cdn;
+        yc = ycn;
     }
     U0i[at(n - 1)] = pivot_inv(cd);
     X[at(n - 1)] = yc;
-    // back substitution U z = y (z into X); returns max |z| (with norm2: the sum of squares too)
+    // back substitution U z = y (z into X): max |z| and sum z^2
     auto back = [&](double& norm2) {
         double z1 = 0.0, z2 = 0.0, zmax = 0.0, nn = 0.0;
-        int i = n - 1;
-        while (i >= 0) {
-            const int c = i + 1 < 8 ? i + 1 : 8;  // steps i, i-1, .., i-c+1
-            double xv[8], u1[8], u2[8], ui[8];
+        double xa[8], ua[8], va[8], ia[8], xb[8], ub[8], vb2[8], ib[8];
+        auto load = [&](int i0, double (&x)[8], double (&u1)[8], double (&u2)[8], double (&ui)[8]) {
 #pragma unroll
-            for (int u = 0; u < 8; ++u)
-                if (u < c) {
-                    xv[u] = X[at(i - u)];
-                    u1[u] = U1[at(i - u)];
-                    u2[u] = U2[at(i - u)];
-                    ui[u] = U0i[at(i - u)];
+            for (int u = 0; u < 8; ++u) {
+                const int i = i0 - u;
+                if (i >= 0) {
+                    x[u] = X[at(i)];
+                    u1[u] = U1[at(i)];
+                    u2[u] = U2[at(i)];
+                    ui[u] = U0i[at(i)];
                 }
+            }
+        };
+        load(n - 1, xa, ua, va, ia);
+        for (int i0 = n - 1; i0 >= 0; i0 -= 16) {
+            if (i0 - 8 >= 0) load(i0 - 8, xb, ub, vb2, ib);
 #pragma unroll
             for (int u = 0; u < 8; ++u)
-                if (u < c) {
-                    const double z = (xv[u] - u1[u] * z1 - u2[u] * z2) * ui[u];
-                    X[at(i - u)] = z;
+                if (i0 - u >= 0) {
+                    const double z = (xa[u] - ua[u] * z1 - va[u] * z2) * ia[u];
+                    X[at(i0 - u)] = z;
                     zmax = fmax(zmax, fabs(z));
                     nn += z * z;
                     z2 = z1;
                     z1 = z;
                 }
-            i -= c;
+            if (i0 - 8 < 0) break;
+            if (i0 - 16 >= 0) load(i0 - 16, xa, ua, va, ia);
+#pragma unroll
+            for (int u = 0; u < 8; ++u)
+                if (i0 - 8 - u >= 0) {
+                    const double z = (xb[u] - ub[u] * z1 - vb2[u] * z2) * ib[u];
+                    X[at(i0 - 8 - u)] = z;
+                    zmax = fmax(zmax, fabs(z));
+                    nn += z * z;
+                    z2 = z1;
+                    z1 = z;
+                }
         }
         norm2 = nn;
         return zmax;
@@ -610,30 +695,39 @@ __global__ __launch_bounds__(64) void tridiag_invit_kernel(const double* __restr
     const double sc = zmax > 0.0 ? 1.0 / zmax : 1.0;
     {
         double ycur = X[at(0)] * sc;
-        int i = 0;
-        while (i < n - 1) {
-            const int c = n - 1 - i < 8 ? n - 1 - i : 8;  // steps i .. i + c - 1
-            double xn[8], lm[8], pv[8];
+        double xa[8], la[8], pa[8], xb[8], lb[8], pb[8];
+        auto load = [&](int i0, double (&x)[8], double (&l)[8], double (&pv)[8]) {
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int i = i0 + u;
+                if (i < n - 1) {
+                    x[u] = X[at(i + 1)];
+                    l[u] = Lm[at(i)];
+                    pv[u] = Pv[at(i)];
+                }
+            }
+        };
+        auto step = [&](int i, double xn, double lmv, double pvv) {
+            const double yn = xn * sc;
+            if (pvv != 0.0) {
+                X[at(i)] = yn;
+                ycur = ycur - lmv * yn;
+            } else {
+                X[at(i)] = ycur;
+                ycur = yn - lmv * ycur;
+            }
+        };
+        load(0, xa, la, pa);
+        for (int i0 = 0; i0 < n - 1; i0 += 16) {
+            if (i0 + 8 < n - 1) load(i0 + 8, xb, lb, pb);
 #pragma unroll
             for (int u = 0; u < 8; ++u)
-                if (u < c) {
-                    xn[u] = X[at(i + u + 1)];
-                    lm[u] = Lm[at(i + u)];
-                    pv[u] = Pv[at(i + u)];
-                }
+                if (i0 + u < n - 1) step(i0 + u, xa[u], la[u], pa[u]);
+            if (i0 + 8 >= n - 1) break;
+            if (i0 + 16 < n - 1) load(i0 + 16, xa, la, pa);
 #pragma unroll
             for (int u = 0; u < 8; ++u)
-                if (u < c) {
-                    const double yn = xn[u] * sc;
-                    if (pv[u] != 0.0) {
-                        X[at(i + u)] = yn;
-                        ycur = ycur - lm[u] * yn;
-                    } else {
-                        X[at(i + u)] = ycur;
-                        ycur = yn - lm[u] * ycur;
-                    }
-                }
-            i += c;
+                if (i0 + 8 + u < n - 1) step(i0 + 8 + u, xb[u], lb[u], pb[u]);
         }
         X[at(n - 1)] = ycur;
     }
@@ -944,6 +1038,14 @@ hipError_t launch_tridiag(const double* src, int lds, int n, int off, int kend, 
 constexpr int kTailRows = 192;  // phase 2 (one workgroup) takes the last kTailRows rows
 
 }  // namespace
+
+#ifdef RSVD_TRI_PROF
+void tri_prof_read(long long* out) {
+    (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tri_prof), sizeof(long long) * 8);
+    long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_tri_prof), z, sizeof(z));
+}
+#endif
 
 size_t eig_svd_ws_doubles(int LP) {
     const size_t L2 = (size_t)LP * LP;
