@@ -210,9 +210,11 @@ __global__ __launch_bounds__(kEigThreads) void tridiag_kernel(const double* __re
     constexpr int XS = NW * RPW + 8 * NW + kEigMaxN;     // one parity's exchange slots: p, v.p partials, row
     __shared__ double vb[2][kEigMaxN];
     __shared__ double ps[kEigMaxN], ws[kEigMaxN], rs[kEigMaxN], rb[kEigMaxN];
+    __shared__ double rv[kEigMaxN];  // rb past index k + 2 (else 0): v_{k+1} = scal rv + e_{k+2}
     __shared__ double vpw[8 * NW];
     __shared__ double red[8];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform: the row-slot tests stay scalar
     const int g = lane / LPR, c = lane % LPR;
     const int wg = blockIdx.x;
     const int t = n - off;  // local size
@@ -302,8 +304,13 @@ __global__ __launch_bounds__(kEigThreads) void tridiag_kernel(const double* __re
             const double tot = group_sum<LPR>(s[q]);
             const int li = lrow(q);
             const double p = (li < t && li > l1 - 1) ? tau * tot : 0.0;  // rows > k
-            const double vli = k == kbeg ? vc[li < kEigMaxN ? li : 0]
-                                         : (li == l1 ? 1.0 : ((li > l1 && li < t) ? rb[li] * scal : 0.0));
+            const int lc = li < kEigMaxN ? li : 0;
+            double vli;
+            if (k == kbeg) {  // (uniform branch)
+                vli = vc[lc];
+            } else {  // the LDS read is unconditional (a select around it became a branch + wait)
+                vli = fma(rv[lc], scal, li == l1 ? 1.0 : 0.0);
+            }
             pv += vli * p;
             if (c == 0 && li < t) {
                 if constexpr (NW == 1) ps[li] = p;
@@ -365,16 +372,17 @@ __global__ __launch_bounds__(kEigThreads) void tridiag_kernel(const double* __re
         // [C] K, w, the pivot row of A_{k+1} (into rb), |row[k+3 ..]|^2
         const double K = 0.5 * tau * kk;
         const double wk1 = pl1 - K;  // v_k[k+1] = 1
-        double xq = 0.0;
-        if (j < kEigMaxN) {
-            const double wjv = j < t ? pj - K * vc[j] : 0.0;
+        double xq;
+        {
+            const double vj = vc[j];
+            const double wjv = j < t ? pj - K * vj : 0.0;
             ws[j] = wjv;
-            double rn = 0.0;
-            if (j >= l1 && j < t) {
-                rn = rj - wjv - wk1 * vc[j];
-                if (j > l1 + 1) xq = rn * rn;
-            }
+            double rn = rj - wjv - wk1 * vj;
+            rn = (j >= l1 && j < t) ? rn : 0.0;
+            const double rt = j > l1 + 1 ? rn : 0.0;
+            xq = rt * rt;
             rb[j] = rn;
+            rv[j] = rt;
         }
         xq = wave_total(xq);
         if (lane == 0) red[w] = xq;
@@ -408,30 +416,28 @@ __global__ __launch_bounds__(kEigThreads) void tridiag_kernel(const double* __re
                 }
             }
         }
-        auto vnext = [&](int jj) -> double {  // v_{k+1}[jj]
-            if (!more) return 0.0;
-            return jj == l1 + 1 ? 1.0 : ((jj > l1 + 1 && jj < t) ? rb[jj] * scal : 0.0);
+        const double one = more ? 1.0 : 0.0;
+        auto vnext = [&](int jj) -> double {  // v_{k+1}[jj] (scal = 0 when !more); the read is unconditional
+            return fma(rv[jj], scal, jj == l1 + 1 ? one : 0.0);
         };
-        if (j < kEigMaxN) {
+        {
             const double v = vnext(j);
             vn[j] = v;  // own entry: read back by this thread only until the next barrier
             if (more && wg == 0 && j < t) Y[(int64_t)(k + 1) * ldy + off + j] = v;
         }
         // [D] A_{k+1} = A_k - v w^T - w v^T on the registers, and the next partial products; column
-        // groups of 4 whose columns are all <= k + 1 (dead from here on) are skipped, as are row slots
-        // whose rows on this wave are all dead; a compiler memory barrier between column groups keeps
-        // their LDS reads from being hoisted together (that kept 3 CPL extra doubles live and spilled)
+        // groups of 4 whose columns are all <= k + 1 (dead from here on) are skipped (a scalar
+        // branch).  Dead rows are updated too: v and w vanish there (v_k[i] = p_i = 0 for i <= k),
+        // so the update leaves them exactly as they are -- cheaper than per-element predication.
+        // The LDS reads are unconditional (v, w, rv are 0 past t), and a compiler memory barrier
+        // between column groups keeps their reads from being hoisted together (that spilled).
         double vi[RPL], wi[RPL];
-        bool live[RPL];
 #pragma unroll
         for (int q = 0; q < RPL; ++q) {
-            const int li = lrow(q);
-            const int lc = li < kEigMaxN ? li : kEigMaxN - 1;
-            vi[q] = li < t ? vc[lc] : 0.0;
-            wi[q] = li < t ? ws[lc] : 0.0;
+            const int li = lrow(q);  // < RPL 8 G NW <= kEigMaxN
+            vi[q] = vc[li];
+            wi[q] = ws[li];
             s[q] = 0.0;
-            // the wave's last row of slot q: (q 8G + w G + G - 1) NW + NW - 1
-            live[q] = ((q * 8 * G + w * G + G - 1) * NW + NW - 1) > l1;
         }
 #pragma unroll
         for (int u0 = 0; u0 < CPL; u0 += 4) {
@@ -445,10 +451,8 @@ __global__ __launch_bounds__(kEigThreads) void tridiag_kernel(const double* __re
                     const double wj = ws[jj], vj = vc[jj], vnj = vnext(jj);
 #pragma unroll
                     for (int q = 0; q < RPL; ++q) {
-                        if (live[q]) {
-                            a[q][u] -= vi[q] * wj + wi[q] * vj;
-                            s[q] += a[q][u] * vnj;
-                        }
+                        a[q][u] -= vi[q] * wj + wi[q] * vj;
+                        s[q] += a[q][u] * vnj;
                     }
                 }
             }
