@@ -68,9 +68,10 @@ template <> struct Vec16<double> {
 // a cooperative launch, so co-residency is the runtime's guarantee -- the launch fails when the
 // grid cannot be resident at once (e.g. CUs held by another process's kernels) -- instead of an
 // assumption the kernel's bounded spins can only report after the fact.
-// RSVD_COOP=0 in the environment launches them plainly (the same kernel; for profiling runs:
-// rocprofv3 7.2's kernel-trace teardown segfaults at process exit after a cooperative launch --
-// C4 / C5 traces, never C2's -- although the trace it wrote is complete).
+// RSVD_COOP=0 in the environment launches them plainly (the same kernel; for profiling runs that
+// need a clean exit: under rocprofv3 7.2 --kernel-trace ANY process that made a cooperative launch
+// segfaults in the HIP runtime's exit-time teardown, after the trace is written -- reproduced without
+// this library by tools/coop_repro.hip, see profiles/r04_exit_segv/README.md).
 inline bool coop_launch_enabled() {
     static const int env = [] {
         const char* v = std::getenv("RSVD_COOP");
