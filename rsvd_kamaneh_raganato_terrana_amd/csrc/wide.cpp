@@ -128,7 +128,8 @@ struct WideLayout {
         off_R1 = take(sizeof(double) * L2);
         off_Uw = take(sizeof(double) * L2);
         off_Vw = take(sizeof(double) * L2);
-        off_JX = take(sizeof(double) * 2 * L2);
+        // (also the two-level Cholesky's scratch during the QR chain, up to 3 levels at LP = 512)
+        off_JX = take(sizeof(double) * std::max<size_t>(2 * L2, LP >= 256 ? chol_2level_scratch_doubles(LP, 1) : 0));
         off_JJ = take(sizeof(double) * 2 * L2);
         off_M32 = take(sizeof(float) * 3 * L2);  // Rinv, Uw, Vw in fp32 (panel_gemm operand for fp32 panels)
         off_MS = take(sizeof(T) == 4 ? sizeof(bf16_t) * 3 * L2 : 0);  // the three bf16 pieces of panel_gemm's M
@@ -289,10 +290,12 @@ struct WideEngine {
     bf16_t* Ms = nullptr;
     bf16_t* ms() const { return split_panel ? Ms : nullptr; }
     // two-level factor: bit 0 at LP = 512, bit 1 at LP = 256 (RSVD_CHOL2 overrides; 0: one level
-    // everywhere).  Default LP = 512 only: at LP = 256 two chol_reg<8> levels (70 us each) + four
-    // 128^3 products (14 us each, latency-bound) lose to the one-level 175 us factor (C4 28.63 vs
-    // 28.88 ms on the same box)
-    int chol2 = 1;
+    // everywhere).  Round 4 default 3: with the K-split 128^3 / 256^3 products (four waves per tile)
+    // and the DPP diagonal factor, tools/wide_lab chol: LP = 256 one level 157.8 us vs two levels
+    // 145.5 us; LP = 512 two levels 350.2 us vs three (each 256 level itself two-level) 321.8 us
+    int chol2 = 3;
+    // LP = 512 with bit 1 also set: each 256-column level is itself two-level (three levels of 128)
+    int chol_depth() const { return (L.LP == 512 && (chol2 & 2)) ? 1 : 0; }
     int bj_groups = 0;  // block-Jacobi row groups (0: auto; RSVD_BJ_GROUPS, for A/B runs)
     bool eig_svd = true;  // fp32 results: the small SVD through the eigensolver (RSVD_SMALL_SVD=jacobi: block Jacobi)
     // panel_gemm's operand in the panel precision: fp64 matrices as-is, fp32 copies for fp32 panels
@@ -313,7 +316,8 @@ struct WideEngine {
         const bool two = (chol2 & (L.LP == 512 ? 1 : (L.LP == 256 ? 2 : 0))) && L.l > L.LP / 2;
         auto factor = [&](int* fl, double ill_tol, int* ill) -> hipError_t {
             if (two)
-                return launch_chol_wide_2level(G, L.l, L.LP, tol(), R, Rinv, r32, colflag, fl, W, JX, s, ill_tol, ill);
+                return launch_chol_wide_2level(G, L.l, L.LP, tol(), R, Rinv, r32, colflag, fl, W, JX, s, ill_tol, ill,
+                                               nullptr, chol_depth());
             return launch_chol_wide(G, L.l, L.LP, tol(), R, Rinv, r32, colflag, fl, W, nullptr, s, ill_tol, ill);
         };
         if (split_gram && !sharded && !pred) {
@@ -531,7 +535,7 @@ int wide_typed(rsvd_handle_t h, const rsvd_desc_t* d, const void* A, const void*
         E.split_gram = env != 0 && sizeof(T) == 4 && L.lowp && gram_split_ok(L.LP);
         static const int env2 = [] {
             const char* v = std::getenv("RSVD_CHOL2");
-            return v ? std::atoi(v) : 1;
+            return v ? std::atoi(v) : 3;
         }();
         E.chol2 = env2;
         static const int env3 = [] {

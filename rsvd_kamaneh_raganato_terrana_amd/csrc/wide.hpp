@@ -81,13 +81,15 @@ hipError_t launch_chol_wide(const double* G, int l, int LP, double tol, double* 
                             int* colflag, int* flag, double* work, const int* pred, hipStream_t s,
                             double ill_tol = 0.0, int* ill = nullptr, const double* d0src = nullptr);
 // The same factor at LP = 2 B (B = 128, 256; l > B) in two B-column levels: R11 = chol(G11) and
-// S = G22 - R12^T R12 (R12 = R11^-T G12) on the one-workgroup LP = B kernels, the off-diagonal
-// blocks R12 and Rinv12 = -Rinv11 R12 Rinv22 on a B^3 fp64 MFMA GEMM, breakdowns judged against the
-// diagonal of G as the one-level factor does.  scratch: kChol2ScratchDoubles.
+// S = G22 - R12^T R12 (R12 = R11^-T G12), the off-diagonal blocks R12 and Rinv12 = -Rinv11 R12 Rinv22
+// on a B^3 fp64 MFMA GEMM, breakdowns judged against the diagonal of G (d0src when this factor is
+// itself a level) as the one-level factor does.  The levels are the one-workgroup LP = B kernels,
+// or (depth > 0, B = 256) two-level factors themselves.  scratch: chol_2level_scratch_doubles.
 hipError_t launch_chol_wide_2level(const double* G, int l, int LP, double tol, double* R, double* Rinv,
                                    float* Rinv32, int* colflag, int* flag, double* work, double* scratch,
-                                   hipStream_t s, double ill_tol = 0.0, int* ill = nullptr);
-constexpr size_t kChol2ScratchDoubles = (size_t)7 * 256 * 256 + 768;
+                                   hipStream_t s, double ill_tol = 0.0, int* ill = nullptr,
+                                   const double* d0src = nullptr, int depth = 0);
+size_t chol_2level_scratch_doubles(int LP, int depth);
 // G = P^T P of an fp32 panel by the three-piece bf16 split on the bf16 MFMA (fp32 chunk sums added
 // in fp64; |dG| ~ 1e-8 |G|) -- same plan / slab layout as launch_gram_wide.  LP in {128, 256, 512}.
 bool gram_split_ok(int LP);

@@ -1054,7 +1054,8 @@ void tri_prof_read(long long* out) {
 size_t eig_svd_ws_doubles(int LP) {
     const size_t L2 = (size_t)LP * LP;
     const size_t nb = (LP + kWY - 1) / kWY;
-    return 9 * L2 + nb * kWY * kWY + 4 * (size_t)LP + 64 + 2 * (size_t)(2 * kEigMaxN);
+    // exchange: 2 parities x (p of n rows + 8 NW v.p partials + one row), NW <= 16
+    return 9 * L2 + nb * kWY * kWY + 4 * (size_t)LP + 64 + 2 * (size_t)(2 * kEigMaxN + 8 * 16);
 }
 
 template <typename T>

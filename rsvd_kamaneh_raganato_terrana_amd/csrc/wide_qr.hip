@@ -586,6 +586,91 @@ __device__ __forceinline__ void chol_diag16_fast(double (&col)[16], int p16, int
     }
 }
 
+// The same factor with the row broadcasts on the 64-bit DPP of gfx90a+ (row_newbcast:i -- lane i of
+// every 16-lane row to the whole row): the tile is replicated in the wave's four rows (lane j of each
+// row owns column j), so D[k][i] = lane i's col[k] reaches every lane of the row inside the FMA that
+// uses it -- v_fmac_f64_dpp, ONE instruction per update instead of two v_readlane (SGPRs, which the
+// compiler hoisted and spilled) and an FMA.  Same operations in the same order (fma(d, -c, x) rounds as
+// fma(-d, c, x)): bit-identical to chol_diag16_fast.  The d0 diagonal of the block is read before the
+// pivot chain (lane j: d0[p16 + j], broadcast per pivot).  The asm carries `s_nop 1` for the
+// VALU-write -> DPP-read hazard (the compiler's hazard recognizer does not look into inline asm).
+template <int I>
+__device__ __forceinline__ double nbcast_f64(double v) {
+    double r;
+    asm("s_nop 1\n\tv_mov_b64_dpp %0, %1 row_newbcast:%2 row_mask:0xf bank_mask:0xf" : "=v"(r) : "v"(v), "i"(I));
+    return r;
+}
+template <int I>
+__device__ __forceinline__ void fmac_nbcast_f64(double& acc, double x, double y) {  // acc += x[lane I of the row] * y
+    asm("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+        : "+v"(acc)
+        : "v"(x), "v"(y), "i"(I));
+}
+template <int K, int I>
+__device__ __forceinline__ void diag16_updates(double (&col)[16], double (&acc)[16], double ck, double nck, double yk) {
+    if constexpr (I < 16) {
+        fmac_nbcast_f64<I>(col[I], ck, nck);  // col[i] -= D[k][i] col[k]
+        fmac_nbcast_f64<I>(acc[I], ck, yk);   // acc[i] += D[k][i] Y[k][j]
+        diag16_updates<K, I + 1>(col, acc, ck, nck, yk);
+    }
+}
+template <int K>
+__device__ __forceinline__ void diag16_pivots(double (&col)[16], double (&acc)[16], int j, int p16, int l, double tol,
+                                              double d0j, double* Di, int lane, int& badmask) {
+    if constexpr (K < 16) {
+        const int gk = p16 + K;
+        const double dkk = nbcast_f64<K>(col[K]);
+        const double d0k = nbcast_f64<K>(d0j);
+        const bool pad = gk >= l;
+        const bool isbad = !pad && (!(dkk > tol * d0k) || !(d0k > 0.0) || !isfinite(dkk));
+        if (isbad) badmask |= 1 << K;
+        const bool unit = pad || isbad;
+        const double y = unit ? 1.0 : rsqrt_nr(dkk);
+        const double rk = unit ? 1.0 : dkk * y;
+        const double v = unit ? 0.0 : col[K] * y;
+        col[K] = (j == K) ? rk : v;
+        const double yk = ((j == K ? 1.0 : 0.0) - acc[K]) * y;  // Y[k][j] = D^-1[j][k]
+        if (lane < 16) Di[j * 16 + K] = yk;
+        diag16_updates<K, K + 1>(col, acc, col[K], -col[K], yk);
+        diag16_pivots<K + 1>(col, acc, j, p16, l, tol, d0j, Di, lane, badmask);
+    }
+}
+__device__ __forceinline__ void chol_diag16_dpp(double (&col)[16], int p16, int l, int LP, double tol, const double* d0,
+                                                double* Di, int* bad, double* R, double* Rinv, int* colflag, int* flag,
+                                                int lane) {
+    const int j = lane & 15;
+    const double d0j = d0[p16 + j];
+    int badmask = 0;  // the same in every lane (uniform tests)
+    double acc[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.0;
+    diag16_pivots<0>(col, acc, j, p16, l, tol, d0j, Di, lane, badmask);
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+        if (i > j) col[i] = 0.0;
+    if (lane < 16) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) R[(int64_t)(p16 + i) * LP + p16 + j] = col[i];
+        bad[lane] = (badmask >> lane) & 1;
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's D^-1 rows landed
+    __builtin_amdgcn_wave_barrier();
+    if (lane < 16) {
+#pragma unroll
+        for (int i = 0; i < 16; i += 2)
+            *reinterpret_cast<double2*>(Rinv + (int64_t)(p16 + j) * LP + p16 + i) =
+                *reinterpret_cast<const double2*>(Di + j * 16 + i);
+    }
+    if (lane == 0 && badmask) {
+        atomicAdd(flag, __popc(badmask));
+        for (int k = 0; k < 16; ++k)
+            if (badmask & (1 << k)) colflag[p16 + k] = 1;
+    }
+}
+#ifndef RSVD_CHOL_DIAG
+#define RSVD_CHOL_DIAG chol_diag16_dpp
+#endif
+
 // The split-Gram fallback test after a factor (off the pivot chain): ill = some valid pivot broke
 // down or R_kk^2 <= ill_tol G_kk.  Called by the whole workgroup after its last barrier (the R
 // diagonal and colflag stores of the factor are then visible workgroup-wide).
@@ -768,7 +853,7 @@ __global__ __launch_bounds__(NT) void chol_wide_kernel(const double* __restrict_
                 for (int i = 0; i < 16; ++i) col[i] = Tsc[i * 16 + r];
                 __builtin_amdgcn_s_waitcnt(0xc07f);
                 __builtin_amdgcn_wave_barrier();
-                chol_diag16_fast(col, 16 * b1, l, LP, tol, d0, Dd + (b1 & 1) * 256, bad + (b1 & 1) * 16, R, Rinv,
+                RSVD_CHOL_DIAG(col, 16 * b1, l, LP, tol, d0, Dd + (b1 & 1) * 256, bad + (b1 & 1) * 16, R, Rinv,
                                  colflag, flag, lane);
             } else if (p >= 0) {
                 // local tile t of the (nt2 x nt2) upper triangle; t = 0 is wave 0's
@@ -932,7 +1017,7 @@ __global__ __launch_bounds__(64 * kCholRegWaves) void chol_reg_kernel(const doub
             for (int i = 0; i < 16; ++i) col[i] = Tsc[i * 16 + r];
             __builtin_amdgcn_s_waitcnt(0xc07f);
             __builtin_amdgcn_wave_barrier();
-            chol_diag16_fast(col, p16, l, LP, tol, d0, Di + (p & 1) * 256, bad + (p & 1) * 16, R, Rinv,
+            RSVD_CHOL_DIAG(col, p16, l, LP, tol, d0, Di + (p & 1) * 256, bad + (p & 1) * 16, R, Rinv,
                             colflag, flag, lane);
         }
         __syncthreads();
@@ -1649,12 +1734,13 @@ hipError_t launch_chol_wide(const double* G, int l, int LP, double tol, double* 
 // ---- two-level factor, LP = 2 B (launch_chol_wide_2level) ----------------------------------------
 // Ga = G11, Sb = G22 (B x B, ld B), d0b = diag(G22): the breakdown / ill tests of the second level
 // judge S's pivots against G's own diagonal, as the one-level factor does
+// (d0src: the diagonal the tests judge against when this factor is itself a second level)
 __global__ void chol2_prep_kernel(const double* __restrict__ G, int B, double* __restrict__ Ga, double* __restrict__ Sb,
-                                  double* __restrict__ d0b) {
+                                  double* __restrict__ d0b, const double* __restrict__ d0src) {
     const int i = blockIdx.x, c = threadIdx.x, LP = 2 * B;  // B x B
     Ga[i * B + c] = G[(int64_t)i * LP + c];
     Sb[i * B + c] = G[(int64_t)(B + i) * LP + B + c];
-    if (c == 0) d0b[i] = G[(int64_t)(B + i) * LP + B + i];
+    if (c == 0) d0b[i] = d0src ? d0src[B + i] : G[(int64_t)(B + i) * LP + B + i];
 }
 // rows of R12 (row-major, ld 2 B) whose first-level pivot broke down are zero, as the one-level
 // factor's strips are
@@ -1694,15 +1780,22 @@ __global__ void chol2_assemble_kernel(const double* __restrict__ R11, const doub
 // row-major with ld lda / ldb): one wave per 16 x 16 output tile ((N / 16)^2 workgroups -- the
 // 64 x 64-tile general GEMM kept 16 CUs busy, 56 us per 256^3 product), four independent fp64 MFMA
 // chains over K, every operand an L2 hit.
-__global__ __launch_bounds__(64) void gemmsq_f64_kernel(int N, int ta, double alpha, const double* __restrict__ A,
-                                                        int lda, const double* __restrict__ B, int ldb, double beta,
-                                                        double* __restrict__ C, int ldc) {
-    const int lane = threadIdx.x, r = lane & 15, h = lane >> 4;
+// K is split over the workgroup's four waves (a quarter each, four chains per wave: the one-wave form
+// was a 16-deep dependent MFMA chain per accumulator behind L2 loads, 24 us per 256^3 product); the
+// wave partials are summed through LDS in wave order.
+constexpr int kGemmSqWaves = 4;
+__global__ __launch_bounds__(64 * kGemmSqWaves) void gemmsq_f64_kernel(int N, int ta, double alpha,
+                                                                       const double* __restrict__ A, int lda,
+                                                                       const double* __restrict__ B, int ldb,
+                                                                       double beta, double* __restrict__ C, int ldc) {
+    __shared__ double part[kGemmSqWaves - 1][4][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 15, h = lane >> 4;
     const int nt = N / 16;
     const int i0 = 16 * (blockIdx.x / nt), j0 = 16 * (blockIdx.x % nt);
+    const int kq = N / kGemmSqWaves;  // N % 64 == 0
     f64x4 acc[4] = {MD::zero(), MD::zero(), MD::zero(), MD::zero()};
-#pragma unroll 4
-    for (int k0 = 0; k0 < N; k0 += 16) {
+#pragma unroll 2
+    for (int k0 = w * kq; k0 < (w + 1) * kq; k0 += 16) {
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
             const int k = k0 + 4 * u + h;
@@ -1710,43 +1803,74 @@ __global__ __launch_bounds__(64) void gemmsq_f64_kernel(int N, int ta, double al
             acc[u] = MD::mma(a, B[(int64_t)k * ldb + j0 + r], acc[u]);
         }
     }
+    double v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = (acc[0][j] + acc[1][j]) + (acc[2][j] + acc[3][j]);
+    if (w > 0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) part[w - 1][j][lane] = v[j];
+    }
+    __syncthreads();
+    if (w != 0) return;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {  // f64 D: col = r, row = h + 4 j
+#pragma unroll
+        for (int q = 0; q < kGemmSqWaves - 1; ++q) v[j] += part[q][j][lane];
         double* c = C + (int64_t)(i0 + MD::row(h, j)) * ldc + j0 + r;
-        const double v = alpha * ((acc[0][j] + acc[1][j]) + (acc[2][j] + acc[3][j]));
-        *c = beta == 0.0 ? v : v + beta * *c;
+        const double o = alpha * v[j];
+        *c = beta == 0.0 ? o : o + beta * *c;
     }
 }
 
 static hipError_t gemm_sq(int N, int ta, double alpha, const double* A, int lda, const double* B, int ldb, double beta,
                           double* C, int ldc, hipStream_t s) {
-    hipLaunchKernelGGL(gemmsq_f64_kernel, dim3((N / 16) * (N / 16)), dim3(64), 0, s, N, ta, alpha, A, lda, B, ldb,
-                       beta, C, ldc);
+    if (N % (16 * kGemmSqWaves)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(gemmsq_f64_kernel, dim3((N / 16) * (N / 16)), dim3(64 * kGemmSqWaves), 0, s, N, ta, alpha, A, lda,
+                       B, ldb, beta, C, ldc);
     return hipGetLastError();
+}
+
+size_t chol_2level_scratch_doubles(int LP, int depth) {
+    const size_t B = LP / 2;
+    const size_t own = 7 * B * B + B + 64;  // Ga R11 Ri11 Sb R22 Ri22 T, d0b, ill2 (+ alignment)
+    return own + (depth > 0 && B >= 256 ? chol_2level_scratch_doubles((int)B, depth - 1) : 0);
+}
+
+// One level of the factor: the two-level form (recursing `depth` more times) when LP >= 256 and more
+// than half the columns are valid, else the one-workgroup kernel.
+static hipError_t chol_level(const double* G, int l, int LP, double tol, double* R, double* Rinv, int* colflag,
+                             int* flag, double* work, double* scratch, hipStream_t s, double ill_tol, int* ill,
+                             const double* d0src, int depth) {
+    if (depth >= 0 && LP >= 256 && l > LP / 2)
+        return launch_chol_wide_2level(G, l, LP, tol, R, Rinv, nullptr, colflag, flag, work, scratch, s, ill_tol, ill,
+                                       d0src, depth);
+    return launch_chol_wide(G, l, LP, tol, R, Rinv, nullptr, colflag, flag, work, nullptr, s, ill_tol, ill, d0src);
 }
 
 hipError_t launch_chol_wide_2level(const double* G, int l, int LP, double tol, double* R, double* Rinv,
                                    float* Rinv32, int* colflag, int* flag, double* work, double* scratch,
-                                   hipStream_t s, double ill_tol, int* ill) {
+                                   hipStream_t s, double ill_tol, int* ill, const double* d0src, int depth) {
     if ((LP != 256 && LP != 512) || l <= LP / 2 || l > LP) return hipErrorInvalidValue;
     const int B = LP / 2, B2 = B * B;
     double *Ga = scratch, *R11 = Ga + B2, *Ri11 = R11 + B2, *Sb = Ri11 + B2, *R22 = Sb + B2, *Ri22 = R22 + B2,
            *T = Ri22 + B2, *d0b = T + B2;
     int* ill2 = reinterpret_cast<int*>(d0b + B);
-    hipLaunchKernelGGL(chol2_prep_kernel, dim3(B), dim3(B), 0, s, G, B, Ga, Sb, d0b);
+    double* inner = d0b + B + 64;  // the next level's scratch (depth > 0)
+    const int sub = depth - 1;     // < 0: the levels below are one-workgroup factors
+    hipLaunchKernelGGL(chol2_prep_kernel, dim3(B), dim3(B), 0, s, G, B, Ga, Sb, d0b, d0src);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     // level 1: R11, Ri11 = chol(G11) (columns 0 .. B - 1 of colflag)
-    e = launch_chol_wide(Ga, B, B, tol, R11, Ri11, nullptr, colflag, flag, work, nullptr, s, ill_tol, ill);
+    e = chol_level(Ga, B, B, tol, R11, Ri11, colflag, flag, work, inner, s, ill_tol, ill, d0src, sub);
     if (e != hipSuccess) return e;
     // R12 = Ri11^T G12 -> R[:B, B:] (ld LP), broken-down rows zeroed
     if ((e = gemm_sq(B, 1, 1.0, Ri11, B, G + B, LP, 0.0, R + B, LP, s)) != hipSuccess) return e;
     hipLaunchKernelGGL(chol2_zero_rows_kernel, dim3(B), dim3(B), 0, s, R + B, B, colflag);
     // S = G22 - R12^T R12
     if ((e = gemm_sq(B, 1, -1.0, R + B, LP, R + B, LP, 1.0, Sb, B, s)) != hipSuccess) return e;
-    // level 2 on the l - B valid columns of S, tested against diag(G22)
-    e = launch_chol_wide(Sb, l - B, B, tol, R22, Ri22, nullptr, colflag + B, flag, work, nullptr, s, ill_tol,
-                         ill ? ill2 : nullptr, d0b);
+    // level 2 on the l - B valid columns of S, tested against diag(G22) (or the caller's d0src)
+    e = chol_level(Sb, l - B, B, tol, R22, Ri22, colflag + B, flag, work, inner, s, ill_tol, ill ? ill2 : nullptr,
+                   d0b, sub);
     if (e != hipSuccess) return e;
     // Rinv12 = -Ri11 (R12 Ri22) -> Rinv[:B, B:]
     if ((e = gemm_sq(B, 0, 1.0, R + B, LP, Ri22, B, 0.0, T, B, s)) != hipSuccess) return e;
@@ -1868,7 +1992,58 @@ RSVD_INST(double)
 }  // namespace rsvd
 
 #ifdef RSVD_CHOL_PROF
+#include <vector>
 namespace rsvd {
+namespace {
+// one wave factors a 16 x 16 SPD tile `reps` times (the diagonal factor alone, no barriers): cycles per factor
+template <int V>
+__global__ __launch_bounds__(64) void diag_bench_kernel(const double* __restrict__ T, int reps, double* R, double* Rinv,
+                                                        int* colflag, int* flag, long long* out) {
+    __shared__ double Di[256], d0[16];
+    __shared__ int bad[16];
+    const int lane = threadIdx.x, r = lane & 15;
+    if (lane < 16) d0[lane] = T[lane * 16 + lane];
+    __syncthreads();
+    double col0[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) col0[i] = T[i * 16 + r];
+    double sink = 0.0;
+    const long long t0 = __builtin_amdgcn_s_memtime();
+    for (int it = 0; it < reps; ++it) {
+        double col[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) col[i] = col0[i] + sink * 1e-300;
+        if constexpr (V == 0) chol_diag16_fast(col, 0, 16, 16, 1e-13, d0, Di, bad, R, Rinv, colflag, flag, lane);
+        else chol_diag16_dpp(col, 0, 16, 16, 1e-13, d0, Di, bad, R, Rinv, colflag, flag, lane);
+        sink += col[15];
+    }
+    const long long t1 = __builtin_amdgcn_s_memtime();
+    if (lane == 0) out[V] = (t1 - t0) / reps + (sink == 12345.0 ? 1 : 0);
+}
+}  // namespace
+void chol_diag_bench() {
+    std::vector<double> h(256);
+    for (int i = 0; i < 16; ++i)
+        for (int j = 0; j < 16; ++j) h[i * 16 + j] = (i == j ? 20.0 : 0.0) + 1.0 / (1 + i + j);
+    double *T, *R, *Ri;
+    int *cf, *fl;
+    long long* out;
+    (void)hipMalloc(&T, 256 * 8);
+    (void)hipMalloc(&R, 256 * 8);
+    (void)hipMalloc(&Ri, 256 * 8);
+    (void)hipMalloc(&cf, 64);
+    (void)hipMalloc(&fl, 64);
+    (void)hipMalloc(&out, 16);
+    (void)hipMemcpy(T, h.data(), 256 * 8, hipMemcpyHostToDevice);
+    long long o[2];
+    for (int rep = 0; rep < 2; ++rep) {
+        hipLaunchKernelGGL(diag_bench_kernel<0>, dim3(1), dim3(64), 0, 0, T, 256, R, Ri, cf, fl, out);
+        hipLaunchKernelGGL(diag_bench_kernel<1>, dim3(1), dim3(64), 0, 0, T, 256, R, Ri, cf, fl, out);
+        (void)hipMemcpy(o, out, 16, hipMemcpyDeviceToHost);
+    }
+    printf("  16x16 diagonal factor, one wave: readlane form %lld cycles, DPP form %lld cycles\n", o[0], o[1]);
+    (void)hipFree(T); (void)hipFree(R); (void)hipFree(Ri); (void)hipFree(cf); (void)hipFree(fl); (void)hipFree(out);
+}
 void chol_prof_dump(int LP) {
     long long t[256];
     (void)hipMemcpyFromSymbol(t, HIP_SYMBOL(g_chol_prof), sizeof(t));

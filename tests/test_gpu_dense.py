@@ -397,3 +397,21 @@ def test_svd_big_parallel_jacobi_and_f32(engine):
     h = n // 2
     assert rel_fro(sign_align(U32[:, :h], Ul[:, :h]), Ul[:, :h]) < 1e-4
     assert rel_fro(sign_align(V32[:, :h], Vlt.T[:, :h]), Vlt.T[:, :h]) < 1e-4
+
+
+def test_svd_jacobi_tall_rank_deficient(engine):
+    """SVD<Jacobi> with max(m, n) far past what per-row LDS could hold (24000 rows) and
+    zero singular values, so the completion kernel (block_jacobi_complete_kernel, LDS sized by the
+    column count) runs: S against LAPACK, the rank-590 part of U, V sign-aligned, U and V orthonormal
+    and U S V^T = A."""
+    m, n, r = 24000, 600, 590
+    sig = np.concatenate([0.99 ** np.arange(r), np.zeros(n - r)])
+    A = _spectrum_matrix(m, n, sig, seed=24)
+    U, S, V = engine.svd_host(A, 0)
+    Ul, Sl, Vlt = np.linalg.svd(A, full_matrices=False)
+    assert U.shape == (m, n) and S.shape == (n,) and V.shape == (n, n)
+    assert np.max(np.abs(S - Sl)) < 1e-12 * Sl[0]
+    assert rel_fro(sign_align(U[:, :r], Ul[:, :r]), Ul[:, :r]) < 1e-9
+    assert rel_fro(sign_align(V[:, :r], Vlt.T[:, :r]), Vlt.T[:, :r]) < 1e-9
+    assert _orth_err(U) < 1e-12 and _orth_err(V) < 1e-12
+    assert rel_fro((U * S) @ V.T, A) < 1e-12

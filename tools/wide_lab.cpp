@@ -116,6 +116,33 @@ static void bench_gram() {
     }
 }
 
+static void bench_gsplit() {  // the split Gram (bf16 MFMA) against the fp64 Gram of the same panel
+    for (int LP : {128, 256, 512}) {
+        const int64_t rows = LP == 128 ? (1 << 20) : (LP == 256 ? 65536 : 131072);
+        float* P = dev_random<float>((size_t)rows * LP);
+        GramPlan gp = plan_gram_wide(rows, LP, 0);
+        double *slabs, *G, *G64;
+        CK(hipMalloc(&slabs, (size_t)gp.blocks * gp.chunks * 1024 * 8));
+        CK(hipMalloc(&G, (size_t)LP * LP * 8));
+        CK(hipMalloc(&G64, (size_t)LP * LP * 8));
+        double t = time_us([&] { CK(launch_gram_split(P, rows, LP, gp, slabs, G, S)); });
+        CK(launch_gram_wide<float>(P, nullptr, rows, LP, gp, slabs, G64, nullptr, S));
+        CK(hipStreamSynchronize(S));
+        std::vector<double> a((size_t)LP * LP), b((size_t)LP * LP);
+        CK(hipMemcpy(a.data(), G, a.size() * 8, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(b.data(), G64, b.size() * 8, hipMemcpyDeviceToHost));
+        double md = 0;
+        for (int i = 0; i < LP; ++i)
+            for (int j = i; j < LP; ++j)
+                md = std::max(md, std::fabs(a[(size_t)i * LP + j] - b[(size_t)i * LP + j]) /
+                                      std::sqrt(b[(size_t)i * LP + i] * b[(size_t)j * LP + j]));
+        const double fl = 6.0 * rows * LP * (LP + 16);  // six bf16 products over the upper tile triangle
+        printf("gram_split rows=%ld LP=%d chunks=%d: %.1f us (%.0f TF/s bf16 issued, %.0f GB/s)  max|dG|/sqrt(GiiGjj) %.2e\n",
+               (long)rows, LP, gp.chunks, t, fl / t / 1e6, rows * LP * 4.0 / t / 1e3, md);
+        CK(hipFree(P)); CK(hipFree(slabs)); CK(hipFree(G)); CK(hipFree(G64));
+    }
+}
+
 static double* spd(int LP, int l) {  // G = X^T X + I with X random l x l
     std::vector<double> X((size_t)l * l), G((size_t)LP * LP, 0.0);
     std::mt19937 g(3);
@@ -134,9 +161,12 @@ static double* spd(int LP, int l) {  // G = X^T X + I with X random l x l
 }
 
 #ifdef RSVD_CHOL_PROF
-namespace rsvd { void chol_prof_dump(int LP); }
+namespace rsvd { void chol_prof_dump(int LP); void chol_diag_bench(); }
 #endif
 static void bench_chol() {
+#ifdef RSVD_CHOL_PROF
+    rsvd::chol_diag_bench();
+#endif
     for (int LP : {64, 128, 256, 512}) {
         double* G = spd(LP, LP);
         double *R, *Ri, *W;
@@ -183,6 +213,30 @@ static void bench_chol() {
         const bool same = !memcmp(hR0.data(), hR.data(), hR.size() * 8) && !memcmp(hRi0.data(), hRi.data(), hRi.size() * 8);
         printf("chol LP=%d: wide %.1f us  reg %.1f us  bit-identical %d   |R^T R - G|/|G| = %.2e  |R Rinv - I| = %.2e\n", LP,
                t0, t, (int)same, sqrt(e1 / ng), sqrt(e2));
+        for (int depth = 0; LP >= 256 && depth <= (LP == 512 ? 1 : 0); ++depth) {  // the two-level factor
+            double* scr;
+            CK(hipMalloc(&scr, chol_2level_scratch_doubles(LP, depth) * 8));
+            double t2 = time_us([&] {
+                CK(launch_chol_wide_2level(G, LP, LP, 1e-13, R, Ri, R32, cf, fl, W, scr, S, 0.0, nullptr, nullptr,
+                                           depth));
+            });
+            CK(hipMemcpy(hR.data(), R, hR.size() * 8, hipMemcpyDeviceToHost));
+            CK(hipMemcpy(hRi.data(), Ri, hRi.size() * 8, hipMemcpyDeviceToHost));
+            double f1 = 0, f2 = 0;
+            for (int i = 0; i < LP; ++i)
+                for (int j = 0; j < LP; ++j) {
+                    double s = 0, s2 = 0;
+                    for (int k = 0; k < LP; ++k) {
+                        s += hR[(size_t)k * LP + i] * hR[(size_t)k * LP + j];
+                        s2 += hR[(size_t)i * LP + k] * hRi[(size_t)k * LP + j];
+                    }
+                    f1 += (s - hG[(size_t)i * LP + j]) * (s - hG[(size_t)i * LP + j]);
+                    f2 += (s2 - (i == j)) * (s2 - (i == j));
+                }
+            printf("chol2 LP=%d depth %d: %.1f us   |R^T R - G|/|G| = %.2e  |R Rinv - I| = %.2e\n", LP, depth, t2,
+                   sqrt(f1 / ng), sqrt(f2));
+            CK(hipFree(scr));
+        }
         CK(hipFree(G)); CK(hipFree(R)); CK(hipFree(Ri)); CK(hipFree(W)); CK(hipFree(R32)); CK(hipFree(cf)); CK(hipFree(fl));
     }
 }
@@ -678,6 +732,7 @@ int main(int argc, char** argv) {
     if (what == "all" || what == "pg") bench_pg();
     if (what == "all" || what == "gram") bench_gram();
     if (what == "all" || what == "chol") bench_chol();
+    if (what == "gsplit") bench_gsplit();
     if (what == "all" || what == "jac") bench_jac();
     if (what == "all" || what == "proj") bench_proj();
     if (what == "proj4") bench_proj(true);
