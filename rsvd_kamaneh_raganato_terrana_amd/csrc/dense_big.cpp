@@ -408,11 +408,28 @@ int big_rsvd_typed(rsvd_handle_t h, const rsvd_desc_t* d, const void* Av, const 
     // (their Grams and block projections all-reduced), A^T Q is all-reduced, the n side replicated
     const int32_t tdt = sizeof(T) == 8 ? RSVD_F64 : RSVD_F32;
     if (h->world > 1) {
+        // the global row count, the SAME on every rank: it sets the CholeskyQR shift, which must give
+        // bit-identical R factors everywhere (world * m differed by rank under the reference's
+        // remainder rule -- 1001 / 1000 rows -- and the ranks' Q then disagreed at 1.7e-4)
+        if (!h->allreduce) {
+            h->err = "l > 512 on several ranks needs the all-reduce hook";
+            return RSVD_ERR_COMM;
+        }
+        const T mloc = (T)m;
+        RSVD_CK(hipMemcpyAsync(R, &mloc, sizeof(T), hipMemcpyHostToDevice, s));
+        if (h->allreduce(R, 1, tdt, (void*)s, h->ar_user) != 0) {
+            h->err = "all-reduce hook failed";
+            return RSVD_ERR_COMM;
+        }
+        T mg = 0;
+        RSVD_CK(hipMemcpyAsync(&mg, R, sizeof(T), hipMemcpyDeviceToHost, s));
+        RSVD_CK(hipStreamSynchronize(s));
+        const int64_t m_global = (int64_t)(mg + (T)0.5);
         Em.shard = true;
         Em.row_off = (int64_t)h->rank << 40;
         Em.rows_total = (int64_t)h->world << 40;
-        Em.norm_rows = (int64_t)h->world * m;
-        Em.rows_global = (int64_t)h->world * m;
+        Em.norm_rows = m_global;
+        Em.rows_global = m_global;
     }
     auto reduce_z = [&]() -> int {
         if (h->world <= 1 || !h->allreduce) return RSVD_OK;

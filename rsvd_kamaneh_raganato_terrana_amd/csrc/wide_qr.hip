@@ -348,16 +348,26 @@ __global__ __launch_bounds__(GramSplit<LP>::THREADS) void gram_split_kernel(cons
 
     // thread unit u = tid + THREADS t (u < NU): rows kr = 4 (u & 7) .. + 3 of columns 4 (u >> 3) .. + 3
     float4 reg[LPT][4];
+    // (the unit guard is wave-uniform -- NU is a multiple of 64 -- and a full step loads unguarded: a
+    // per-load guard compiled to an exec branch per load; the partial last step clamps and zeroes)
     auto load = [&](int64_t r0) {
+        const bool full = r0 + 32 <= end;
 #pragma unroll
         for (int t = 0; t < LPT; ++t) {
             const int u = tid + G::THREADS * t;
+            if (u - lane >= G::NU) break;
             const int64_t row = r0 + 4 * (u & 7);
             const int c = 4 * (u >> 3);
 #pragma unroll
-            for (int q = 0; q < 4; ++q)
-                reg[t][q] = (u < G::NU && row + q < end) ? *reinterpret_cast<const float4*>(P + (row + q) * LP + c)
-                                                         : make_float4(0.f, 0.f, 0.f, 0.f);
+            for (int q = 0; q < 4; ++q) {
+                if (full) {
+                    reg[t][q] = *reinterpret_cast<const float4*>(P + (row + q) * LP + c);
+                } else {
+                    const int64_t rr = row + q < end ? row + q : end - 1;
+                    const float4 x = *reinterpret_cast<const float4*>(P + rr * LP + c);
+                    reg[t][q] = row + q < end ? x : make_float4(0.f, 0.f, 0.f, 0.f);
+                }
+            }
         }
     };
     auto stage = [&](char* img) {
@@ -428,6 +438,223 @@ __global__ __launch_bounds__(GramSplit<LP>::THREADS) void gram_split_kernel(cons
         }
         buf = G::NBUF - 1 - buf;
     }
+#pragma unroll
+    for (int i = 0; i < TG; ++i)
+#pragma unroll
+        for (int j = 0; j < TG; ++j) {
+            const int ta = GA * TG + i, tb = GB * TG + j;
+            if (ta > tb) continue;  // (diagonal group pairs) the mirror of an upper pair
+            const int a = ta >> 1, b = tb >> 1;
+            const int blk = a * G::NB - a * (a - 1) / 2 + (b - a);
+            double* dst = slabs + ((int64_t)chunk * G::NBLK + blk) * 1024;
+            const bool mirror = (a == b) && (ta != tb);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {  // bf16 MFMA D: col = lane & 15, row = 4 h + e
+                const int li = 16 * (ta & 1) + 4 * h + e, lj = 16 * (tb & 1) + r;
+                dst[li * 32 + lj] = (double)acc[i][j][e];
+                if (mirror) dst[lj * 32 + li] = (double)acc[i][j][e];
+            }
+        }
+}
+
+// LP = 512, round 4: the same arithmetic (six bf16 products per tile pair, fp32 chunk accumulators,
+// the same slabs) with each of a chunk's workgroups staging ONLY the column groups its group pairs
+// read.  gram_split_kernel<512> staged all 512 columns (96 KB per 32-row step) in each of four
+// workgroups: single-buffered, the VALU split work (430 instructions per wave per step) run 4x over
+// between barriers, 168 VGPRs with spills at 9 waves -- rocprofv3: MFMA busy 23 %, waves parked
+// 61 %, LDS 11 % busy.  Here the 36 group pairs of the 8 column groups (64 columns each) are dealt
+// to five 8-wave workgroup types, each reading at most 6 groups:
+//   0: groups {0,1,2,3}, pairs (0,0) (0,1) (0,2) (1,1) (1,2) (2,2) (0,3) (1,3)
+//   1: groups {4,5,6,7}, the same pairs shifted by 4
+//   2: {0,1} x {4,5,6,7}    3: {2,3} x {4,5,6,7}    4: (2,3) (3,3) (6,7) (7,7)
+// so a step is at most 6 groups (72 KB): two buffers fit the LDS and the next step's split is
+// staged while this step's MFMAs run (one barrier per step), at 2 waves per SIMD (256 VGPRs).
+struct GramSplit4 {
+    static constexpr int LP = 512, TG = 4, NB = 16, NBLK = NB * (NB + 1) / 2;
+    static constexpr int TYPES = 5, WAVES = 12, THREADS = 64 * WAVES;  // 8 MFMA waves + 4 staging waves
+    static constexpr int CWAVES = 8, SWAVES = WAVES - CWAVES;
+    static constexpr int MAXG = 6;                 // staged groups (64 columns) per workgroup, at most
+    static constexpr int IMG = MAXG * 64 * 64;     // bytes of one piece image (6 x 64 columns x 32 rows bf16)
+    static constexpr int STEP = 3 * IMG;           // one 32-row step, three pieces (72 KB)
+    static constexpr int LDS = 2 * STEP;           // double-buffered: 144 KB
+    static constexpr int LPT = (MAXG * 64 * 4 + 64 * SWAVES - 1) / (64 * SWAVES);  // 8-row units per staging thread
+};
+
+// global group of local staged group lg, for workgroup type ty
+__device__ __forceinline__ int gs4_group(int ty, int lg) {
+    switch (ty) {
+        case 0: return lg;
+        case 1: return 4 + lg;
+        case 2: return lg < 2 ? lg : 2 + lg;
+        case 3: return 2 + lg;
+        default: return lg < 2 ? 2 + lg : 4 + lg;
+    }
+}
+
+__global__ __launch_bounds__(GramSplit4::THREADS) void gram_split4_kernel(const float* __restrict__ P, int64_t rows,
+                                                                         int64_t rpc, int nchunk,
+                                                                         double* __restrict__ slabs, int ablate) {
+    typedef GramSplit4 G;
+    constexpr int TG = G::TG, LPT = G::LPT;
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    const int tid = threadIdx.x, lane = tid & 63, r = lane & 15, h = lane >> 4;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    // a chunk's five workgroups are 8 apart in dispatch order: one XCD (its L2 serves the repeats)
+    const int v = blockIdx.x >> 3;
+    const int ty = v % G::TYPES;
+    const int chunk = ((v / G::TYPES) << 3) | (blockIdx.x & 7);
+    if (chunk >= nchunk) return;
+    const int64_t beg = (int64_t)chunk * rpc;
+    const int64_t end = (beg + rpc < rows) ? beg + rpc : rows;
+    const int ngl = (ty == 2 || ty == 3) ? 6 : 4;  // staged groups
+    const int NU = ngl * 64 * 4;                  // units of a step
+    // this wave's group pair: local (LA <= LB) and global (GA <= GB)
+    int LA, LB;
+    bool active = true;
+    if (ty < 2) {
+        LA = (0x10211000 >> (4 * w)) & 15;  // w = 0..7: 0 0 0 1 1 2 0 1
+        LB = (0x33221210 >> (4 * w)) & 15;  //          0 1 2 1 2 2 3 3
+    } else if (ty < 4) {
+        LA = w >> 2;
+        LB = 2 + (w & 3);
+    } else {
+        LA = w & 3;
+        LB = (w & 2) ? 3 : 1;
+        active = w < 4;
+    }
+    const bool stager = w >= G::CWAVES;
+    if (stager) active = false;
+    const int sid = tid - 64 * G::CWAVES;  // staging thread index (stagers only)
+    const int GA = gs4_group(ty, LA), GB = gs4_group(ty, LB);
+    f32x4 acc[TG][TG];
+#pragma unroll
+    for (int i = 0; i < TG; ++i)
+#pragma unroll
+        for (int j = 0; j < TG; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    if (stager) {  // the staging waves: their own loop, the same barriers as the MFMA waves'
+        // unit u = sid + 256 t (u < NU): row octet u / ncol (8 rows) of local column u % ncol.  A wave's
+        // lanes take 64 consecutive columns (256-B row segments per load), each lane splits its 8 rows into
+        // the three pieces with no component selects, and writes one 16-B octet per piece.  LDS image as
+        // gram_split_kernel's: column c's 32 rows as four 16-B octets, octet o at o ^ ((c >> 1) & 3) -- 8
+        // consecutive columns of a ds_write_b128 lane group hit 8 distinct slots, the fragment reads'
+        // 16-lane groups 16.  Offsets are fixed for the launch: computed once.
+        const int ncol = ngl * 64;
+        int64_t goff[LPT];
+        int loff[LPT];
+#pragma unroll
+        for (int t = 0; t < LPT; ++t) {
+            const int u = sid + 64 * G::SWAVES * t;
+            const int oc = u / ncol, lc = u - oc * ncol;
+            goff[t] = (int64_t)(8 * oc) * G::LP + ((gs4_group(ty, lc >> 6) << 6) | (lc & 63));
+            loff[t] = u < NU ? lc * 64 + 16 * (oc ^ ((lc >> 1) & 3)) : -1;
+        }
+        // two steps of loads in flight (a step's stage is ~1 us of work, an HBM round trip under this
+        // load longer): register sets A and B alternate, loads issued two steps ahead of their stage
+        typedef float Regs[LPT][8];
+        Regs ra, rb;
+        // (every guard is wave-uniform: no per-load exec branches -- they were 10 instructions per load;
+        // the rows of a chunk's partial last step are clamped and zeroed)
+        const int tmax = ngl == 6 ? LPT : 4;  // units t >= tmax do not exist for the 4-group types
+        auto load = [&](Regs& reg, int64_t r0) {
+            const bool full = r0 + 32 <= end;
+#pragma unroll
+            for (int t = 0; t < LPT; ++t) {
+                if (t >= tmax) break;
+                if (full) {
+                    const float* src = P + r0 * G::LP + goff[t];
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) reg[t][q] = src[q * G::LP];
+                } else {
+                    const int64_t row = r0 + (goff[t] >> 9);  // + 8 oc (G::LP = 512)
+                    const int gc = (int)(goff[t] & (G::LP - 1));
+#pragma unroll
+                    for (int q = 0; q < 8; ++q) {
+                        const int64_t rr = row + q < end ? row + q : end - 1;
+                        const float x = P[rr * G::LP + gc];
+                        reg[t][q] = row + q < end ? x : 0.f;
+                    }
+                }
+            }
+        };
+        auto stage = [&](const Regs& reg, char* img) {
+#pragma unroll
+            for (int t = 0; t < LPT; ++t) {
+                if (t >= tmax) break;
+                uint32_t pw[3][4];
+#pragma unroll
+                for (int q = 0; q < 8; q += 2) {
+                    // exact three-piece split, two rows at a time: h = bf16(v), m = bf16(v - h), t = v - h - m
+                    const float a = reg[t][q], b = reg[t][q + 1];
+                    const uint32_t ph = cvt_pk_bf16(a, b);
+                    const float ra_ = a - __uint_as_float(ph << 16), rb_ = b - __uint_as_float(ph & 0xffff0000u);
+                    const uint32_t pm = cvt_pk_bf16(ra_, rb_);
+                    const float ta = ra_ - __uint_as_float(pm << 16), tb = rb_ - __uint_as_float(pm & 0xffff0000u);
+                    pw[0][q >> 1] = ph;
+                    pw[1][q >> 1] = pm;
+                    pw[2][q >> 1] = cvt_pk_bf16(ta, tb);
+                }
+#pragma unroll
+                for (int x = 0; x < 3; ++x)
+                    *reinterpret_cast<uint4*>(img + x * G::IMG + loff[t]) = make_uint4(pw[x][0], pw[x][1], pw[x][2], pw[x][3]);
+            }
+        };
+        if (beg < end) {
+            load(ra, beg);
+            stage(ra, smem_raw);
+            if (beg + 32 < end) load(rb, beg + 32);
+            if (beg + 64 < end) load(ra, beg + 64);
+        }
+        __syncthreads();
+        // iteration of step r0: stage step r0 + 32 into the other buffer (its last readers passed the
+        // previous barrier) from the set loaded two iterations ago, then reload that set with r0 + 96
+        auto iter = [&](Regs& reg, int64_t r0, int b) {
+            if (r0 + 32 < end && !(ablate & 2)) {
+                stage(reg, smem_raw + (b ^ 1) * G::STEP);
+                if (r0 + 96 < end) load(reg, r0 + 96);
+            }
+            __syncthreads();
+        };
+        for (int64_t r0 = beg; r0 < end; r0 += 64) {
+            iter(rb, r0, 0);
+            if (r0 + 32 < end) iter(ra, r0 + 32, 1);
+        }
+        return;
+    }
+    const uint32_t lo = (uint32_t)(r * 64 + 16 * (h ^ ((r >> 1) & 3)));
+    auto frag = [&](const char* img, int piece, int t) {  // t: local tile (16 columns)
+        return *reinterpret_cast<const bf16x8s*>(img + piece * G::IMG + t * 1024 + lo);
+    };
+    __syncthreads();  // step 0 staged
+    int buf = 0;
+    for (int64_t r0 = beg; r0 < end; r0 += 32) {
+        const char* img = smem_raw + buf * G::STEP;
+        if (active && !(ablate & 1)) {
+            bf16x8s fa[TG][3];
+#pragma unroll
+            for (int i = 0; i < TG; ++i)
+#pragma unroll
+                for (int x = 0; x < 3; ++x) fa[i][x] = frag(img, x, LA * TG + i);
+#pragma unroll
+            for (int j = 0; j < TG; ++j) {
+                const bf16x8s hb_ = frag(img, 0, LB * TG + j), mb = frag(img, 1, LB * TG + j),
+                              tb = frag(img, 2, LB * TG + j);
+#pragma unroll
+                for (int i = 0; i < TG; ++i) {
+                    f32x4 c = acc[i][j];
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][2], hb_, c, 0, 0, 0);  // smallest terms first
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], tb, c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][1], mb, c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][1], hb_, c, 0, 0, 0);
+                    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], mb, c, 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], hb_, c, 0, 0, 0);
+                }
+            }
+        }
+        __syncthreads();
+        buf ^= 1;
+    }
+    if (!active) return;
 #pragma unroll
     for (int i = 0; i < TG; ++i)
 #pragma unroll
@@ -1693,14 +1920,37 @@ hipError_t launch_gram_split(const float* P, int64_t rows, int LP, const GramPla
         hipLaunchKernelGGL(gram_split_kernel<L>, dim3(grid), dim3(GS::THREADS), GS::NBUF * GS::STEP, s, P, rows,
                            gp.rows_per_chunk, gp.chunks, slabs);
     };
+    static const int v4 = [] {  // RSVD_GSPLIT4=0: the all-columns LP = 512 kernel (A/B runs)
+        const char* e = std::getenv("RSVD_GSPLIT4");
+        return e ? std::atoi(e) : 1;
+    }();
     if (LP == 128) go(std::integral_constant<int, 128>{});
     else if (LP == 256) go(std::integral_constant<int, 256>{});
-    else go(std::integral_constant<int, 512>{});
+    int nchunk = gp.chunks;
+    if (LP == 512 && v4) {
+        // one round of 5-workgroup chunks on the 256 CUs (51 x 5 = 255), >= 512 rows each, within the
+        // plan's slab count (the fp32 accumulators then run over up to ~2600 rows, as C3's 4096 do)
+        int64_t ch = (rows + 511) / 512;
+        if (ch > 51) ch = 51;
+        if (ch > gp.chunks) ch = gp.chunks;
+        if (ch < 1) ch = 1;
+        int64_t rpc = (rows + ch - 1) / ch;
+        rpc = (rpc + 31) / 32 * 32;
+        nchunk = (int)((rows + rpc - 1) / rpc);
+        static const int abl = [] {  // lab only: bit 0 skips the MFMAs, bit 1 the staging
+            const char* e = std::getenv("RSVD_GSPLIT4_ABLATE");
+            return e ? std::atoi(e) : 0;
+        }();
+        hipLaunchKernelGGL(gram_split4_kernel, dim3((nchunk + 7) / 8 * 8 * GramSplit4::TYPES),
+                           dim3(GramSplit4::THREADS), GramSplit4::LDS, s, P, rows, rpc, nchunk, slabs, abl);
+    } else if (LP == 512) {
+        go(std::integral_constant<int, 512>{});
+    }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const int64_t tot = (int64_t)gp.blocks * 1024;
     hipLaunchKernelGGL(gram_reduce_kernel, dim3((int)((tot + 255) / 256)), dim3(256), 0, s, slabs, gp.blocks,
-                       gp.chunks, LP, 0, G, (const int*)nullptr);
+                       nchunk, LP, 0, G, (const int*)nullptr);
     return hipGetLastError();
 }
 
