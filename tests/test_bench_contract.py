@@ -43,3 +43,30 @@ def test_committed_evidence_lookups():
     assert mb is not None and 0.5 < mb["frac"] < 1.0 and mb["clock_GHz"] <= 2.4
     # a pass with an impossible clock estimate is not evidence
     assert bench.pmc_mfma_busy("c2_f32_4096x4096_l64_q2", "proj_nn_kernel") is None
+def test_self_launch_builds_torchrun_command(monkeypatch):
+    """`python bench.py --gpus N` starts its own N ranks: torch.distributed.run
+    with one process per GPU on 127.0.0.1, the bench's flags carried in RSVD_BENCH_ARGV (torchrun's
+    own parser would take --m / --n placed after the script).  The GPU run of the same path is
+    tests/test_gpu_bench_multirank.py."""
+    import json
+    import subprocess
+
+    import bench
+
+    seen = {}
+
+    def fake_call(cmd, env=None):
+        seen["cmd"], seen["env"] = cmd, env
+        return 0
+
+    monkeypatch.setattr(subprocess, "call", fake_call)
+    argv = ["--gpus", "2", "--config", "c5", "--m", "4096", "--backend", "gloo", "--comm", "torch"]
+    monkeypatch.setattr(sys, "argv", ["bench.py"] + argv)
+    assert bench.launch_ranks(2) == 0
+    cmd = seen["cmd"]
+    assert cmd[1:3] == ["-m", "torch.distributed.run"]
+    assert "--nnodes=1" in cmd and "--nproc-per-node=2" in cmd
+    assert cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert any(c.startswith("--master-port=") for c in cmd)
+    assert cmd[-1].endswith("bench.py")
+    assert json.loads(seen["env"]["RSVD_BENCH_ARGV"]) == argv
