@@ -761,7 +761,7 @@ __device__ __forceinline__ double rsqrt_nr(double d) {
 // (e_j[k] - acc[k]) / D[k][k], and each broadcast D[k][i] feeds both the factor update and
 // acc[i] += D[k][i] Y[k][j] -- one readlane per element for both.  Writes the R and R^-1 diagonal
 // blocks (global), D^-1 (Di, LDS, row-major), the breakdown rows (bad) and flags.
-__device__ __forceinline__ void chol_diag16_fast(double (&col)[16], int p16, int l, int LP, double tol,
+__device__ __forceinline__ __attribute__((unused)) void chol_diag16_fast(double (&col)[16], int p16, int l, int LP, double tol,
                                                  const double* d0, double* Di, int* bad, double* R, double* Rinv,
                                                  int* colflag, int* flag, int lane) {
     const int j = lane & 15;
