@@ -84,6 +84,24 @@ static void bench_pg() {
     }
 }
 
+static void bench_psplit() {  // the split panel product (panel_split_kernel), C3 / C4 / C5 m-side shapes
+    for (int LP : {128, 256, 512}) {
+        const int64_t rows = LP == 128 ? (1 << 20) : (LP == 256 ? 65536 : 131072);
+        float* In = dev_random<float>((size_t)rows * LP);
+        float* Out;
+        bf16_t *hi, *lo, *ms;
+        CK(hipMalloc(&Out, (size_t)rows * LP * 4));
+        CK(hipMalloc(&hi, (size_t)rows * LP * 2));
+        CK(hipMalloc(&lo, (size_t)rows * LP * 2));
+        CK(hipMalloc(&ms, (size_t)3 * LP * LP * 2));
+        float* M = dev_random<float>((size_t)LP * LP, 0.1f);
+        const double gb = (double)rows * LP * (4 + 4 + 2 + 2) / 1e9;
+        double t = time_us([&] { CK(launch_panel_gemm<float>(In, rows, LP, M, 1, Out, 0, 0, hi, lo, nullptr, S, ms)); });
+        printf("panel_split rows=%ld LP=%d: %.1f us (%.0f GB/s of In + Out + hi + lo)\n", (long)rows, LP, t, gb / t * 1e6);
+        CK(hipFree(In)); CK(hipFree(Out)); CK(hipFree(hi)); CK(hipFree(lo)); CK(hipFree(ms)); CK(hipFree(M));
+    }
+}
+
 static void bench_gram() {
     for (int LP : {128, 256, 512}) {
         const int64_t rows = LP == 128 ? (1 << 20) : (LP == 256 ? 65536 : 131072);
@@ -733,6 +751,7 @@ int main(int argc, char** argv) {
     if (what == "all" || what == "gram") bench_gram();
     if (what == "all" || what == "chol") bench_chol();
     if (what == "gsplit") bench_gsplit();
+    if (what == "psplit") bench_psplit();
     if (what == "all" || what == "jac") bench_jac();
     if (what == "all" || what == "proj") bench_proj();
     if (what == "proj4") bench_proj(true);
