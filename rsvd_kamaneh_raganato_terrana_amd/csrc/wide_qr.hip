@@ -1794,8 +1794,46 @@ __device__ __forceinline__ double round_sig(double x, int fp8) {
     return y;
 }
 
+// One thread per PAIR of stream elements (e, e + 1) = rows (i, i + 1) of column c (n even, i even):
+// the two share the Philox block, log and square root of gauss_elem -- the same operations, so the
+// values are bit-identical to gauss_elem's (cos for the even element, sin for the odd one); an odd n
+// falls back to one element per thread.  C4's 65536 x 256 Omega: half the Philox / log / sqrt work.
+__device__ __forceinline__ void gauss_pair(uint64_t e, uint64_t seed, double& g0, double& g1) {
+    uint32_t x[4];
+    philox4x32_10(e >> 1, seed, x);
+    const double two_m53 = 1.1102230246251565404e-16;
+    const double u1 = ((double)(((uint64_t)(x[0] >> 5) << 26) | (x[1] >> 6)) + 0.5) * two_m53;
+    const double u2 = ((double)(((uint64_t)(x[2] >> 5) << 26) | (x[3] >> 6)) + 0.5) * two_m53;
+    const double rr = sqrt(-2.0 * log(u1));
+    const double th = 6.283185307179586476925286766559 * u2;
+    g0 = rr * cos(th);
+    g1 = rr * sin(th);
+}
+
 __global__ void omega_lowp_kernel(bf16_t* __restrict__ panel, int64_t n, int l, int LP, uint64_t seed, int fp8,
                                   float* __restrict__ f) {
+    if ((n & 1) == 0) {
+        const int64_t total = (n >> 1) * LP;  // (row pair, column)
+        for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total;
+             e += (int64_t)gridDim.x * blockDim.x) {
+            const int64_t i = 2 * (e / LP);
+            const int c = (int)(e % LP);
+            float v0 = 0.f, v1 = 0.f;
+            if (c < l) {
+                double g0, g1;
+                gauss_pair((uint64_t)(i + n * (int64_t)c), seed, g0, g1);  // even stream index
+                v0 = (float)round_sig(g0, fp8);
+                v1 = (float)round_sig(g1, fp8);
+                if (f) {
+                    f[i + n * (int64_t)c] = v0;
+                    f[i + 1 + n * (int64_t)c] = v1;
+                }
+            }
+            panel[i * LP + c] = (bf16_t)(__float_as_uint(v0) >> 16);  // exact: <= 8 significant bits
+            panel[(i + 1) * LP + c] = (bf16_t)(__float_as_uint(v1) >> 16);
+        }
+        return;
+    }
     const int64_t total = n * LP;
     for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
         const int64_t i = e / LP;
