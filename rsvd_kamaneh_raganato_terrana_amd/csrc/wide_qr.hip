@@ -493,7 +493,7 @@ __device__ __forceinline__ int gs4_group(int ty, int lg) {
 
 __global__ __launch_bounds__(GramSplit4::THREADS) void gram_split4_kernel(const float* __restrict__ P, int64_t rows,
                                                                          int64_t rpc, int nchunk,
-                                                                         double* __restrict__ slabs, int ablate) {
+                                                                         double* __restrict__ slabs) {
     typedef GramSplit4 G;
     constexpr int TG = G::TG, LPT = G::LPT;
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
@@ -609,7 +609,7 @@ __global__ __launch_bounds__(GramSplit4::THREADS) void gram_split4_kernel(const 
         // iteration of step r0: stage step r0 + 32 into the other buffer (its last readers passed the
         // previous barrier) from the set loaded two iterations ago, then reload that set with r0 + 96
         auto iter = [&](Regs& reg, int64_t r0, int b) {
-            if (r0 + 32 < end && !(ablate & 2)) {
+            if (r0 + 32 < end) {
                 stage(reg, smem_raw + (b ^ 1) * G::STEP);
                 if (r0 + 96 < end) load(reg, r0 + 96);
             }
@@ -629,7 +629,7 @@ __global__ __launch_bounds__(GramSplit4::THREADS) void gram_split4_kernel(const 
     int buf = 0;
     for (int64_t r0 = beg; r0 < end; r0 += 32) {
         const char* img = smem_raw + buf * G::STEP;
-        if (active && !(ablate & 1)) {
+        if (active) {
             bf16x8s fa[TG][3];
 #pragma unroll
             for (int i = 0; i < TG; ++i)
@@ -1975,12 +1975,8 @@ hipError_t launch_gram_split(const float* P, int64_t rows, int LP, const GramPla
         int64_t rpc = (rows + ch - 1) / ch;
         rpc = (rpc + 31) / 32 * 32;
         nchunk = (int)((rows + rpc - 1) / rpc);
-        static const int abl = [] {  // lab only: bit 0 skips the MFMAs, bit 1 the staging
-            const char* e = std::getenv("RSVD_GSPLIT4_ABLATE");
-            return e ? std::atoi(e) : 0;
-        }();
         hipLaunchKernelGGL(gram_split4_kernel, dim3((nchunk + 7) / 8 * 8 * GramSplit4::TYPES),
-                           dim3(GramSplit4::THREADS), GramSplit4::LDS, s, P, rows, rpc, nchunk, slabs, abl);
+                           dim3(GramSplit4::THREADS), GramSplit4::LDS, s, P, rows, rpc, nchunk, slabs);
     } else if (LP == 512) {
         go(std::integral_constant<int, 512>{});
     }
