@@ -452,7 +452,13 @@ struct WideEngine {
             RSVD_CK(launch_gram_wide<T>(Xn + c0 * L.LP, Zn + c0 * L.LP, L.nc, L.LP, L.gxc, gslab, R1, nullptr, s));
             RSVD_TRY(allreduce(R1, (int64_t)L.LP * L.LP, RSVD_F64));
         } else {
-            RSVD_CK(launch_gram_wide<T>(Xn, Zn, L.n, L.LP, L.gx, gslab, R1, nullptr, s));  // R = Q_B^T B^T
+            // R = Q_B^T B^T: fp32 panels of bf16 / e4m3 A at LP = 256 by the three-piece bf16 split (the
+            // entries to ~1e-8 of |Q_B| |B^T|, as the split Grams; RSVD_GRAM_SPLIT=0: fp64 MFMA)
+            if (split_gram && L.LP == 256)
+                RSVD_CK(launch_gram_split_cross(reinterpret_cast<const float*>(Xn), reinterpret_cast<const float*>(Zn),
+                                                L.n, L.LP, L.gx, gslab, R1, s));
+            else
+                RSVD_CK(launch_gram_wide<T>(Xn, Zn, L.n, L.LP, L.gx, gslab, R1, nullptr, s));
         }
         // Inf / NaN in A reach R through B^T = A^T Q whatever the orthonormalisations did with them
         RSVD_CK(launch_check_finite<double>(R1, L.LP * L.LP, h->dflags + kFlagNonFinite, s));

@@ -674,6 +674,153 @@ __global__ __launch_bounds__(GramSplit4::THREADS) void gram_split4_kernel(const 
         }
 }
 
+// Cross Gram R = X^T Y of two fp32 panels at LP = 256 by the same three-piece bf16 split (round 4:
+// R = Q_B^T B^T, the fp64-MFMA gram_wide_kernel<float, true> took 256 us at C4 for 8.6 GFLOP).  Four
+// workgroup types per row chunk, type g the 64 columns of X's group g against all 256 of Y: a step
+// stages 64 + 256 columns (octet units as gram_split4_kernel, 60 KB, double-buffered); wave w takes
+// X tiles 2 (w & 1) .. + 1 of the group and Y tiles 4 (w >> 1) .. + 3 -- 8 tile pairs, six MFMAs
+// each.  Partial 32 x 32 blocks go to the cross slab layout gram_reduce_kernel sums (blk = a nb + b).
+struct GramSplitX {
+    static constexpr int LP = 256, NB = 8, NBLK = NB * NB, WAVES = 8, THREADS = 64 * WAVES;
+    static constexpr int XC = 64, YC = 256;               // staged columns of X (one group) and Y
+    static constexpr int XIMG = XC * 64, YIMG = YC * 64;  // bytes per piece image (32 rows bf16 per column)
+    static constexpr int STEP = 3 * (XIMG + YIMG);        // 60 KB
+    static constexpr int NU = 4 * (XC + YC);              // 8-row x 1-column units per step
+    static constexpr int LPT = (NU + THREADS - 1) / THREADS;
+};
+
+__global__ __launch_bounds__(GramSplitX::THREADS) void gram_split_cross_kernel(const float* __restrict__ X,
+                                                                              const float* __restrict__ Y,
+                                                                              int64_t rows, int64_t rpc, int nchunk,
+                                                                              double* __restrict__ slabs) {
+    typedef GramSplitX G;
+    constexpr int LPT = G::LPT;
+    extern __shared__ __attribute__((aligned(16))) char smem_raw[];
+    const int tid = threadIdx.x, lane = tid & 63, r = lane & 15, h = lane >> 4;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int v = blockIdx.x >> 3;  // a chunk's four types are 8 apart: one XCD
+    const int gx = v & 3;
+    const int chunk = ((v >> 2) << 3) | (blockIdx.x & 7);
+    if (chunk >= nchunk) return;
+    const int64_t beg = (int64_t)chunk * rpc;
+    const int64_t end = (beg + rpc < rows) ? beg + rpc : rows;
+    const int xt0 = 2 * (w & 1), yt0 = 4 * (w >> 1);  // local X tiles (of the group), Y tiles
+    f32x4 acc[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // unit u: units [0, 4 XC) are X's (octet u / XC of local column u % XC), the rest Y's
+    int oct[LPT], coff[LPT], loff[LPT];
+    bool isx[LPT];
+#pragma unroll
+    for (int t = 0; t < LPT; ++t) {
+        const int u = tid + G::THREADS * t;
+        const bool xu = u < 4 * G::XC;
+        const int uu = xu ? u : u - 4 * G::XC;
+        const int nc = xu ? G::XC : G::YC;
+        const int oc = uu / nc, c = uu - oc * nc;
+        isx[t] = xu;
+        oct[t] = 8 * oc;
+        coff[t] = xu ? 64 * gx + c : c;
+        loff[t] = (u < G::NU) ? (xu ? 0 : 3 * G::XIMG) + c * 64 + 16 * (oc ^ ((c >> 1) & 3)) : -1;
+    }
+    float reg[LPT][8];
+    auto load = [&](int64_t r0) {
+        const bool full = r0 + 32 <= end;
+#pragma unroll
+        for (int t = 0; t < LPT; ++t) {
+            if (tid + G::THREADS * t - lane >= G::NU) break;  // wave-uniform (NU, THREADS multiples of 64)
+            const float* base = isx[t] ? X : Y;
+            const int64_t row = r0 + oct[t];
+            if (full) {
+                const float* src = base + row * G::LP + coff[t];
+#pragma unroll
+                for (int q = 0; q < 8; ++q) reg[t][q] = src[q * G::LP];
+            } else {  // the chunk's partial last step: rows clamped and zeroed
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const int64_t rr = row + q < end ? row + q : end - 1;
+                    const float x = base[rr * G::LP + coff[t]];
+                    reg[t][q] = row + q < end ? x : 0.f;
+                }
+            }
+        }
+    };
+    auto stage = [&](char* img) {
+#pragma unroll
+        for (int t = 0; t < LPT; ++t) {
+            if (loff[t] < 0) break;
+            uint32_t pw[3][4];
+#pragma unroll
+            for (int q = 0; q < 8; q += 2) {
+                const float a = reg[t][q], b = reg[t][q + 1];
+                const uint32_t ph = cvt_pk_bf16(a, b);
+                const float ra = a - __uint_as_float(ph << 16), rb = b - __uint_as_float(ph & 0xffff0000u);
+                const uint32_t pm = cvt_pk_bf16(ra, rb);
+                const float ta = ra - __uint_as_float(pm << 16), tb = rb - __uint_as_float(pm & 0xffff0000u);
+                pw[0][q >> 1] = ph;
+                pw[1][q >> 1] = pm;
+                pw[2][q >> 1] = cvt_pk_bf16(ta, tb);
+            }
+            const int pstride = isx[t] ? G::XIMG : G::YIMG;
+#pragma unroll
+            for (int x = 0; x < 3; ++x)
+                *reinterpret_cast<uint4*>(img + loff[t] + x * pstride) = make_uint4(pw[x][0], pw[x][1], pw[x][2], pw[x][3]);
+        }
+    };
+    const uint32_t lo = (uint32_t)(r * 64 + 16 * (h ^ ((r >> 1) & 3)));
+    if (beg < end) {
+        load(beg);
+        stage(smem_raw);
+        if (beg + 32 < end) load(beg + 32);
+    }
+    __syncthreads();
+    int buf = 0;
+    for (int64_t r0 = beg; r0 < end; r0 += 32) {
+        const char* img = smem_raw + buf * G::STEP;
+        bf16x8s fa[2][3];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int x = 0; x < 3; ++x)
+                fa[i][x] = *reinterpret_cast<const bf16x8s*>(img + x * G::XIMG + (xt0 + i) * 1024 + lo);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const char* yb = img + 3 * G::XIMG + (yt0 + j) * 1024 + lo;
+            const bf16x8s yh = *reinterpret_cast<const bf16x8s*>(yb), ym = *reinterpret_cast<const bf16x8s*>(yb + G::YIMG),
+                          yt = *reinterpret_cast<const bf16x8s*>(yb + 2 * G::YIMG);
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                f32x4 c = acc[i][j];
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][2], yh, c, 0, 0, 0);  // smallest terms first
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], yt, c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][1], ym, c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][1], yh, c, 0, 0, 0);
+                c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], ym, c, 0, 0, 0);
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i][0], yh, c, 0, 0, 0);
+            }
+        }
+        if (r0 + 32 < end) {
+            stage(smem_raw + (buf ^ 1) * G::STEP);
+            if (r0 + 64 < end) load(r0 + 64);
+        }
+        __syncthreads();
+        buf ^= 1;
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int ta = 4 * gx + xt0 + i, tb = yt0 + j;  // global 16-column tiles of X, Y
+            const int blk = (ta >> 1) * G::NB + (tb >> 1);
+            double* dst = slabs + ((int64_t)chunk * G::NBLK + blk) * 1024;
+#pragma unroll
+            for (int e = 0; e < 4; ++e)  // bf16 MFMA D: col = lane & 15, row = 4 h + e
+                dst[(16 * (ta & 1) + 4 * h + e) * 32 + 16 * (tb & 1) + r] = (double)acc[i][j][e];
+        }
+}
+
 __global__ void gram_reduce_kernel(const double* __restrict__ slabs, int nblk, int nchunk, int LP, int cross,
                                    double* __restrict__ G, const int* __restrict__ pred) {
     if (pred && *pred == 0) return;
@@ -1947,6 +2094,27 @@ hipError_t launch_gram_wide(const T* P, const T* P2, int64_t rows, int LP, const
 }
 
 bool gram_split_ok(int LP) { return LP == 128 || LP == 256 || LP == 512; }
+
+hipError_t launch_gram_split_cross(const float* X, const float* Y, int64_t rows, int LP, const GramPlan& gp,
+                                   double* slabs, double* G, hipStream_t s) {
+    if (LP != 256 || gp.blocks != GramSplitX::NBLK) return hipErrorInvalidValue;
+    // >= 256 rows per chunk, at most the plan's chunk count (its slabs), ~64 chunks x 4 types = 256 CUs
+    int64_t ch = (rows + 255) / 256;
+    if (ch > 64) ch = 64;
+    if (ch > gp.chunks) ch = gp.chunks;
+    if (ch < 1) ch = 1;
+    int64_t rpc = (rows + ch - 1) / ch;
+    rpc = (rpc + 31) / 32 * 32;
+    const int nchunk = (int)((rows + rpc - 1) / rpc);
+    hipLaunchKernelGGL(gram_split_cross_kernel, dim3((nchunk + 7) / 8 * 8 * 4), dim3(GramSplitX::THREADS),
+                       2 * GramSplitX::STEP, s, X, Y, rows, rpc, nchunk, slabs);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const int64_t tot = (int64_t)gp.blocks * 1024;
+    hipLaunchKernelGGL(gram_reduce_kernel, dim3((int)((tot + 255) / 256)), dim3(256), 0, s, slabs, gp.blocks, nchunk,
+                       LP, 1, G, (const int*)nullptr);
+    return hipGetLastError();
+}
 
 hipError_t launch_gram_split(const float* P, int64_t rows, int LP, const GramPlan& gp, double* slabs, double* G,
                              hipStream_t s) {

@@ -161,6 +161,32 @@ static void bench_gsplit() {  // the split Gram (bf16 MFMA) against the fp64 Gra
     }
 }
 
+static void bench_gcross() {  // R = X^T Y by the split (LP = 256) against the fp64 cross Gram
+    const int LP = 256;
+    const int64_t rows = 65536;
+    float* X = dev_random<float>((size_t)rows * LP, 1.0f, 1);
+    float* Y = dev_random<float>((size_t)rows * LP, 1.0f, 2);
+    GramPlan gp = plan_gram_wide(rows, LP, 1);
+    double *slabs, *G, *G64;
+    CK(hipMalloc(&slabs, (size_t)gp.blocks * gp.chunks * 1024 * 8));
+    CK(hipMalloc(&G, (size_t)LP * LP * 8));
+    CK(hipMalloc(&G64, (size_t)LP * LP * 8));
+    double t = time_us([&] { CK(launch_gram_split_cross(X, Y, rows, LP, gp, slabs, G, S)); });
+    double t64 = time_us([&] { CK(launch_gram_wide<float>(X, Y, rows, LP, gp, slabs, G64, nullptr, S)); });
+    CK(hipStreamSynchronize(S));
+    std::vector<double> a((size_t)LP * LP), b((size_t)LP * LP);
+    CK(hipMemcpy(a.data(), G, a.size() * 8, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(b.data(), G64, b.size() * 8, hipMemcpyDeviceToHost));
+    double md = 0, mx = 0;
+    for (size_t i = 0; i < a.size(); ++i) {
+        md = std::max(md, std::fabs(a[i] - b[i]));
+        mx = std::max(mx, std::fabs(b[i]));
+    }
+    printf("gram_split_cross rows=%ld LP=%d: %.1f us (fp64 cross Gram %.1f us)  max|dR| %.3e  max|R| %.3e  (|X_i||Y_j| = %.0f)\n",
+           (long)rows, LP, t, t64, md, mx, (double)rows);
+    CK(hipFree(X)); CK(hipFree(Y)); CK(hipFree(slabs)); CK(hipFree(G)); CK(hipFree(G64));
+}
+
 static double* spd(int LP, int l) {  // G = X^T X + I with X random l x l
     std::vector<double> X((size_t)l * l), G((size_t)LP * LP, 0.0);
     std::mt19937 g(3);
@@ -751,6 +777,7 @@ int main(int argc, char** argv) {
     if (what == "all" || what == "gram") bench_gram();
     if (what == "all" || what == "chol") bench_chol();
     if (what == "gsplit") bench_gsplit();
+    if (what == "gcross") bench_gcross();
     if (what == "psplit") bench_psplit();
     if (what == "all" || what == "jac") bench_jac();
     if (what == "all" || what == "proj") bench_proj();
