@@ -55,6 +55,7 @@ constexpr int kEigMaxN = 512;
 // the whole Z squares that (its mixing of a pair i, j is ~eps |G| / |lam_i - lam_j|, so the eigen
 // residuals stay at eps |G|).
 constexpr double kClusterTol = 1e-12;
+constexpr double kE2Min = 1e-300;  // smallest squared off-diagonal in the Sturm counts (T scaled to |T| <= 1)
 // sync words (in the block-Jacobi sync block, past its own 384): hand-off counter, abort
 constexpr int kTriCtr = 448, kTriAbort = 449;
 
@@ -521,8 +522,11 @@ __device__ __forceinline__ int sturm_count(const double* d, const double* e2, in
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
             if (u < m) {
-                double p2 = fma(dc[u], p1, -ec[u] * p0);
-                if (p2 == 0.0) p2 = p1 < 0.0 ? 1e-300 : -1e-300;
+                // no zero guard on the chain (it was a compare and two selects per step): an exact
+                // p_i = 0 reads as positive, and p_{i+1} = -e2_i p_{i-1} then has the sign the guard's
+                // +-tiny p_i would have led to, so the count over (p_{i-1}, p_i, p_{i+1}) is the same;
+                // e2 has no exact zeros (clamped to kE2Min below), so p_{i+1} != 0
+                const double p2 = fma(dc[u], p1, -ec[u] * p0);
                 c += (p2 < 0.0) != (p1 < 0.0);
                 p0 = p1;
                 p1 = p2;
@@ -563,7 +567,7 @@ __global__ __launch_bounds__(256) void tridiag_bisect_kernel(const double* __res
     for (int i = tid; i < kEigMaxN + 16; i += 256) {
         d[i] = i < n ? dg[i] * inv : 0.0;
         const double es = i + 1 < n ? eg[i] * inv : 0.0;
-        e2[i] = es * es;
+        e2[i] = i + 1 < n ? fmax(es * es, kE2Min) : 0.0;  // a split (e = 0) couples at 1e-300: |dlambda| <= 1e-150
     }
     if (blockIdx.x == 0 && tid == 0) tnorm[0] = nrm;
     __syncthreads();
