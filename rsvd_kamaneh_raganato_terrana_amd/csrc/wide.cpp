@@ -286,6 +286,7 @@ struct WideEngine {
     // fp64 Gram and factor run again.
     static constexpr double kSplitIllTol = 1e-7;
     bool split_gram = false;
+    int split_cross = 3;  // RSVD_GSPLIT_X bits: 1 the split cross Gram at LP = 256, 2 at LP = 512
     bool split_panel = false;  // panel products on the bf16 MFMA, three-piece split (RSVD_PANEL_SPLIT=0: fp32 MFMA)
     bf16_t* Ms = nullptr;
     bf16_t* ms() const { return split_panel ? Ms : nullptr; }
@@ -452,9 +453,9 @@ struct WideEngine {
             RSVD_CK(launch_gram_wide<T>(Xn + c0 * L.LP, Zn + c0 * L.LP, L.nc, L.LP, L.gxc, gslab, R1, nullptr, s));
             RSVD_TRY(allreduce(R1, (int64_t)L.LP * L.LP, RSVD_F64));
         } else {
-            // R = Q_B^T B^T: fp32 panels of bf16 / e4m3 A at LP = 256 by the three-piece bf16 split (the
-            // entries to ~1e-8 of |Q_B| |B^T|, as the split Grams; RSVD_GRAM_SPLIT=0: fp64 MFMA)
-            if (split_gram && L.LP == 256)
+            // R = Q_B^T B^T: fp32 panels of bf16 / e4m3 A at LP = 256 / 512 by the three-piece bf16 split
+            // (the entries to ~1e-8 of |Q_B| |B^T|, as the split Grams; RSVD_GRAM_SPLIT=0: fp64 MFMA)
+            if (split_gram && ((L.LP == 256 && (split_cross & 1)) || (L.LP == 512 && (split_cross & 2))))
                 RSVD_CK(launch_gram_split_cross(reinterpret_cast<const float*>(Xn), reinterpret_cast<const float*>(Zn),
                                                 L.n, L.LP, L.gx, gslab, R1, s));
             else
@@ -544,6 +545,11 @@ int wide_typed(rsvd_handle_t h, const rsvd_desc_t* d, const void* A, const void*
             return v ? std::atoi(v) : 3;
         }();
         E.chol2 = env2;
+        static const int envx = [] {
+            const char* v = std::getenv("RSVD_GSPLIT_X");
+            return v ? std::atoi(v) : 3;
+        }();
+        E.split_cross = envx;
         static const int env3 = [] {
             const char* v = std::getenv("RSVD_PANEL_SPLIT");
             return v ? std::atoi(v) : 1;

@@ -674,33 +674,38 @@ __global__ __launch_bounds__(GramSplit4::THREADS) void gram_split4_kernel(const 
         }
 }
 
-// Cross Gram R = X^T Y of two fp32 panels at LP = 256 by the same three-piece bf16 split (round 4:
-// R = Q_B^T B^T, the fp64-MFMA gram_wide_kernel<float, true> took 256 us at C4 for 8.6 GFLOP).  Four
-// workgroup types per row chunk, type g the 64 columns of X's group g against all 256 of Y: a step
-// stages 64 + 256 columns (octet units as gram_split4_kernel, 60 KB, double-buffered); wave w takes
-// X tiles 2 (w & 1) .. + 1 of the group and Y tiles 4 (w >> 1) .. + 3 -- 8 tile pairs, six MFMAs
-// each.  Partial 32 x 32 blocks go to the cross slab layout gram_reduce_kernel sums (blk = a nb + b).
-struct GramSplitX {
-    static constexpr int LP = 256, NB = 8, NBLK = NB * NB, WAVES = 8, THREADS = 64 * WAVES;
-    static constexpr int XC = 64, YC = 256;               // staged columns of X (one group) and Y
+// Cross Gram R = X^T Y of two fp32 panels at LP = 256 / 512 by the same three-piece bf16 split (round
+// 4: R = Q_B^T B^T, the fp64-MFMA gram_wide_kernel<float, true> took 237 us at C4 for 8.6 GFLOP).
+// Workgroup types per row chunk: the 64 columns of X's group gx against 256 columns (half gy) of Y
+// -- 4 types at LP = 256, 16 at LP = 512.  A step stages 64 + 256 columns (octet units as
+// gram_split4_kernel, 60 KB, double-buffered); wave w takes X tiles 2 (w & 1) .. + 1 of the group and
+// Y tiles 4 (w >> 1) .. + 3 of the half -- 8 tile pairs, six MFMAs each.  Partial 32 x 32 blocks go
+// to the cross slab layout gram_reduce_kernel sums (blk = a nb + b).
+template <int LP_> struct GramSplitX {
+    static constexpr int LP = LP_, NB = LP / 32, NBLK = NB * NB, WAVES = 8, THREADS = 64 * WAVES;
+    static constexpr int GXN = LP / 64, GYN = LP / 256, TYPES = GXN * GYN;
+    static constexpr int XC = 64, YC = 256;               // staged columns of X (one group) and Y (one half)
     static constexpr int XIMG = XC * 64, YIMG = YC * 64;  // bytes per piece image (32 rows bf16 per column)
     static constexpr int STEP = 3 * (XIMG + YIMG);        // 60 KB
     static constexpr int NU = 4 * (XC + YC);              // 8-row x 1-column units per step
     static constexpr int LPT = (NU + THREADS - 1) / THREADS;
 };
 
-__global__ __launch_bounds__(GramSplitX::THREADS) void gram_split_cross_kernel(const float* __restrict__ X,
-                                                                              const float* __restrict__ Y,
-                                                                              int64_t rows, int64_t rpc, int nchunk,
-                                                                              double* __restrict__ slabs) {
-    typedef GramSplitX G;
+template <int LP_>
+__global__ __launch_bounds__(GramSplitX<LP_>::THREADS) void gram_split_cross_kernel(const float* __restrict__ X,
+                                                                                   const float* __restrict__ Y,
+                                                                                   int64_t rows, int64_t rpc,
+                                                                                   int nchunk,
+                                                                                   double* __restrict__ slabs) {
+    typedef GramSplitX<LP_> G;
     constexpr int LPT = G::LPT;
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
     const int tid = threadIdx.x, lane = tid & 63, r = lane & 15, h = lane >> 4;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int v = blockIdx.x >> 3;  // a chunk's four types are 8 apart: one XCD
-    const int gx = v & 3;
-    const int chunk = ((v >> 2) << 3) | (blockIdx.x & 7);
+    const int v = blockIdx.x >> 3;  // a chunk's types are 8 apart in dispatch order: one XCD
+    const int ty = v % G::TYPES;
+    const int gx = ty % G::GXN, gy = ty / G::GXN;
+    const int chunk = ((v / G::TYPES) << 3) | (blockIdx.x & 7);
     if (chunk >= nchunk) return;
     const int64_t beg = (int64_t)chunk * rpc;
     const int64_t end = (beg + rpc < rows) ? beg + rpc : rows;
@@ -722,7 +727,7 @@ __global__ __launch_bounds__(GramSplitX::THREADS) void gram_split_cross_kernel(c
         const int oc = uu / nc, c = uu - oc * nc;
         isx[t] = xu;
         oct[t] = 8 * oc;
-        coff[t] = xu ? 64 * gx + c : c;
+        coff[t] = xu ? 64 * gx + c : 256 * gy + c;
         loff[t] = (u < G::NU) ? (xu ? 0 : 3 * G::XIMG) + c * 64 + 16 * (oc ^ ((c >> 1) & 3)) : -1;
     }
     float reg[LPT][8];
@@ -812,7 +817,7 @@ __global__ __launch_bounds__(GramSplitX::THREADS) void gram_split_cross_kernel(c
     for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const int ta = 4 * gx + xt0 + i, tb = yt0 + j;  // global 16-column tiles of X, Y
+            const int ta = 4 * gx + xt0 + i, tb = 16 * gy + yt0 + j;  // global 16-column tiles of X, Y
             const int blk = (ta >> 1) * G::NB + (tb >> 1);
             double* dst = slabs + ((int64_t)chunk * G::NBLK + blk) * 1024;
 #pragma unroll
@@ -2097,17 +2102,23 @@ bool gram_split_ok(int LP) { return LP == 128 || LP == 256 || LP == 512; }
 
 hipError_t launch_gram_split_cross(const float* X, const float* Y, int64_t rows, int LP, const GramPlan& gp,
                                    double* slabs, double* G, hipStream_t s) {
-    if (LP != 256 || gp.blocks != GramSplitX::NBLK) return hipErrorInvalidValue;
-    // >= 256 rows per chunk, at most the plan's chunk count (its slabs), ~64 chunks x 4 types = 256 CUs
+    if ((LP != 256 && LP != 512) || gp.blocks != (LP / 32) * (LP / 32)) return hipErrorInvalidValue;
+    // >= 256 rows per chunk, at most the plan's chunk count (its slabs), ~256 workgroups
+    const int types = LP == 256 ? GramSplitX<256>::TYPES : GramSplitX<512>::TYPES;
     int64_t ch = (rows + 255) / 256;
-    if (ch > 64) ch = 64;
+    if (ch > 256 / types) ch = 256 / types;
     if (ch > gp.chunks) ch = gp.chunks;
     if (ch < 1) ch = 1;
     int64_t rpc = (rows + ch - 1) / ch;
     rpc = (rpc + 31) / 32 * 32;
     const int nchunk = (int)((rows + rpc - 1) / rpc);
-    hipLaunchKernelGGL(gram_split_cross_kernel, dim3((nchunk + 7) / 8 * 8 * 4), dim3(GramSplitX::THREADS),
-                       2 * GramSplitX::STEP, s, X, Y, rows, rpc, nchunk, slabs);
+    const dim3 grid((unsigned)((nchunk + 7) / 8 * 8 * types));
+    if (LP == 256)
+        hipLaunchKernelGGL(gram_split_cross_kernel<256>, grid, dim3(GramSplitX<256>::THREADS), 2 * GramSplitX<256>::STEP,
+                           s, X, Y, rows, rpc, nchunk, slabs);
+    else
+        hipLaunchKernelGGL(gram_split_cross_kernel<512>, grid, dim3(GramSplitX<512>::THREADS), 2 * GramSplitX<512>::STEP,
+                           s, X, Y, rows, rpc, nchunk, slabs);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const int64_t tot = (int64_t)gp.blocks * 1024;

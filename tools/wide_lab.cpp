@@ -161,9 +161,9 @@ static void bench_gsplit() {  // the split Gram (bf16 MFMA) against the fp64 Gra
     }
 }
 
-static void bench_gcross() {  // R = X^T Y by the split (LP = 256) against the fp64 cross Gram
-    const int LP = 256;
-    const int64_t rows = 65536;
+static void bench_gcross() {  // R = X^T Y by the split (LP = 256 / 512) against the fp64 cross Gram
+  for (int LP : {256, 512}) {
+    const int64_t rows = LP == 256 ? 65536 : 8192;
     float* X = dev_random<float>((size_t)rows * LP, 1.0f, 1);
     float* Y = dev_random<float>((size_t)rows * LP, 1.0f, 2);
     GramPlan gp = plan_gram_wide(rows, LP, 1);
@@ -185,6 +185,7 @@ static void bench_gcross() {  // R = X^T Y by the split (LP = 256) against the f
     printf("gram_split_cross rows=%ld LP=%d: %.1f us (fp64 cross Gram %.1f us)  max|dR| %.3e  max|R| %.3e  (|X_i||Y_j| = %.0f)\n",
            (long)rows, LP, t, t64, md, mx, (double)rows);
     CK(hipFree(X)); CK(hipFree(Y)); CK(hipFree(slabs)); CK(hipFree(G)); CK(hipFree(G64));
+  }
 }
 
 static double* spd(int LP, int l) {  // G = X^T X + I with X random l x l
