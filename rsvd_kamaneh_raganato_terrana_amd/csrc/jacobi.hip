@@ -154,12 +154,15 @@ __global__ __launch_bounds__((JacobiShape<C, LP>::NTHR)) void small_svd_kernel(c
     C negl = C(0);
     __syncthreads();
     for (; sweeps < 40; ++sweeps) {
-        // exact squared norms at the start of every sweep (the rounds update them incrementally)
-        for (int c = tid; c < LP; c += nt) {
-            C s2 = C(0);
-            for (int i = 0; i < LP; ++i) s2 += X[c * CS + i] * X[c * CS + i];
-            nrm[c] = s2;
-        }
+        // exact squared norms at the start of every sweep (the rounds update them incrementally):
+        // all LP columns before sweep 0 (negl below reads them); later sweeps take them in round 0,
+        // whose pairs cover every live column, by the same DPP group sums as the dot products
+        if (sweeps == 0)
+            for (int c = tid; c < LP; c += nt) {
+                C s2 = C(0);
+                for (int i = 0; i < LP; ++i) s2 += X[c * CS + i] * X[c * CS + i];
+                nrm[c] = s2;
+            }
         if (tid == 0) {
             flags[0] = 0;
             flags[1] = 0;
@@ -197,7 +200,24 @@ __global__ __launch_bounds__((JacobiShape<C, LP>::NTHR)) void small_svd_kernel(c
                         jq[t + v] = dp[v];
                     }
                 }
-                const C a = nrm[p], b = nrm[q];
+                C a, b;
+                if (round == 0 && sweeps > 0) {
+                    C a0 = C(0), b0 = C(0);
+#pragma unroll
+                    for (int t = 0; t < CH; ++t) {
+                        a0 += xp[t] * xp[t];
+                        b0 += xq[t] * xq[t];
+                    }
+                    a = group_sum<TPP>(a0);
+                    b = group_sum<TPP>(b0);
+                    if (sub == 0) {  // kept when the pair does not rotate
+                        nrm[p] = a;
+                        nrm[q] = b;
+                    }
+                } else {
+                    a = nrm[p];
+                    b = nrm[q];
+                }
                 C g0 = C(0), g1 = C(0);
 #pragma unroll
                 for (int t = 0; t < CH; ++t) {
