@@ -316,12 +316,18 @@ __device__ __forceinline__ uint32_t cvt_pk_bf16(float a, float b) {
     return r;
 }
 
-template <int LP>
+// Loader groups (round 4): the NU units of a step are loaded by GSZ = NU / LPTG threads, LPTG units
+// each; NLG such groups take the steps round robin, so a group issues its next load NLG steps ahead
+// of the step it stages.  <1, 1> is the original one-step prefetch; at LP = 128 one step is 16 KB per
+// CU and the 1-step prefetch left the kernel waiting on HBM latency (205 us for a 2^20-row panel).
+template <int LP, int LPTG = GramSplit<LP>::LPT, int NLG = 1>
 __global__ __launch_bounds__(GramSplit<LP>::THREADS) void gram_split_kernel(const float* __restrict__ P, int64_t rows,
                                                                           int64_t rpc, int nchunk,
                                                                           double* __restrict__ slabs) {
     typedef GramSplit<LP> G;
-    constexpr int TG = G::TG, LPT = G::LPT;
+    constexpr int TG = G::TG, LPT = LPTG;
+    constexpr int GSZ = (G::NU + LPTG - 1) / LPTG;  // threads of one loader group
+    static_assert(NLG == 1 || (GSZ % 64 == 0 && NLG * GSZ <= G::THREADS), "loader groups");
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
     const int tid = threadIdx.x, lane = tid & 63, r = lane & 15, h = lane >> 4;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -354,7 +360,7 @@ __global__ __launch_bounds__(GramSplit<LP>::THREADS) void gram_split_kernel(cons
         const bool full = r0 + 32 <= end;
 #pragma unroll
         for (int t = 0; t < LPT; ++t) {
-            const int u = tid + G::THREADS * t;
+            const int u = (NLG == 1 ? tid : tid % GSZ) + (NLG == 1 ? G::THREADS : GSZ) * t;
             if (u - lane >= G::NU) break;
             const int64_t row = r0 + 4 * (u & 7);
             const int c = 4 * (u >> 3);
@@ -373,7 +379,7 @@ __global__ __launch_bounds__(GramSplit<LP>::THREADS) void gram_split_kernel(cons
     auto stage = [&](char* img) {
 #pragma unroll
         for (int t = 0; t < LPT; ++t) {
-            const int u = tid + G::THREADS * t;
+            const int u = (NLG == 1 ? tid : tid % GSZ) + (NLG == 1 ? G::THREADS : GSZ) * t;
             if (u >= G::NU) break;
             const int kr = 4 * (u & 7);
             const int c0 = 4 * (u >> 3);
@@ -410,13 +416,30 @@ __global__ __launch_bounds__(GramSplit<LP>::THREADS) void gram_split_kernel(cons
         return *reinterpret_cast<const bf16x8s*>(img + piece * G::IMG + t * 1024 + lo);
     };
     int buf = 0;
-    if (beg < end) load(beg);
+    // loader group of this wave (NLG > 1): it stages steps lg, lg + NLG, ... and loads NLG ahead
+    const int lg = NLG == 1 ? 0 : __builtin_amdgcn_readfirstlane(tid / GSZ);
+    if (NLG == 1) {
+        if (beg < end) load(beg);
+    } else if (lg < NLG && beg + 32 * lg < end) {
+        load(beg + 32 * lg);
+    }
+    int sm = 0;  // step index mod NLG
     for (int64_t r0 = beg; r0 < end; r0 += 32) {
         char* img = smem_raw + buf * G::STEP;
         if (G::NBUF == 1) __syncthreads();  // single buffer: the previous step's reads are done
-        stage(img);
-        __syncthreads();
-        if (r0 + 32 < end) load(r0 + 32);
+        if (NLG == 1) {
+            stage(img);
+            __syncthreads();
+            if (r0 + 32 < end) load(r0 + 32);
+        } else {
+            static_assert(NLG == 1 || G::NBUF == 2, "loader groups need two buffers");
+            if (sm == lg) {
+                stage(img);
+                if (r0 + 32 * NLG < end) load(r0 + 32 * NLG);
+            }
+            sm = sm + 1 == NLG ? 0 : sm + 1;
+            __syncthreads();
+        }
         bf16x8s fa[TG][3];
 #pragma unroll
         for (int i = 0; i < TG; ++i)
@@ -2134,6 +2157,22 @@ hipError_t launch_gram_split(const float* P, int64_t rows, int LP, const GramPla
         constexpr int L = decltype(lpc)::value;
         typedef GramSplit<L> GS;
         const int grid = GS::NH == 1 ? gp.chunks : (gp.chunks + 7) / 8 * 8 * GS::NH;
+        static const int lgv = [] {  // RSVD_GSPLIT_LG (LP = 128): 0 one-step prefetch, 1 two loader groups, 2 four
+            const char* e = std::getenv("RSVD_GSPLIT_LG");
+            return e ? std::atoi(e) : 1;
+        }();
+        if constexpr (L == 128) {
+            if (lgv == 1) {
+                hipLaunchKernelGGL((gram_split_kernel<L, 1, 2>), dim3(grid), dim3(GS::THREADS), GS::NBUF * GS::STEP, s,
+                                   P, rows, gp.rows_per_chunk, gp.chunks, slabs);
+                return;
+            }
+            if (lgv == 2) {
+                hipLaunchKernelGGL((gram_split_kernel<L, 2, 4>), dim3(grid), dim3(GS::THREADS), GS::NBUF * GS::STEP, s,
+                                   P, rows, gp.rows_per_chunk, gp.chunks, slabs);
+                return;
+            }
+        }
         hipLaunchKernelGGL(gram_split_kernel<L>, dim3(grid), dim3(GS::THREADS), GS::NBUF * GS::STEP, s, P, rows,
                            gp.rows_per_chunk, gp.chunks, slabs);
     };
