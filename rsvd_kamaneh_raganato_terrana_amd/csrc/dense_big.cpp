@@ -415,16 +415,18 @@ int big_rsvd_typed(rsvd_handle_t h, const rsvd_desc_t* d, const void* Av, const 
             h->err = "l > 512 on several ranks needs the all-reduce hook";
             return RSVD_ERR_COMM;
         }
-        const T mloc = (T)m;
-        RSVD_CK(hipMemcpyAsync(R, &mloc, sizeof(T), hipMemcpyHostToDevice, s));
-        if (h->allreduce(R, 1, tdt, (void*)s, h->ar_user) != 0) {
+        // (summed in fp64 -- exact for any row count -- in the S slot, written only at the end)
+        double* cnt = reinterpret_cast<double*>(b + L.off_S);
+        const double mloc = (double)m;
+        RSVD_CK(hipMemcpyAsync(cnt, &mloc, sizeof(double), hipMemcpyHostToDevice, s));
+        if (h->allreduce(cnt, 1, RSVD_F64, (void*)s, h->ar_user) != 0) {
             h->err = "all-reduce hook failed";
             return RSVD_ERR_COMM;
         }
-        T mg = 0;
-        RSVD_CK(hipMemcpyAsync(&mg, R, sizeof(T), hipMemcpyDeviceToHost, s));
+        double mg = 0;
+        RSVD_CK(hipMemcpyAsync(&mg, cnt, sizeof(double), hipMemcpyDeviceToHost, s));
         RSVD_CK(hipStreamSynchronize(s));
-        const int64_t m_global = (int64_t)(mg + (T)0.5);
+        const int64_t m_global = (int64_t)(mg + 0.5);
         Em.shard = true;
         Em.row_off = (int64_t)h->rank << 40;
         Em.rows_total = (int64_t)h->world << 40;
@@ -538,6 +540,10 @@ int big_rsvd_run(rsvd_handle_t h, const rsvd_desc_t* d, const void* A, const voi
     if (h->world > 1 && !h->allreduce) {
         h->err = "a row-sharded rSVD needs the all-reduce hook (rsvd_set_comm / rsvd_comm_init)";
         return RSVD_ERR_INVALID_ARG;
+    }
+    if (d->flags & RSVD_FLAG_FORCE_NSHARD) {  // (the n side past 512 columns is replicated, A^T Q all-reduced)
+        h->err = "RSVD_FLAG_FORCE_NSHARD: the sharded n-side path is built for l <= 512";
+        return RSVD_ERR_UNSUPPORTED;
     }
     if (!Qout && (d->method == RSVD_SVD_POWER || d->method == RSVD_SVD_POWER_IC)) {
         h->err = "SVDMethod::Power is built for l <= 512";

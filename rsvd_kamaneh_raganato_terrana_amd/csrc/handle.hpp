@@ -44,6 +44,12 @@ struct rsvd_handle_s {
 #define RSVD_CK(expr)                                                                         \
     do {                                                                                      \
         hipError_t _e = (expr);                                                               \
+        if (_e == hipErrorCooperativeLaunchTooLarge) {                                        \
+            /* a persistent grid the device cannot hold at once (launch_coresident) */        \
+            h->err = std::string(#expr) + ": persistent grid exceeds the device's co-resident " \
+                     "workgroup capacity (size not supported on this device)";                \
+            return RSVD_ERR_UNSUPPORTED;                                                      \
+        }                                                                                     \
         if (_e != hipSuccess) {                                                               \
             h->err = std::string(#expr) + ": " + hipGetErrorString(_e);                       \
             return RSVD_ERR_HIP;                                                              \

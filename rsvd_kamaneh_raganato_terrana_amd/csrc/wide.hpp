@@ -95,7 +95,9 @@ size_t chol_2level_scratch_doubles(int LP, int depth);
 bool gram_split_ok(int LP);
 hipError_t launch_gram_split(const float* P, int64_t rows, int LP, const GramPlan& gp, double* slabs, double* G,
                              hipStream_t s);
-// R = X^T Y of two fp32 panels by the same split (LP = 256 / 512; gp: the cross plan, plan_gram_wide(rows, LP, 1))
+// R = X^T Y of two fp32 panels by the same split (LP = 256 / 512; gp: the cross plan, plan_gram_wide(rows, LP, 1));
+// more than kSplitCrossRows rows per chunk fall back to the fp64 cross Gram (launch_gram_wide)
+constexpr int64_t kSplitCrossRows = 4096;
 hipError_t launch_gram_split_cross(const float* X, const float* Y, int64_t rows, int LP, const GramPlan& gp,
                                    double* slabs, double* G, hipStream_t s);
 // 1 (default): chol_reg_kernel for LP <= 128, chol_wide_kernel above; 0: chol_wide_kernel everywhere;

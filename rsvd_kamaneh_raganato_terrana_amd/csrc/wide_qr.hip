@@ -888,6 +888,78 @@ __global__ void gram_reduce_kernel(const double* __restrict__ slabs, int nblk, i
     if (!cross && a != b) G[(int64_t)cb * LP + ra] = s;
 }
 
+// The same sum with more parallelism per entry: one workgroup = 64 Gram entries x 4 chunk ranges
+// (wave k sums chunks [k n / 4, (k + 1) n / 4) with four interleaved partials, a wave's 64 entries
+// one 512-B load per chunk), the ranges combined in a fixed order -- deterministic, but a different
+// order than gram_reduce_kernel.  C3's LP = 128 Gram (10 blocks, 256 chunks) ran gram_reduce_kernel
+// on 40 workgroups; this gives it 160.  Default; RSVD_GRAM_REDUCE4=0 selects gram_reduce_kernel (A/B,
+// one box: C4 23.81 -> 23.68 ms, C5 19.15 -> 19.13, C3 5.65 -> 5.62; gpurun_out r5a).
+__global__ __launch_bounds__(256) void gram_reduce4_kernel(const double* __restrict__ slabs, int nblk, int nchunk,
+                                                           int LP, int cross, double* __restrict__ G,
+                                                           const int* __restrict__ pred) {
+    if (pred && *pred == 0) return;
+    __shared__ double part[4][64];
+    const int lane = threadIdx.x & 63, k = threadIdx.x >> 6;
+    const int64_t e = blockIdx.x * (int64_t)64 + lane;
+    bool ok = e < (int64_t)nblk * 1024;
+    const int blk = ok ? (int)(e / 1024) : 0, loc = (int)(e % 1024);
+    const int nb = (LP + 31) / 32;
+    int a, b;
+    if (cross) {
+        a = blk / nb;
+        b = blk % nb;
+    } else {
+        int rem = blk;
+        a = 0;
+        while (rem >= nb - a) {
+            rem -= nb - a;
+            ++a;
+        }
+        b = a + rem;
+    }
+    const int ra = 32 * a + loc / 32, cb = 32 * b + loc % 32;
+    ok = ok && ra < LP && cb < LP;
+    double sum = 0.0;
+    if (ok) {
+        const int64_t cs = (int64_t)nblk * 1024;
+        const double* src = slabs + (int64_t)blk * 1024 + loc;
+        const int c0 = (int)((int64_t)nchunk * k / 4), c1 = (int)((int64_t)nchunk * (k + 1) / 4);
+        double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+        int c = c0;
+        for (; c + 4 <= c1; c += 4) {
+            s0 += src[(c + 0) * cs];
+            s1 += src[(c + 1) * cs];
+            s2 += src[(c + 2) * cs];
+            s3 += src[(c + 3) * cs];
+        }
+        for (; c < c1; ++c) s0 += src[c * cs];
+        sum = (s0 + s1) + (s2 + s3);
+    }
+    part[k][lane] = sum;
+    __syncthreads();
+    if (k == 0 && ok) {
+        const double t = (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]);
+        G[(int64_t)ra * LP + cb] = t;
+        if (!cross && a != b) G[(int64_t)cb * LP + ra] = t;
+    }
+}
+
+hipError_t launch_gram_reduce(const double* slabs, int nblk, int nchunk, int LP, int cross, double* G, const int* pred,
+                              hipStream_t s) {
+    static const int v4 = [] {
+        const char* e = std::getenv("RSVD_GRAM_REDUCE4");
+        return e ? std::atoi(e) : 1;
+    }();
+    const int64_t tot = (int64_t)nblk * 1024;
+    if (v4)
+        hipLaunchKernelGGL(gram_reduce4_kernel, dim3((int)((tot + 63) / 64)), dim3(256), 0, s, slabs, nblk, nchunk, LP,
+                           cross, G, pred);
+    else
+        hipLaunchKernelGGL(gram_reduce_kernel, dim3((int)((tot + 255) / 256)), dim3(256), 0, s, slabs, nblk, nchunk,
+                           LP, cross, G, pred);
+    return hipGetLastError();
+}
+
 // ------------------------------------------------------------------------------------------------
 // Cholesky, one workgroup of kCholThreads threads.  W (work) holds the Gram being reduced (upper
 // block triangle only); R gets the factor's upper block triangle, Rinv the inverse diagonal blocks
@@ -2115,10 +2187,7 @@ hipError_t launch_gram_wide(const T* P, const T* P2, int64_t rows, int LP, const
                            gp.chunks, gp.rows_per_chunk, slabs, pred);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    const int64_t tot = (int64_t)gp.blocks * 1024;
-    hipLaunchKernelGGL(gram_reduce_kernel, dim3((int)((tot + 255) / 256)), dim3(256), 0, s, slabs, gp.blocks,
-                       gp.chunks, LP, P2 ? 1 : 0, G, pred);
-    return hipGetLastError();
+    return launch_gram_reduce(slabs, gp.blocks, gp.chunks, LP, P2 ? 1 : 0, G, pred, s);
 }
 
 bool gram_split_ok(int LP) { return LP == 128 || LP == 256 || LP == 512; }
@@ -2134,6 +2203,9 @@ hipError_t launch_gram_split_cross(const float* X, const float* Y, int64_t rows,
     if (ch < 1) ch = 1;
     int64_t rpc = (rows + ch - 1) / ch;
     rpc = (rpc + 31) / 32 * 32;
+    // each fp32 MFMA accumulator sums one chunk's rows; past kSplitCrossRows per chunk (n > 262144 at
+    // LP = 256, n > 65536 at LP = 512) its error would grow with n -- the fp64 cross Gram instead
+    if (rpc > kSplitCrossRows) return launch_gram_wide<float>(X, Y, rows, LP, gp, slabs, G, nullptr, s);
     const int nchunk = (int)((rows + rpc - 1) / rpc);
     const dim3 grid((unsigned)((nchunk + 7) / 8 * 8 * types));
     if (LP == 256)
@@ -2144,10 +2216,7 @@ hipError_t launch_gram_split_cross(const float* X, const float* Y, int64_t rows,
                            s, X, Y, rows, rpc, nchunk, slabs);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    const int64_t tot = (int64_t)gp.blocks * 1024;
-    hipLaunchKernelGGL(gram_reduce_kernel, dim3((int)((tot + 255) / 256)), dim3(256), 0, s, slabs, gp.blocks, nchunk,
-                       LP, 1, G, (const int*)nullptr);
-    return hipGetLastError();
+    return launch_gram_reduce(slabs, gp.blocks, nchunk, LP, 1, G, nullptr, s);
 }
 
 hipError_t launch_gram_split(const float* P, int64_t rows, int LP, const GramPlan& gp, double* slabs, double* G,
@@ -2200,10 +2269,7 @@ hipError_t launch_gram_split(const float* P, int64_t rows, int LP, const GramPla
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    const int64_t tot = (int64_t)gp.blocks * 1024;
-    hipLaunchKernelGGL(gram_reduce_kernel, dim3((int)((tot + 255) / 256)), dim3(256), 0, s, slabs, gp.blocks,
-                       nchunk, LP, 0, G, (const int*)nullptr);
-    return hipGetLastError();
+    return launch_gram_reduce(slabs, gp.blocks, nchunk, LP, 0, G, nullptr, s);
 }
 
 int chol_variant = 1;

@@ -616,8 +616,9 @@ __global__ __launch_bounds__(kBJThreads) void block_jacobi_kernel(const double* 
     BJ_T(0);
     int par = 0, sweeps = 0;
     bool done = false;
-    if (given && tol_chk2 > 0.0) {
+    if (given == 1 && tol_chk2 > 0.0) {
         // the given X may already be orthogonal to the tolerance: the global check first (slot 31)
+        // (given == 2: the check is skipped and the sweeps run -- RSVD_EIG_FORCE_POLISH, tests only)
         const double mx = slice_max_cos2(Xb, MR, LP, pr, g, G, w, lane, negl);
         if (tid == 0) lmax = 0ull;
         __syncthreads();
@@ -1007,6 +1008,14 @@ hipError_t bj_launch(const double* src, int64_t lds, int src_rowmajor, int mrv, 
     if (LP % 32 || LP < 64 || LP > 4096 || MR % 32 || MR < 32 || l > LP || mrv > MR) return hipErrorInvalidValue;
     G = block_jacobi_groups(MR, LP, G);
     if (G < 1) return hipErrorInvalidValue;
+    // the persistent grid (LP / 32 pair slots x G row-group members) must be co-resident: fewer
+    // members per pair when the device cannot hold it (LP = 4096: 128 x 4 workgroups of 512
+    // threads), and a refusal when even one member per pair does not fit
+    while (G > 1 && (int64_t)(LP / 32) * G > coresident_capacity(block_jacobi_kernel, kBJThreads,
+                                                                   block_jacobi_lds(MR / G)))
+        G = G / 2 >= 1 && block_jacobi_groups(MR, LP, G / 2) ? G / 2 : 1;
+    if ((int64_t)(LP / 32) * G > coresident_capacity(block_jacobi_kernel, kBJThreads, block_jacobi_lds(MR / G)))
+        return hipErrorCooperativeLaunchTooLarge;
     hipError_t e = hipMemsetAsync(sync, 0, kSyncWords * sizeof(unsigned), s);
     if (e != hipSuccess) return e;
     e = launch_coresident(block_jacobi_kernel, dim3(LP / 32 * G), dim3(kBJThreads), block_jacobi_lds(MR / G), s, src,
@@ -1037,8 +1046,14 @@ template <typename T>
 hipError_t launch_block_jacobi_given(int l, int LP, double* X, double* J, double* Uw, double* Vw, T* S, unsigned* sync,
                                      int* info, hipStream_t s, double tol_chk) {
     if (LP > 512) return hipErrorInvalidValue;
+    // RSVD_EIG_FORCE_POLISH=1 (tests): skip the orthogonality check, so the Jacobi polish of the
+    // eigensolver's X always runs -- the path a failed check takes
+    static const int force = [] {
+        const char* v = std::getenv("RSVD_EIG_FORCE_POLISH");
+        return v ? std::atoi(v) : 0;
+    }();
     return bj_launch<T>(nullptr, LP, 0, l, l, LP, LP, X, J, Uw, Vw, S, sync, info, s,
-                        tol_chk > 1e-9 ? 1e-8 : 1e-16, tol_chk, 0, 1);
+                        tol_chk > 1e-9 ? 1e-8 : 1e-16, tol_chk, 0, force ? 2 : 1);
 }
 template hipError_t launch_block_jacobi_given<float>(int, int, double*, double*, double*, double*, float*, unsigned*,
                                                      int*, hipStream_t, double);

@@ -58,6 +58,83 @@ def test_big_l_bf16_matches_oracle(engine):
     _check(U, S, V, Uo, So, Vo, 1e-4, 1e-4, 1e-3)
 
 
+def _known_svd_device(m, n, sig, seed):
+    """A = X diag(sig) Y^T with orthonormal X (m x k), Y (n x k) drawn on the GPU (torch QR, fp64):
+    the exact SVD is known by construction, so sizes the CPU oracle cannot finish (its Householder QR
+    and two-sided Jacobi on a 4096-wide B take hours) still get a known answer."""
+    torch = _torch()
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    k = sig.shape[0]
+    X = torch.linalg.qr(torch.randn(m, k, generator=g, device="cuda", dtype=torch.float64))[0]
+    Y = torch.linalg.qr(torch.randn(n, k, generator=g, device="cuda", dtype=torch.float64))[0]
+    A = (X * torch.from_numpy(sig).cuda()) @ Y.t()
+    return A, X, Y
+
+
+def _head_spectrum(n, head=64):
+    """64 leading singular values 10 % apart (their vectors are determined far below the fp32 bar),
+    then a smooth 0.997^i tail down to ~1e-6 of sigma_1 at i ~ 4300."""
+    h = 0.9 ** np.arange(head)
+    t = h[-1] * 0.997 ** np.arange(1, n - head + 1)
+    return np.concatenate([h, t])
+
+
+@pytest.mark.parametrize("m,n,l", [(2560, 2304, 2048), (4608, 4352, 4096)])
+def test_big_l_2048_4096_known_answer(engine, m, n, l):
+    """rSVD() at l = 2048 and l = 4096, the top of the advertised range (VERDICT r04 item 1;
+    src/rSVD.cpp:72 has no cap): f32 A with a known SVD (_known_svd_device), q = 1.  The sketch
+    captures all but a ~1e-6 tail, so S matches the known sigma to 1e-4 (relative Frobenius), the 64
+    well-separated leading singular vectors match X / Y to 1e-4, U and V are orthonormal, and
+    |A - U S V^T|_F / |A|_F is at the fp32 floor.  Exercises the l = 4096 block Jacobi small SVD on its
+    occupancy-capped cooperative grid (launch_coresident)."""
+    torch = _torch()
+    sig = _head_spectrum(n)
+    A64, X, Y = _known_svd_device(m, n, sig, seed=l)
+    A = A64.float().t().contiguous().t()
+    U, S, V = engine.rsvd(A, l, q=1, seed=l + 1)
+    torch.cuda.synchronize()
+    assert U.shape == (m, l) and S.shape == (l,) and V.shape == (n, l)
+    S64 = S.double().cpu().numpy()
+    assert np.all(np.diff(S64) <= 1e-6 * S64[0])
+    assert rel_fro(S64, sig[:l]) < 1e-4, rel_fro(S64, sig[:l])
+    Ud, Vd = U.double(), V.double()
+    h = 64
+    Xh, Yh = X[:, :h].cpu().numpy(), Y[:, :h].cpu().numpy()
+    eu = rel_fro(sign_align(Ud[:, :h].cpu().numpy(), Xh), Xh)
+    ev = rel_fro(sign_align(Vd[:, :h].cpu().numpy(), Yh), Yh)
+    assert eu < 1e-4 and ev < 1e-4, (eu, ev)
+    eye = torch.eye(l, dtype=torch.float64, device="cuda")
+    # fp32 factors: ~1e-7 per entry over l^2 entries
+    assert torch.linalg.norm(Ud.t() @ Ud - eye).item() < 1e-3 * l / 512
+    assert torch.linalg.norm(Vd.t() @ Vd - eye).item() < 1e-3 * l / 512
+    # the rank-l truncation itself leaves the tail past l (2.0e-5 at l = 2048, ~0 at 4096)
+    trunc = np.linalg.norm(sig[l:]) / np.linalg.norm(sig)
+    res = torch.linalg.norm(A.double() - (Ud * S.double()) @ Vd.t()) / torch.linalg.norm(A.double())
+    assert res.item() < trunc * 1.01 + 1e-5, (res.item(), trunc)
+
+
+def test_svd_jacobi_4096_columns_known_answer(engine):
+    """SVD<Jacobi> at min(m, n) = 4096 (SVD_class.hpp:100-180; INTEGRATION.md's advertised limit): the
+    block Jacobi on 128 column blocks, its persistent grid capped by the device's co-resident capacity.
+    fp64 A with a known SVD (0.999^i, relative gaps 1e-3): S to 1e-12, the leading 2048 vectors to 1e-8,
+    U S V^T = A to 4e-12 (fp64 sums over 4096 terms; 1.9e-12 measured)."""
+    torch = _torch()
+    m, n = 4200, 4096
+    sig = 0.999 ** np.arange(n)
+    A, X, Y = _known_svd_device(m, n, sig, seed=4096)
+    U, S, V = engine.svd(A.t().contiguous().t(), 0)
+    torch.cuda.synchronize()
+    assert U.shape == (m, n) and S.shape == (n,) and V.shape == (n, n)
+    S64 = S.cpu().numpy()
+    assert rel_fro(S64, sig) < 1e-12, rel_fro(S64, sig)
+    h = 2048
+    Xh, Yh = X[:, :h].cpu().numpy(), Y[:, :h].cpu().numpy()
+    assert rel_fro(sign_align(U[:, :h].cpu().numpy(), Xh), Xh) < 1e-8
+    assert rel_fro(sign_align(V[:, :h].cpu().numpy(), Yh), Yh) < 1e-8
+    res = torch.linalg.norm(A - (U * S) @ V.t()) / torch.linalg.norm(A)
+    assert res.item() < 4e-12, res.item()
+
+
 def test_big_l_range_finder_and_limits(engine):
     """intermediate_step at l = 520 spans the oracle's Q; Power and l > 4096 are refused."""
     m, n, l = 1200, 900, 520

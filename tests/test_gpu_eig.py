@@ -121,3 +121,105 @@ def test_eig_small_svd_e4m3_l512(engine):
     scale = float(np.abs(A32).max()) / 400.0
     res, ref, A, info = _run_bf16(engine, A32, l, 2, seed=19, dtype=torch.float8_e4m3fn, scale=scale)
     _check(res, ref, A, frac=0.25)
+
+
+@pytest.mark.parametrize("l", [193, 196])
+def test_eig_small_svd_phase_boundary(engine, l):
+    """l just past the one-workgroup tridiagonalisation (n <= 192): phase 1 runs
+    n - 193 steps (none at l = 193, three at 196) on four workgroups before the single-workgroup
+    phase 2 takes the trailing 192 rows -- the hand-off at its boundary."""
+    A32 = gapped_matrix(2600, 1800, 2 * l, decay=0.97, seed=l).astype(np.float32) * 10
+    res, ref, A, info = _run_bf16(engine, A32, l, 1, seed=l + 1)
+    _check(res, ref, A)
+    assert info["jacobi_sweeps"] == 0, info
+
+
+def test_eig_small_svd_f32_A(engine):
+    """fp32 A (the narrow projection kernels per 64-column group) into the same eigensolver small SVD:
+    its fp32 results take the eigensolver path too (wide.cpp, sizeof(T) == 4, 128 <= LP <= 512)."""
+    torch = _torch()
+    m, n, l = 2048, 1536, 256
+    A = gapped_matrix(m, n, 2 * l, decay=0.97, seed=9)
+    A32 = A.astype(np.float32)
+    Ad = _dev_colmajor(A32, torch.float32)
+    Om = oracle.generate_omega(n, l, 23)
+    Uo, So, Vo = oracle.rsvd(A32.astype(np.float64), l, q=2, Omega=Om)
+    U, S, V = engine.rsvd(Ad, l, q=2, omega=torch.from_numpy(Om))
+    torch.cuda.synchronize()
+    info = engine.info()
+    _check([x.cpu().double().numpy() for x in (U, S, V)], (Uo, So, Vo), A32.astype(np.float64))
+    assert info["jacobi_sweeps"] == 0, info
+
+
+_POLISH = r"""
+import os, sys, json
+import numpy as np
+sys.path.insert(0, {repo!r}); sys.path.insert(0, os.path.join({repo!r}, "tests"))
+import torch, oracle
+import rsvd_kamaneh_raganato_terrana_amd as R
+from conftest import gapped_matrix, rel_fro, sign_align
+eng = R.Engine(0)
+m, n, l = 2048, 1500, 256
+A32 = gapped_matrix(m, n, 2 * l, decay=0.97, seed=31).astype(np.float32) * 10
+Ad = torch.from_numpy(np.ascontiguousarray(A32.T)).cuda().to(torch.bfloat16).t()
+Ax = Ad.float().cpu().double().numpy()
+Om = eng.generate_omega(n, l, seed=17, dtype=torch.bfloat16).cpu().double().numpy()
+Uo, So, Vo = oracle.rsvd(Ax, l, q=1, Omega=Om)
+U, S, V = (x.cpu().double().numpy() for x in eng.rsvd(Ad, l, q=1, seed=17))
+k = l // 2
+out = dict(sweeps=eng.info()["jacobi_sweeps"], s=rel_fro(S, So),
+           u=rel_fro(sign_align(U[:, :k], Uo[:, :k]), Uo[:, :k]), v=rel_fro(sign_align(V[:, :k], Vo[:, :k]), Vo[:, :k]),
+           uo=float(np.linalg.norm(U.T @ U - np.eye(l))), vo=float(np.linalg.norm(V.T @ V - np.eye(l))))
+eng.close()
+print("RESULT " + json.dumps(out))
+"""
+
+
+def test_eig_small_svd_forced_polish():
+    """the block-Jacobi polish of the eigensolver's X -- what runs when the orthogonality
+    check fails (near-clusters the cluster tolerance does not catch).  RSVD_EIG_FORCE_POLISH=1 skips
+    the check (read once per process, so in a child process): the sweeps run on X = W V_w as given,
+    jacobi_sweeps > 0, and the results still match the oracle at 1e-4."""
+    import json
+    import subprocess
+
+    env = dict(os.environ, RSVD_EIG_FORCE_POLISH="1")
+    p = subprocess.run([sys.executable, "-c", _POLISH.format(repo=REPO)], env=env, capture_output=True, text=True,
+                       timeout=110)
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = [x for x in p.stdout.splitlines() if x.startswith("RESULT ")][-1]
+    r = json.loads(line[7:])
+    assert r["sweeps"] > 0, r
+    assert r["s"] < 1e-4 and r["u"] < 1e-4 and r["v"] < 1e-4, r
+    assert r["uo"] < 1e-4 and r["vo"] < 1e-4, r
+
+
+def test_eig_small_svd_small_sigma(engine):
+    """the eigensolver squares the condition number (G = W^T W), so a small
+    sigma_i carries an extra absolute error ~ eps_64 |W|^2 / sigma_i from G.  fp32 A with a graded
+    spectrum 0.93^i (sigma_255 / sigma_0 ~ 1e-8): every S_i below 1e-4 sigma_1 is checked against the
+    oracle with the absolute bound  |S_i - So_i| <= 1e-6 sigma_1 + 1e-13 sigma_1^2 / So_i  (the fp32
+    pipeline's noise on R, ~1e-7 sigma_1, plus 1e3 x the eigensolver's eps_64 sigma_1^2 / sigma_i).
+    On this spectrum the eigenvectors of the smallest sigma lose orthogonality past the check's 1e-6
+    (measured: 4 polish sweeps), so the check hands X to the block-Jacobi polish -- the designed
+    route; the bound holds for the result either way."""
+    torch = _torch()
+    m, n, l = 3000, 2000, 256
+    rng = np.random.default_rng(77)
+    X = np.linalg.qr(rng.standard_normal((m, 400)))[0]
+    Y = np.linalg.qr(rng.standard_normal((n, 400)))[0]
+    A32 = ((X * 0.93 ** np.arange(400)) @ Y.T).astype(np.float32)
+    Ax = A32.astype(np.float64)
+    Om = oracle.generate_omega(n, l, 5)
+    Uo, So, Vo = oracle.rsvd(Ax, l, q=2, Omega=Om)
+    U, S, V = engine.rsvd(_dev_colmajor(A32, torch.float32), l, q=2, omega=torch.from_numpy(Om))
+    torch.cuda.synchronize()
+    sweeps = engine.info()["jacobi_sweeps"]
+    S = S.cpu().double().numpy()
+    s1 = So[0]
+    small = So < 1e-4 * s1
+    assert small.sum() > 100, small.sum()
+    bound = 1e-6 * s1 + 1e-13 * s1 * s1 / np.maximum(So, 1e-300)
+    err = np.abs(S - So)
+    assert np.all(err[small] <= bound[small]), (err[small].max(), np.argmax(err[small] / bound[small]), sweeps)
+    assert rel_fro(S, So) < 1e-4
