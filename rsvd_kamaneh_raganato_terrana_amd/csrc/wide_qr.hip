@@ -16,6 +16,7 @@
 // reference's Householder Q.
 #include <algorithm>
 #include <cstdlib>
+#include <string>
 #include <utility>
 
 #include "common.hpp"
@@ -1141,8 +1142,122 @@ __device__ __forceinline__ void chol_diag16_dpp(double (&col)[16], int p16, int 
             if (badmask & (1 << k)) colflag[p16 + k] = 1;
     }
 }
-#ifndef RSVD_CHOL_DIAG
-#define RSVD_CHOL_DIAG chol_diag16_dpp
+// Round 5: the same factor with fewer instructions on the pivot loop.  One wave issues at most one
+// instruction per four cycles, and the DPP form above spent 1686 instructions per factor (974 VALU,
+// 712 SALU: s_nop hazards, exec-mask branches around the rsqrt and the D^-1 stores, per-pivot
+// breakdown tests) -- 7844 cycles.  Here:
+//  * the breakdown / finiteness tests leave the pivot loop: lane k keeps its pivot d_kk, and after
+//    the loop one vector test (lane j judges pivot j) and a ballot decide; a bad or padding pivot
+//    (rare: rank deficiency, l % 16) re-runs chol_diag16_dpp from the staged tile -- the only path
+//    that needs the unit-pivot substitutions;
+//  * rsqrt unconditional (no branch), the D^-1 rows stay in registers (lane j: row j of D^-1) and
+//    are stored once after the loop (LDS Di and the global R^-1 block), no per-pivot exec masks;
+//  * -col[K] is the DPP FMA's src1 negation modifier, and only the first DPP use of each pivot
+//    row carries the `s_nop 1` (its source was just written); the later ones read it again.
+// Same operations in the same order as chol_diag16_dpp on a pivot chain without breakdowns:
+// bit-identical R and R^-1 (tools/wide_lab chol checks it).
+template <int I>
+__device__ __forceinline__ void fmsub_nbcast_nop(double& acc, double x, double y) {  // acc -= x[lane I] * y, hazard-safe
+    asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, -%2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+                 : "+v"(acc)
+                 : "v"(x), "v"(y), "i"(I));
+}
+// (volatile: kept in program order, so every hazard-free use follows the s_nop'ed first use)
+template <int I>
+__device__ __forceinline__ void fmsub_nbcast(double& acc, double x, double y) {  // x written >= 2 instrs earlier
+    asm volatile("v_fmac_f64_dpp %0, %1, -%2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+                 : "+v"(acc)
+                 : "v"(x), "v"(y), "i"(I));
+}
+template <int I>
+__device__ __forceinline__ void fmadd_nbcast(double& acc, double x, double y) {
+    asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+                 : "+v"(acc)
+                 : "v"(x), "v"(y), "i"(I));
+}
+template <int K, int I>
+__device__ __forceinline__ void diag16v2_updates(double (&col)[16], double (&acc)[16], double ck, double yk) {
+    if constexpr (I < 16) {
+        if constexpr (I == K + 1) fmsub_nbcast_nop<I>(col[I], ck, ck);  // col[i] -= D[k][i] col[k]
+        else fmsub_nbcast<I>(col[I], ck, ck);
+        fmadd_nbcast<I>(acc[I], ck, yk);  // acc[i] += D[k][i] Y[k][j]
+        diag16v2_updates<K, I + 1>(col, acc, ck, yk);
+    }
+}
+// `careful` (uniform): the breakdown / padding tests of chol_diag16_dpp on every pivot; a unit pivot
+// (padding row or breakdown) is the same arithmetic on the substituted row e_k with d_kk = 1 (then
+// y = rk = 1, v = 0, exactly the unit-pivot values of the DPP form).
+template <int K>
+__device__ __forceinline__ void diag16v2_pivots(double (&col)[16], double (&acc)[16], double (&yrow)[16], int j,
+                                                double& dsave, bool careful, int p16, int l, double tol, double d0j,
+                                                int& badmask) {
+    if constexpr (K < 16) {
+        double dkk = nbcast_f64<K>(col[K]);
+        if (careful) {
+            const double d0k = nbcast_f64<K>(d0j);
+            const bool pad = p16 + K >= l;
+            const bool isbad = !pad && (!(dkk > tol * d0k) || !(d0k > 0.0) || !isfinite(dkk));
+            if (isbad) badmask |= 1 << K;
+            if (pad || isbad) {
+                dkk = 1.0;
+                col[K] = (j == K) ? 1.0 : 0.0;
+            }
+        }
+        dsave = (j == K) ? dkk : dsave;
+        const double y = rsqrt_nr(dkk);
+        const double rk = dkk * y;
+        const double v = col[K] * y;
+        col[K] = (j == K) ? rk : v;
+        const double yk = ((j == K ? 1.0 : 0.0) - acc[K]) * y;  // Y[k][j] = D^-1[j][k]
+        yrow[K] = yk;
+        diag16v2_updates<K, K + 1>(col, acc, col[K], yk);
+        diag16v2_pivots<K + 1>(col, acc, yrow, j, dsave, careful, p16, l, tol, d0j, badmask);
+    }
+}
+// src: the staged tile (LDS, [i][16] row-major: src[i * 16 + j] = T[i][j]).  Pass 0 runs without the
+// per-pivot tests; if a pivot then fails them (ballot) -- or the block has padding rows -- the same
+// unrolled body runs again from src with the tests on (pass 1).
+__device__ __forceinline__ void chol_diag16_v2(double (&col)[16], int p16, int l, int LP, double tol, const double* d0,
+                                               double* Di, int* bad, double* R, double* Rinv, int* colflag, int* flag,
+                                               int lane, const double* src) {
+    const int j = lane & 15;
+    const double d0j = d0[p16 + j];
+    double acc[16], yrow[16];
+    int badmask = 0;
+    for (int pass = p16 + 16 > l ? 1 : 0;; ++pass) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[i] = 0.0;
+        double dsave = 0.0;
+        diag16v2_pivots<0>(col, acc, yrow, j, dsave, pass != 0, p16, l, tol, d0j, badmask);
+        if (pass) break;
+        // lane j judges its own pivot (the test chol_diag16_dpp applies per pivot)
+        const bool isbad = !(dsave > tol * d0j) || !(d0j > 0.0) || !isfinite(dsave);
+        if (!__ballot(isbad && lane < 16)) break;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) col[i] = src[i * 16 + j];
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+        if (i > j) col[i] = 0.0;
+    if (lane < 16) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) R[(int64_t)(p16 + i) * LP + p16 + j] = col[i];
+#pragma unroll
+        for (int k = 0; k < 16; k += 2) {
+            const double2 v2 = make_double2(yrow[k], yrow[k + 1]);
+            *reinterpret_cast<double2*>(Di + j * 16 + k) = v2;
+            *reinterpret_cast<double2*>(Rinv + (int64_t)(p16 + j) * LP + p16 + k) = v2;
+        }
+        bad[lane] = (badmask >> lane) & 1;
+    }
+    if (lane == 0 && badmask) {
+        atomicAdd(flag, __popc(badmask));
+        for (int k = 0; k < 16; ++k)
+            if (badmask & (1 << k)) colflag[p16 + k] = 1;
+    }
+}
+#ifndef RSVD_CHOL_DIAG  // the register-resident factor's diagonal blocks
+#define RSVD_CHOL_DIAG chol_diag16_v2
 #endif
 
 // The split-Gram fallback test after a factor (off the pivot chain): ill = some valid pivot broke
@@ -1327,8 +1442,10 @@ __global__ __launch_bounds__(NT) void chol_wide_kernel(const double* __restrict_
                 for (int i = 0; i < 16; ++i) col[i] = Tsc[i * 16 + r];
                 __builtin_amdgcn_s_waitcnt(0xc07f);
                 __builtin_amdgcn_wave_barrier();
-                RSVD_CHOL_DIAG(col, 16 * b1, l, LP, tol, d0, Dd + (b1 & 1) * 256, bad + (b1 & 1) * 16, R, Rinv,
-                                 colflag, flag, lane);
+                // (the DPP form here: this factor overlaps the other waves' trailing updates, and the v2
+                // form's extra registers spilled in this kernel -- LP = 512 637 -> 809 us in the lab)
+                chol_diag16_dpp(col, 16 * b1, l, LP, tol, d0, Dd + (b1 & 1) * 256, bad + (b1 & 1) * 16, R, Rinv,
+                                colflag, flag, lane);
             } else if (p >= 0) {
                 // local tile t of the (nt2 x nt2) upper triangle; t = 0 is wave 0's
                 TriWalk tw(wv, nt2);
@@ -1492,7 +1609,7 @@ __global__ __launch_bounds__(64 * kCholRegWaves) void chol_reg_kernel(const doub
             __builtin_amdgcn_s_waitcnt(0xc07f);
             __builtin_amdgcn_wave_barrier();
             RSVD_CHOL_DIAG(col, p16, l, LP, tol, d0, Di + (p & 1) * 256, bad + (p & 1) * 16, R, Rinv,
-                            colflag, flag, lane);
+                           colflag, flag, lane, Tsc);
         }
         __syncthreads();
         if (p < 32) CHOL_TS(1 + 3 * p);
@@ -2567,10 +2684,11 @@ namespace {
 template <int V>
 __global__ __launch_bounds__(64) void diag_bench_kernel(const double* __restrict__ T, int reps, double* R, double* Rinv,
                                                         int* colflag, int* flag, long long* out) {
-    __shared__ double Di[256], d0[16];
+    __shared__ double Di[256], d0[16], Ts[256];
     __shared__ int bad[16];
     const int lane = threadIdx.x, r = lane & 15;
     if (lane < 16) d0[lane] = T[lane * 16 + lane];
+    for (int e = lane; e < 256; e += 64) Ts[e] = T[e];
     __syncthreads();
     double col0[16];
 #pragma unroll
@@ -2582,7 +2700,8 @@ __global__ __launch_bounds__(64) void diag_bench_kernel(const double* __restrict
 #pragma unroll
         for (int i = 0; i < 16; ++i) col[i] = col0[i] + sink * 1e-300;
         if constexpr (V == 0) chol_diag16_fast(col, 0, 16, 16, 1e-13, d0, Di, bad, R, Rinv, colflag, flag, lane);
-        else chol_diag16_dpp(col, 0, 16, 16, 1e-13, d0, Di, bad, R, Rinv, colflag, flag, lane);
+        else if constexpr (V == 1) chol_diag16_dpp(col, 0, 16, 16, 1e-13, d0, Di, bad, R, Rinv, colflag, flag, lane);
+        else chol_diag16_v2(col, 0, 16, 16, 1e-13, d0, Di, bad, R, Rinv, colflag, flag, lane, Ts);
         sink += col[15];
     }
     const long long t1 = __builtin_amdgcn_s_memtime();
@@ -2601,15 +2720,22 @@ void chol_diag_bench() {
     (void)hipMalloc(&Ri, 256 * 8);
     (void)hipMalloc(&cf, 64);
     (void)hipMalloc(&fl, 64);
-    (void)hipMalloc(&out, 16);
+    (void)hipMalloc(&out, 24);
     (void)hipMemcpy(T, h.data(), 256 * 8, hipMemcpyHostToDevice);
-    long long o[2];
+    long long o[3];
+    std::vector<double> r1(256), r2(256), i1(256), i2(256);
     for (int rep = 0; rep < 2; ++rep) {
         hipLaunchKernelGGL(diag_bench_kernel<0>, dim3(1), dim3(64), 0, 0, T, 256, R, Ri, cf, fl, out);
         hipLaunchKernelGGL(diag_bench_kernel<1>, dim3(1), dim3(64), 0, 0, T, 256, R, Ri, cf, fl, out);
-        (void)hipMemcpy(o, out, 16, hipMemcpyDeviceToHost);
+        (void)hipMemcpy(r1.data(), R, 256 * 8, hipMemcpyDeviceToHost);
+        (void)hipMemcpy(i1.data(), Ri, 256 * 8, hipMemcpyDeviceToHost);
+        hipLaunchKernelGGL(diag_bench_kernel<2>, dim3(1), dim3(64), 0, 0, T, 256, R, Ri, cf, fl, out);
+        (void)hipMemcpy(r2.data(), R, 256 * 8, hipMemcpyDeviceToHost);
+        (void)hipMemcpy(i2.data(), Ri, 256 * 8, hipMemcpyDeviceToHost);
+        (void)hipMemcpy(o, out, 24, hipMemcpyDeviceToHost);
     }
-    printf("  16x16 diagonal factor, one wave: readlane form %lld cycles, DPP form %lld cycles\n", o[0], o[1]);
+    printf("  16x16 diagonal factor, one wave: readlane form %lld cycles, DPP form %lld cycles, v2 %lld cycles "
+           "(v2 bit-identical to DPP: R %d, R^-1 %d)\n", o[0], o[1], o[2], (int)(r1 == r2), (int)(i1 == i2));
     (void)hipFree(T); (void)hipFree(R); (void)hipFree(Ri); (void)hipFree(cf); (void)hipFree(fl); (void)hipFree(out);
 }
 void chol_prof_dump(int LP) {
