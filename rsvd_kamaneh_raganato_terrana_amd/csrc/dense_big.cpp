@@ -329,7 +329,9 @@ struct BigLWs {
     size_t off_qm, off_qn, off_A32, off_Om, off_Y, off_Q, off_Z, off_X, off_R, off_R64, off_JX, off_JJ, off_Uw, off_Vw,
         off_U32, off_S, off_sync, off_om16, total;
     BigLWs(const rsvd_desc_t* d)
-        : qm(d->m, std::min<int64_t>(d->l, d->m)), qn(d->n, std::min<int64_t>(d->l, d->n)) {
+        // (the m-side basis has l columns even where a row shard holds fewer than l rows: its Grams and
+        // block projections are summed over the ranks)
+        : qm(d->m, d->l), qn(d->n, std::min<int64_t>(d->l, d->n)) {
         const int64_t m = d->m, n = d->n, l = d->l;
         MR = (int)rup(l, 32);
         LP = (int)rup(l, 32);
@@ -427,6 +429,10 @@ int big_rsvd_typed(rsvd_handle_t h, const rsvd_desc_t* d, const void* Av, const 
         RSVD_CK(hipMemcpyAsync(&mg, cnt, sizeof(double), hipMemcpyDeviceToHost, s));
         RSVD_CK(hipStreamSynchronize(s));
         const int64_t m_global = (int64_t)(mg + 0.5);
+        if (l > m_global) {  // (every rank sees the same count: all refuse)
+            h->err = "l > min(m, n) not supported (m: the global row count of the sharded A)";
+            return RSVD_ERR_UNSUPPORTED;
+        }
         Em.shard = true;
         Em.row_off = (int64_t)h->rank << 40;
         Em.rows_total = (int64_t)h->world << 40;

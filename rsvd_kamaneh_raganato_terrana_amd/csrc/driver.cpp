@@ -66,7 +66,10 @@ struct Layout {
 // A = a_scale * (stored A); 0 means 1 (rsvd_c.h)
 double a_scale_of(const rsvd_desc_t* d) { return d->a_scale != 0.0 ? d->a_scale : 1.0; }
 
-int check_desc_msg(const rsvd_desc_t* d, const char** err) {
+// world: the handle's rank count (0 = unknown, e.g. a workspace-size query).  On a row-sharded handle
+// d->m is this rank's share, which may hold fewer rows than l (src/rSVD.cpp:20-23 partitions the
+// global m): the engines then check l against the global row count themselves.
+int check_desc_msg(const rsvd_desc_t* d, const char** err, int world = 1) {
     if (!d) { *err = "null descriptor"; return RSVD_ERR_INVALID_ARG; }
     if (d->m <= 0 || d->n <= 0 || d->l <= 0 || d->q < 0 || d->lda < d->m) {
         *err = "invalid sizes (need m, n, l > 0, q >= 0, lda >= m)";
@@ -81,14 +84,14 @@ int check_desc_msg(const rsvd_desc_t* d, const char** err) {
         return RSVD_ERR_UNSUPPORTED;
     }
     if (d->l > kBigLMax) { *err = "l > 4096 not supported"; return RSVD_ERR_UNSUPPORTED; }
-    if (d->l > d->n || d->l > d->m) { *err = "l > min(m, n) not supported"; return RSVD_ERR_UNSUPPORTED; }
+    if (d->l > d->n || (world == 1 && d->l > d->m)) { *err = "l > min(m, n) not supported"; return RSVD_ERR_UNSUPPORTED; }
     if (!std::isfinite(d->a_scale)) { *err = "a_scale is not finite"; return RSVD_ERR_INVALID_ARG; }
     return RSVD_OK;
 }
 
 int check_desc(rsvd_handle_t h, const rsvd_desc_t* d) {
     const char* err = "";
-    const int st = check_desc_msg(d, &err);
+    const int st = check_desc_msg(d, &err, h->world);
     if (st != RSVD_OK) h->err = err;
     return st;
 }
@@ -519,7 +522,7 @@ int rsvd_set_collectives(rsvd_handle_t h, rsvd_collective_fn fn, void* user) {
 int rsvd_workspace_bytes(const rsvd_desc_t* d, size_t* bytes) {
     if (!d || !bytes) return RSVD_ERR_INVALID_ARG;
     const char* err = "";
-    RSVD_TRY(check_desc_msg(d, &err));
+    RSVD_TRY(check_desc_msg(d, &err, 0));
     if (d->l > 512) {  // dense_big.cpp
         *bytes = big_rsvd_workspace(d);
         return RSVD_OK;

@@ -89,9 +89,12 @@ def test_workspace_bytes_and_argument_checks(lib):
     assert lib.rsvd_workspace_bytes(ctypes.byref(_desc(dtype=_capi.F64)), ctypes.byref(nb64)) == 0
     assert nb64.value > nb.value
     # 1 = RSVD_ERR_INVALID_ARG, 2 = RSVD_ERR_UNSUPPORTED
-    for bad, code in ((dict(l=0), 1), (dict(q=-1), 1), (dict(lda=100), 1), (dict(l=4097), 2), (dict(m=10, l=16), 2),
+    for bad, code in ((dict(l=0), 1), (dict(q=-1), 1), (dict(lda=100), 1), (dict(l=4097), 2), (dict(n=10, l=16), 2),
                       (dict(dtype=7), 2), (dict(method=7), 2), (dict(flags=4), 1)):
         assert lib.rsvd_workspace_bytes(ctypes.byref(_desc(**bad)), ctypes.byref(nb)) == code, bad
+    # m < l is a valid row SHARD (the reference partitions the global m, src/rSVD.cpp:20-23): the size
+    # query accepts it; rsvd_run refuses it on a one-rank handle (tests/test_gpu_big_l.py)
+    assert lib.rsvd_workspace_bytes(ctypes.byref(_desc(m=10, lda=10, l=16)), ctypes.byref(nb)) == 0
     assert lib.rsvd_workspace_bytes(ctypes.byref(_desc(flags=_capi.FLAG_LOWP_INTERMEDIATES)), ctypes.byref(nb)) == 0
     # the wide engine (l > 64, bf16 / e4m3 A): l-wide panels, bf16 hi/lo copies, slabs -- O((m + n) l)
     for dt, l in ((_capi.F32, 128), (_capi.BF16, 256), (_capi.FP8_E4M3, 512), (_capi.F64, 100)):

@@ -136,7 +136,8 @@ def test_svd_jacobi_4096_columns_known_answer(engine):
 
 
 def test_big_l_range_finder_and_limits(engine):
-    """intermediate_step at l = 520 spans the oracle's Q; Power and l > 4096 are refused."""
+    """intermediate_step at l = 520 spans the oracle's Q; Power, l > 4096 and the forced n-side shard
+    past 512 are refused."""
     m, n, l = 1200, 900, 520
     A = gapped_matrix(m, n, 600, decay=0.98, seed=3)
     Om = oracle.generate_omega(n, l, 5)
@@ -152,3 +153,11 @@ def test_big_l_range_finder_and_limits(engine):
         engine.rsvd_host(A, l, q=1, omega=Om, method=SVDMethod.Power)
     with pytest.raises(RSVDError):
         engine.rsvd_host(gapped_matrix(5000, 4200, 300, decay=0.9, seed=1), 4100, q=0)
+    # the n-side sharded path is built for l <= 512; asking for it past 512 is refused,
+    # not silently ignored
+    torch = _torch()
+    with pytest.raises(RSVDError, match="FORCE_NSHARD"):
+        engine.rsvd(_dev_colmajor(A.astype(np.float32), torch.float32), l, q=1, force_nshard=True)
+    # l > m on a one-rank handle (m < l is only a valid row shard)
+    with pytest.raises(RSVDError, match="min"):
+        engine.rsvd(_dev_colmajor(A[:500].astype(np.float32), torch.float32), l, q=1)

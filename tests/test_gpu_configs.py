@@ -158,3 +158,31 @@ def test_split_gram_paths(engine, decay, l):
     U, S, V = engine.rsvd(Ad, l, q=2, seed=5)
     U, S, V = (x.cpu().double().numpy() for x in (U, S, V))
     _check(U, S, V, Uo, So, Vo, A_exact, 1e-4, 1e-3)
+
+
+@pytest.mark.parametrize("n,l", [(131072, 512), (393216, 256)])
+def test_split_cross_gram_long_n(engine, n, l):
+    """R = Q_B^T B^T on the split bf16 MFMA accumulates each row chunk in fp32; past 4096
+    rows per chunk (n > 65536 at LP = 512, n > 262144 at LP = 256) the engine takes the fp64 cross
+    Gram instead (launch_gram_split_cross).  bf16 A, 640 x n, rank-400 0.985^i spectrum: the leading
+    l/2 singular values against the exact SVD of the bf16 A (fp64 eigenvalues of A A^T, 640 x 640),
+    1e-4 relative Frobenius, and V orthonormal."""
+    import torch
+
+    m = 640
+    g = torch.Generator(device="cuda").manual_seed(n + l)
+    X = torch.linalg.qr(torch.randn(m, 400, generator=g, device="cuda", dtype=torch.float64))[0]
+    Y = torch.linalg.qr(torch.randn(n, 400, generator=g, device="cuda", dtype=torch.float64))[0]
+    sig = 0.985 ** torch.arange(400, device="cuda", dtype=torch.float64)
+    Ab = ((X * sig) @ Y.t()).to(torch.bfloat16)
+    Ad = Ab.t().contiguous().t()
+    A64 = Ab.double()
+    lam = torch.linalg.eigvalsh(A64 @ A64.t()).flip(0).clamp_min(0).sqrt().cpu().numpy()
+    del X, Y, A64
+    U, S, V = engine.rsvd(Ad, l, q=1, seed=9)
+    torch.cuda.synchronize()
+    k = l // 2
+    S = S.double().cpu().numpy()
+    assert rel_fro(S[:k], lam[:k]) < 1e-4, rel_fro(S[:k], lam[:k])
+    Vd = V.double()
+    assert torch.linalg.norm(Vd.t() @ Vd - torch.eye(l, dtype=torch.float64, device="cuda")).item() < 1e-3

@@ -212,3 +212,12 @@ def test_row_sharded_world2_l_past_512(case):
     row count in the CholeskyQR shift (it is all-reduced; world * local rows made the ranks' R factors
     differ and moved U by 1.7e-4).  Against the oracle, 1e-4 (measured ~1e-5 on the leading half)."""
     _check_world2(case, False)
+
+
+@pytest.mark.parametrize("case", [(1200, 1000, 768, 1, "f32"), (400, 600, 256, 1, "bf16")])
+def test_row_sharded_world2_shard_smaller_than_l(case):
+    """a row shard may hold fewer rows than l -- the reference partitions the GLOBAL m
+    (src/rSVD.cpp:20-23) and only needs l <= min(m, n) globally.  600 rows per rank at l = 768 (the
+    dense_big.cpp path: its m-side basis workspace is sized by l, not by the local rows) and 200 rows
+    per rank at l = 256 (the wide engine, n side sharded).  Against the oracle, 1e-4."""
+    _check_world2(case, case[2] <= 512)
