@@ -55,6 +55,7 @@ constexpr int kEigMaxN = 512;
 // the whole Z squares that (its mixing of a pair i, j is ~eps |G| / |lam_i - lam_j|, so the eigen
 // residuals stay at eps |G|).
 constexpr double kClusterTol = 1e-12;
+constexpr double kSturmPadD = 4.0;  // the padding steps' diagonal in sturm_count (scaled units)
 constexpr double kE2Min = 1e-300;  // smallest squared off-diagonal in the Sturm counts (T scaled to |T| <= 1)
 // sync words (in the block-Jacobi sync block, past its own 384): hand-off counter, abort
 constexpr int kTriCtr = 448, kTriAbort = 449;
@@ -494,7 +495,8 @@ __global__ __launch_bounds__(kEigThreads) void tridiag_kernel(const double* __re
 // with a power-of-two rescale every 8 steps (the ratios -- all the count uses -- are unchanged).
 // The chain is one dependent FMA per step; the LDS operands of the next 8 steps are read into
 // registers (ds_read_b128 pairs) while the current 8 run, so no step waits on an LDS round trip.
-// d[i], e2[i] must be readable (any value) up to index n + 8.
+// d[i] = kSturmPadD and e2[i - 1] = kE2Min for n <= i < n + 16 (padding steps that leave the count
+// unchanged: the loop runs whole chunks of 8 without a per-step bound test).
 __device__ __forceinline__ int sturm_count(const double* d, const double* e2, int n, double x) {
     double p0 = 1.0, p1 = d[0] - x;
     if (p1 == 0.0) p1 = -1e-300;
@@ -518,19 +520,18 @@ __device__ __forceinline__ int sturm_count(const double* d, const double* e2, in
             dn[u] = d[i0 + 8 + u];
             en[u] = e2[i0 + 7 + u];
         }
-        const int m = n - i0 < 8 ? n - i0 : 8;
+        // (whole chunks: the steps past n - 1 are padding, d = kSturmPadD and e2 = kE2Min, which
+        // keep the sign -- (kSturmPadD - x) > 2 for the scaled |x| <= 1.01 -- and so the count)
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-            if (u < m) {
-                // no zero guard on the chain (it was a compare and two selects per step): an exact
-                // p_i = 0 reads as positive, and p_{i+1} = -e2_i p_{i-1} then has the sign the guard's
-                // +-tiny p_i would have led to, so the count over (p_{i-1}, p_i, p_{i+1}) is the same;
-                // e2 has no exact zeros (clamped to kE2Min below), so p_{i+1} != 0
-                const double p2 = fma(dc[u], p1, -ec[u] * p0);
-                c += (p2 < 0.0) != (p1 < 0.0);
-                p0 = p1;
-                p1 = p2;
-            }
+            // no zero guard on the chain (it was a compare and two selects per step): an exact
+            // p_i = 0 reads as positive, and p_{i+1} = -e2_i p_{i-1} then has the sign the guard's
+            // +-tiny p_i would have led to, so the count over (p_{i-1}, p_i, p_{i+1}) is the same;
+            // e2 has no exact zeros (clamped to kE2Min below), so p_{i+1} != 0
+            const double p2 = fma(dc[u], p1, -ec[u] * p0);
+            c += (p2 < 0.0) != (p1 < 0.0);
+            p0 = p1;
+            p1 = p2;
         }
         const int ex = __builtin_amdgcn_frexp_exp(fmax(fabs(p0), fabs(p1)));
         p0 = __builtin_ldexp(p0, -ex);
@@ -565,9 +566,9 @@ __global__ __launch_bounds__(256) void tridiag_bisect_kernel(const double* __res
     const double nrm = fmax(fabs(lo), fabs(hi));
     const double inv = nrm > 0.0 ? 1.0 / nrm : 0.0;
     for (int i = tid; i < kEigMaxN + 16; i += 256) {
-        d[i] = i < n ? dg[i] * inv : 0.0;
+        d[i] = i < n ? dg[i] * inv : kSturmPadD;
         const double es = i + 1 < n ? eg[i] * inv : 0.0;
-        e2[i] = i + 1 < n ? fmax(es * es, kE2Min) : 0.0;  // a split (e = 0) couples at 1e-300: |dlambda| <= 1e-150
+        e2[i] = fmax(es * es, kE2Min);  // a split (e = 0) couples at 1e-300: |dlambda| <= 1e-150
     }
     if (blockIdx.x == 0 && tid == 0) tnorm[0] = nrm;
     __syncthreads();
