@@ -52,3 +52,51 @@ def test_bench_workload_matches_oracle(engine):
     assert eu < 1e-4 and ev < 1e-4, (k, eu, ev)
     assert np.linalg.norm(U.T @ U - np.eye(l)) < 1e-4
     assert np.linalg.norm(V.T @ V - np.eye(l)) < 1e-4
+
+
+def _pin(engine, cfg, m, n, l, q, dt):
+    """One bench family (bench.make_A, the bench's seed) at a size the fp64 oracle finishes in about
+    a minute, against the oracle on the values the GPU saw (bf16- or e4m3-rounded, a_scale applied)."""
+    import torch
+
+    sys.path.insert(0, REPO)
+    import bench
+
+    seed = 0x5EED0002
+    A, scale = bench.make_A(torch, m, n, 0, dt)
+    tdt = torch.float8_e4m3fn if dt == "fp8" else torch.bfloat16
+    U, S, V = engine.rsvd(A, l, q=q, seed=seed, a_scale=scale)
+    Om = engine.generate_omega(n, l, seed=seed, dtype=tdt)
+    torch.cuda.synchronize()
+    assert engine.info()["jacobi_sweeps"] == 0
+    U, S, V = (x.cpu().double().numpy() for x in (U, S, V))
+    A_exact = np.asfortranarray(A.float().cpu().double().numpy() * scale)
+    Om_np = Om.cpu().double().numpy()
+    del A
+    torch.cuda.empty_cache()
+    oracle.set_threads(min(16, os.cpu_count() or 1))
+    Uo, So, Vo = oracle.rsvd(A_exact, l, q=q, Omega=Om_np)
+    assert rel_fro(S, So) < 1e-4, (cfg, rel_fro(S, So))
+    k = int(np.sum(So >= 10 * So[-1]))
+    assert k >= 32, (cfg, k)
+    eu = rel_fro(sign_align(U[:, :k], Uo[:, :k]), Uo[:, :k])
+    ev = rel_fro(sign_align(V[:, :k], Vo[:, :k]), Vo[:, :k])
+    assert eu < 1e-4 and ev < 1e-4, (cfg, k, eu, ev)
+    assert np.linalg.norm(U.T @ U - np.eye(l)) < 1e-4
+    assert np.linalg.norm(V.T @ V - np.eye(l)) < 1e-4
+
+
+@pytest.mark.timeout(900)
+def test_bench_c3_family_matches_oracle(engine):
+    """C3's tall-skinny family (BASELINE configs[2]: 2^20 x 1024 bf16, l = 128, q = 1) at 131072 rows
+    -- 32x the 4096 rows of its earlier pins -- through the same LP = 128 kernels
+    (two-step TN stages, the split Gram with loader groups, the eigensolver small SVD)."""
+    _pin(engine, "c3", 131072, 1024, 128, 1, "bf16")
+
+
+@pytest.mark.timeout(900)
+def test_bench_c5_family_matches_oracle(engine):
+    """C5's e4m3 family (BASELINE configs[4]: 131072 x 8192 e4m3, per-tensor scale, l = 512, q = 2) at
+    16384 rows: the fp8 x fp8 block-scaled sketch, the four-step e4m3 TN halves, the LP = 512 split
+    Grams and three-level factors, the LP = 512 eigensolver."""
+    _pin(engine, "c5", 16384, 8192, 512, 2, "fp8")
