@@ -1483,6 +1483,203 @@ hipError_t wproj3tn2_go(const void* A, int64_t lda, int64_t m, int64_t n, const 
     return launch_sum_slabs<float>(slabs, stride, p.splits, stride, Out, s);
 }
 
+// bf16 TN at LP = 128 with separate A and S rings (C3: Z = A^T Q, 2^20 x 1024 A, K split 64 ways).
+// The v2 double-step kernel it replaces stages A and S together in two 64-KiB stages, so one stage
+// -- 32 KiB of A -- is in flight while the other computes, and every 64-k stage pays about one HBM
+// latency (2.9 us per stage, 53 % of wave cycles in memory waits: 0.35 of HBM).  Here A has its
+// own ring of NA slots of [256 j][64 i] (128-B lines, tn2's image), and S (hi / lo) a ring of NSS
+// 32-step slots.  Every step issues S(st + SD) and HALF of A slot st / 2 + DA (SD = NSS - 1,
+// DA = NA - 1), so the A stream goes out evenly and one counted wait serves both parities.  The S
+// images are v2's [32 k][128] with the 16-B chunk XOR swizzle (no padding, so NA = 4 / NSS = 2
+// fills exactly 160 KiB); the swizzle only moves the 32-B window of a column tile, so each of the
+// G = 4 tiles gets its own per-lane base, fixed for the launch.  Wave tiles as v2's DS shape
+// (4 x 2 waves, 64 rows x 64 columns each) with the same MFMA sequence per acc tile (k-step by
+// k-step, hi then lo): bit-identical to the v2 kernel.
+// Wait: at step st = 2d + hs, S(st) (issued at step st - SD) is younger than both halves of A(d)
+// (steps 2d - 2DA, 2d - 2DA + 1; needs 2 DA - 1 > SD), and AH + (SD - 1)(S + AH) glds follow it.
+template <int NA, int NSS>
+struct Tn128Shape {
+    static constexpr int NS_MAX = 2, SIMG = 32 * 128 * 2, ASLOT = 256 * 128;
+    static constexpr size_t lds(int ns) { return (size_t)NA * ASLOT + (size_t)NSS * ns * SIMG; }
+    static_assert(2 * (NA - 1) - 1 > NSS - 1, "A must be issued before S");
+};
+
+template <bool SPLIT, int NA, int NSS>
+__global__ __launch_bounds__(512) void wproj3tn128_kernel(const bf16_t* __restrict__ A, int64_t lda, int64_t rows_out,
+                                                          int64_t K, int64_t arows, const bf16_t* __restrict__ Shi,
+                                                          const bf16_t* __restrict__ Slo, float* __restrict__ out,
+                                                          int64_t slab_stride, int64_t kchunk, int nrowblk) {
+    constexpr int LP = 128, WR = 4, G = 4, WI = 256, NS = SPLIT ? 2 : 1;
+    constexpr int DA = NA - 1, SD = NSS - 1;
+    typedef Tn128Shape<NA, NSS> SH;
+    constexpr int SIMG = SH::SIMG, SSLOT = NS * SIMG, ASLOT = SH::ASLOT;
+    constexpr int APW2 = ASLOT / 1024 / 8, AH = APW2 / 2;  // A glds per wave per slot / per half
+    constexpr int SBASE = NA * ASLOT;
+    constexpr int CNT = AH + (SD - 1) * (NS + AH);
+    static_assert(SH::lds(NS) <= 163840, "TN128 LDS");
+    extern __shared__ __attribute__((aligned(1024))) char smem_raw[];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int r = lane & 15, h = lane >> 4, q = r >> 2, p = r & 3;
+    const int wr = w % WR, wc = w / WR;
+    const int bid = xcd_remap(blockIdx.x, gridDim.x);
+    const int rb = bid % nrowblk, sp = bid / nrowblk;
+    const int64_t row0 = (int64_t)rb * WI;
+    const int64_t kbeg = (int64_t)sp * kchunk;
+    const int64_t kend = (kbeg + kchunk < K) ? kbeg + kchunk : K;
+    const int nsteps = (int)((kend - kbeg + KS - 1) / KS);
+    const int nd = (nsteps + 1) / 2;
+
+    // S: one glds per wave per image; lane's 16-B chunk cc of row srow holds source chunk cc ^ swz(srow)
+    const int su = w * 64 + lane, srow = su >> 4;
+    const int32_t soff = srow * LP + 8 * ((su & 15) ^ swz(srow));
+    int64_t aoff[APW2];
+    int arow[APW2];
+#pragma unroll
+    for (int t = 0; t < APW2; ++t) {
+        const int u = (t * 8 + w) * 64 + lane, j = u >> 3, pu = u & 7;
+        int64_t jc = row0 + j;
+        jc = jc < rows_out ? jc : rows_out - 1;
+        const int i = 8 * (pu ^ ((j >> 1) & 7));
+        aoff[t] = jc * lda + i;
+        arow[t] = i;
+    }
+    auto issueS = [&](int st) {
+        char* slot = smem_raw + SBASE + (st % NSS) * SSLOT;
+        const int64_t k0 = kbeg + (int64_t)st * KS;
+        glds16(Shi + k0 * LP + soff, slot + w * 1024);
+        if constexpr (SPLIT) glds16(Slo + k0 * LP + soff, slot + SIMG + w * 1024);
+    };
+    auto issueA = [&](int d, int half) {
+        char* slot = smem_raw + (d % NA) * ASLOT;
+        const int64_t k0 = kbeg + (int64_t)d * 2 * KS;
+        const bool tail = k0 + 2 * KS > arows;
+#pragma unroll
+        for (int tt = 0; tt < AH; ++tt) {
+            const int t = half * AH + tt;
+            const bf16_t* src = A + k0 + aoff[t];
+            if (tail && k0 + arow[t] + 8 > arows) src = A + (arows - 8 - arow[t]) + aoff[t];
+            glds16(src, slot + (t * 8 + w) * 1024);
+        }
+    };
+    // the issue rule of step st (also run over the virtual steps of the prologue)
+    auto issue = [&](int st) {
+        if (st + SD >= 0 && st + SD < nsteps) issueS(st + SD);
+        const int d = (st >> 1) + DA;  // (arithmetic shift: floor for the negative virtual steps)
+        if (d >= 0 && d < nd) {
+            if (st & 1) issueA(d, 1);
+            else issueA(d, 0);
+        }
+    };
+
+    // per-lane S read bases of the G column tiles (row k1; row k2 = k1 + 4 is +1024, lo is +SIMG)
+    const int k1 = 8 * h + q;
+    uint32_t lS[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) lS[g] = k1 * 256 + 16 * (((wc * 8 + 2 * g) ^ swz(k1)) + (p >> 1)) + 8 * (p & 1);
+    const int sw = (r >> 1) & 7;
+    const uint32_t lA0 = (wr * 64 + r) * 128 + 16 * (h ^ sw), lA1 = (wr * 64 + r) * 128 + 16 * ((4 + h) ^ sw);
+
+    f32x4 acc[RT][G];
+#pragma unroll
+    for (int t = 0; t < RT; ++t)
+#pragma unroll
+        for (int g = 0; g < G; ++g) acc[t][g] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    for (int st = -(2 * DA > SD ? 2 * DA : SD); st < 0; ++st) issue(st);
+    const uint32_t lds0 = lds_addr(smem_raw);
+    for (int st = 0; st < nsteps; ++st) {
+        const int d = st >> 1, hs = st & 1;
+        if (st + 2 * DA + SD < nsteps) wait_vm<CNT>();
+        else wait_vm<0>();
+        __builtin_amdgcn_s_barrier();
+        issue(st);
+        const uint32_t sS = lds0 + SBASE + (uint32_t)((st % NSS) * SSLOT);
+        const uint32_t sA = lds0 + (uint32_t)((d % NA) * ASLOT);
+        const uint32_t bA = sA + (hs ? lA1 : lA0);
+        auto wait_b = [&](i32x2* b) {
+            if (SPLIT) wait_lgkm0(b[0], b[1], b[2], b[3]);
+            else wait_lgkm0(b[0], b[1]);
+        };
+        i32x4 a4[RT];
+        bf16x8_t af[RT];
+        auto aread = [&](auto tc) {
+            constexpr int t = decltype(tc)::value;
+            a4[t] = read128_o<2048 * t>(bA);
+        };
+        static_for<RT>(aread);
+        auto bread = [&](auto gc, i32x2* b) {
+            constexpr int g = decltype(gc)::value;
+            const uint32_t bs = sS + lS[g];
+            b[0] = tr_read_o<0>(bs);
+            b[1] = tr_read_o<1024>(bs);
+            if constexpr (SPLIT) {
+                b[2] = tr_read_o<SIMG>(bs);
+                b[3] = tr_read_o<SIMG + 1024>(bs);
+            }
+        };
+        i32x2 bb[2][4];
+        bread(std::integral_constant<int, 0>{}, bb[0]);
+        wait_b(bb[0]);
+#pragma unroll
+        for (int t = 0; t < RT; ++t) {
+            wait_lgkm0(a4[t]);
+            af[t] = __builtin_bit_cast(bf16x8_t, a4[t]);
+        }
+        auto gstep = [&](auto gc) {
+            constexpr int g = decltype(gc)::value;
+            if constexpr (g + 1 < G) bread(std::integral_constant<int, g + 1>{}, bb[(g + 1) & 1]);
+            __builtin_amdgcn_sched_barrier(0);
+            const i32x2* b = bb[g & 1];
+            const bf16x8_t bh = join2(b[0], b[1]);
+#pragma unroll
+            for (int t = 0; t < RT; ++t) acc[t][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[t], bh, acc[t][g], 0, 0, 0);
+            if constexpr (SPLIT) {
+                const bf16x8_t bl = join2(b[2], b[3]);
+#pragma unroll
+                for (int t = 0; t < RT; ++t) acc[t][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[t], bl, acc[t][g], 0, 0, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (g + 1 < G) wait_b(bb[(g + 1) & 1]);
+        };
+        static_for<G>(gstep);
+    }
+
+    float* dst = out + (int64_t)sp * slab_stride;
+#pragma unroll
+    for (int t = 0; t < RT; ++t)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int64_t row = row0 + wr * 64 + 16 * t + 4 * h + j;
+            if (row < rows_out) {
+#pragma unroll
+                for (int g = 0; g < G; ++g) dst[row * LP + wc * G * 16 + 16 * g + r] = acc[t][g][j];
+            }
+        }
+}
+
+// ring depths (A slots, S slots): 4 / 2 in the engine; 3 / 3 for the lab (p.tn3 = 2)
+template <bool SPLIT>
+hipError_t wproj3tn128_go(const void* A, int64_t lda, int64_t m, int64_t n, const bf16_t* Shi, const bf16_t* Slo,
+                          const WProjPlan& p, float* slabs, float* Out, hipStream_t s, hipEvent_t done) {
+    constexpr int NS = SPLIT ? 2 : 1;
+    const int64_t rows_out = n, K = m;
+    float* o = p.splits == 1 ? Out : slabs;
+    const int64_t stride = rows_out * 128;
+    if (p.tn3 == 2)
+        hipLaunchKernelGGL((wproj3tn128_kernel<SPLIT, 3, 3>), dim3(p.blocks * p.splits), dim3(512),
+                           (Tn128Shape<3, 3>::lds(NS)), s, reinterpret_cast<const bf16_t*>(A), lda, rows_out, K, m, Shi,
+                           Slo, o, stride, p.chunk, p.blocks);
+    else
+        hipLaunchKernelGGL((wproj3tn128_kernel<SPLIT, 4, 2>), dim3(p.blocks * p.splits), dim3(512),
+                           (Tn128Shape<4, 2>::lds(NS)), s, reinterpret_cast<const bf16_t*>(A), lda, rows_out, K, m, Shi,
+                           Slo, o, stride, p.chunk, p.blocks);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess && done) e = hipEventRecord(done, s);
+    if (e != hipSuccess || p.splits == 1) return e;
+    return launch_sum_slabs<float>(slabs, stride, p.splits, stride, Out, s);
+}
+
 
 template <bool FP8, bool NN, int LP, bool SPLIT, bool DS = false, bool S8 = false, bool SC = false>
 hipError_t wproj2_go(const void* A, int64_t lda, int64_t m, int64_t n, const bf16_t* Shi, const bf16_t* Slo,
@@ -1565,6 +1762,9 @@ hipError_t wproj_lp(int nn, int fp8, const void* A, int64_t lda, int64_t m, int6
                     const bf16_t* Slo, const WProjPlan& p, float* slabs, float* Out, hipStream_t s, hipEvent_t d) {
     const bool split = Slo != nullptr;
     if constexpr (LP == 128) {
+        if (p.v2 && p.ds && !nn && !fp8 && p.tn3)
+            return split ? wproj3tn128_go<true>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d)
+                         : wproj3tn128_go<false>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d);
         if (p.v2 && p.ds && !nn && !fp8)
             return split ? wproj2_go<false, false, 128, true, true>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d)
                          : wproj2_go<false, false, 128, false, true>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d);
@@ -1652,6 +1852,15 @@ static bool tn4_enabled() {  // RSVD_FP8_TN4=0 in the environment: the wproj2 e4
     return env != 0;
 }
 
+static int tn128_mode() {  // RSVD_TN128: 0 the v2 double-step LP = 128 TN, 1 rings 4 / 2 (default), 2 rings 3 / 3
+    static const int env = [] {
+        const char* v = std::getenv("RSVD_TN128");
+        const int x = v ? std::atoi(v) : 1;
+        return x < 0 || x > 2 ? 1 : x;
+    }();
+    return env;
+}
+
 static bool half_merge_enabled() {
     static const int env = [] {
         const char* v = std::getenv("RSVD_HALF_MERGE");
@@ -1666,6 +1875,7 @@ WProjPlan plan_wproj(int64_t rows_out, int64_t K, int LP, bool v2, bool nn, bool
     p.v3 = p.v2 && !fp8 && (LP == 256 || LP == 512);
     p.tn2 = p.v3 && !nn && LP == 256;  // two k-steps per A slot: K chunks of whole 64-row pairs
     p.ds = p.v2 && LP == 128 && !nn && !fp8 && K % 64 == 0;  // double-step TN stages (whole 64-row K chunks)
+    p.tn3 = p.ds ? tn128_mode() : 0;
     p.half = p.v2 && fp8 && LP == 512;  // two LP = 256 column halves (wproj2_half_go)
     // e4m3 TN: four k-steps per A slot (wproj3tn4_kernel; K chunks of whole 128-row slots)
     p.tn4 = p.v2 && fp8 && !nn && (LP == 256 || LP == 512) && tn4_enabled();

@@ -74,7 +74,8 @@ def test_wide_f32_device(engine):
     _check(U, S, V, Uo, So, Vo, A.astype(np.float64), 1e-4, 1e-4)
 
 
-# (4096, 1024, 128, 1) and (2048, 900, 100, 2) run the two-k-step TN stages (LP = 128, m % 64 == 0);
+# (4096, 1024, 128, 1) and (2048, 900, 100, 2) run the two-k-step TN (LP = 128, m % 64 == 0: the
+# separate-ring wproj3tn128_kernel);
 # (1000, 700, 128, 1) the single-step fallback (m % 64 != 0)
 @pytest.mark.parametrize("m,n,l,q", [(4096, 1024, 128, 1), (2048, 3000, 256, 2), (1024, 1536, 64, 2),
                                      (700, 500, 16, 0), (1000, 700, 128, 1), (2048, 900, 100, 2)])

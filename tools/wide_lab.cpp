@@ -859,6 +859,47 @@ int main(int argc, char** argv) {
             CK(hipFree(A)); CK(hipFree(Sh)); CK(hipFree(Sl)); CK(hipFree(O0)); CK(hipFree(O1));
         }
     }
+    if (what == "tn128") {  // LP = 128 TN: v2 double-step stages (tn3 off) against the separate rings
+        for (int cs = 0; cs < 2; ++cs) {
+            const int64_t m = cs ? (1 << 20) : 4160, n = cs ? 1024 : 1000;  // case 0: ragged rows, K chunks
+            const int LP = 128;
+            void* A;
+            CK(hipMalloc(&A, (size_t)m * n * 2));
+            hipLaunchKernelGGL(fill_random_kernel, dim3(4096), dim3(256), 0, S, (uint16_t*)A, (size_t)m * n, 0);
+            bf16_t* Sh = dev_random<bf16_t>((size_t)m * LP);
+            bf16_t* Sl = dev_random<bf16_t>((size_t)m * LP);
+            float *O0, *O1;
+            CK(hipMalloc(&O0, (size_t)n * LP * 4));
+            CK(hipMalloc(&O1, (size_t)n * LP * 4));
+            WProjPlan p0 = plan_wproj(n, m, LP, true, false, false), p1 = p0, p2 = p0;
+            p0.tn3 = 0;
+            p1.tn3 = p1.ds ? 1 : 0;
+            p2.tn3 = p2.ds ? 2 : 0;
+            float* slabs;
+            CK(hipMalloc(&slabs, (size_t)p0.splits * n * LP * 4));
+            const double bytes = (double)m * n * 2;
+            for (int sp = 1; sp >= 0; --sp) {
+                const bf16_t* lo = sp ? Sl : nullptr;
+                for (int rep = 0; rep < 2; ++rep) {
+                    double t0 = time_us([&] { CK(launch_wproj(0, 0, A, m, m, n, Sh, lo, LP, p0, slabs, O0, S)); });
+                    std::vector<float> h0((size_t)n * LP), h1((size_t)n * LP);
+                    CK(hipMemcpy(h0.data(), O0, h0.size() * 4, hipMemcpyDeviceToHost));
+                    double t1 = time_us([&] { CK(launch_wproj(0, 0, A, m, m, n, Sh, lo, LP, p1, slabs, O1, S)); });
+                    CK(hipMemcpy(h1.data(), O1, h1.size() * 4, hipMemcpyDeviceToHost));
+                    const bool same1 = !memcmp(h0.data(), h1.data(), h0.size() * 4);
+                    CK(hipMemset(O1, 0, h1.size() * 4));
+                    double t2 = time_us([&] { CK(launch_wproj(0, 0, A, m, m, n, Sh, lo, LP, p2, slabs, O1, S)); });
+                    CK(hipMemcpy(h1.data(), O1, h1.size() * 4, hipMemcpyDeviceToHost));
+                    const bool same2 = !memcmp(h0.data(), h1.data(), h0.size() * 4);
+                    printf("tn128 %ldx%ld TN%d splits %d: v2ds %.1f us (%.0f GB/s)  rings 4/2 %.1f us (%.0f GB/s) same %d"
+                           "  rings 3/3 %.1f us (%.0f GB/s) same %d\n",
+                           (long)m, (long)n, sp ? 2 : 1, p0.splits, t0, bytes / t0 / 1e3, t1, bytes / t1 / 1e3, (int)same1,
+                           t2, bytes / t2 / 1e3, (int)same2);
+                }
+            }
+            CK(hipFree(slabs)); CK(hipFree(A)); CK(hipFree(Sh)); CK(hipFree(Sl)); CK(hipFree(O0)); CK(hipFree(O1));
+        }
+    }
     if (what == "all" || what == "check") check_proj();
     if (what == "probe") probe_glds();
     if (what == "s8") check_s8();
