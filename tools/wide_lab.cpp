@@ -86,6 +86,7 @@ static void bench_pg() {
 
 static void bench_psplit() {  // the split panel product (panel_split_kernel), C3 / C4 / C5 m-side shapes
     for (int LP : {128, 256, 512}) {
+        if (std::getenv("LAB_LP") && std::atoi(std::getenv("LAB_LP")) != LP) continue;
         const int64_t rows = LP == 128 ? (1 << 20) : (LP == 256 ? 65536 : 131072);
         float* In = dev_random<float>((size_t)rows * LP);
         float* Out;
@@ -136,6 +137,7 @@ static void bench_gram() {
 
 static void bench_gsplit() {  // the split Gram (bf16 MFMA) against the fp64 Gram of the same panel
     for (int LP : {128, 256, 512}) {
+        if (std::getenv("LAB_LP") && std::atoi(std::getenv("LAB_LP")) != LP) continue;
         const int64_t rows = LP == 128 ? (1 << 20) : (LP == 256 ? 65536 : 131072);
         float* P = dev_random<float>((size_t)rows * LP);
         GramPlan gp = plan_gram_wide(rows, LP, 0);
