@@ -202,8 +202,9 @@ int rsvd_set_workspace(rsvd_handle_t h, void *ptr, size_t bytes);
  * type (rounded to bf16 / e4m3 for the low-precision types); NULL => Philox(desc->seed).
  * l <= 512 on the wide engine; 512 < l <= 4096 (the reference has no cap, src/rSVD.cpp:72) on one GPU
  * through dense_big.cpp's column-major blocks (MFMA GEMM products, block CGS2 + CholeskyQR3, the
- * block Jacobi small SVD; bf16 / e4m3 A widened to fp32 once), methods Jacobi / ParallelJacobi
- * (RSVD_ERR_UNSUPPORTED for Power, for row-sharded handles and past 4096). */
+ * block Jacobi small SVD -- or, for Power, the power method in the coordinates of Q_B on a persistent
+ * grid; bf16 / e4m3 A widened to fp32 once), also row-sharded (RSVD_ERR_UNSUPPORTED for
+ * RSVD_SVD_POWER_IC and past 4096). */
 int rsvd_run(rsvd_handle_t h, const rsvd_desc_t *desc, const void *A, const void *omega, int64_t ldo,
              void *U, int64_t ldu, void *S, void *V, int64_t ldv);
 

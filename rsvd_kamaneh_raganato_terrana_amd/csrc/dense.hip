@@ -582,13 +582,23 @@ __device__ __forceinline__ void pg_rows(int64_t rows, int G, int g, int64_t& r0,
 // sigma_j u_j v_j^T is applied implicitly (the coefficients sigma_j (v_j . v) are reduced over the
 // grid); B is deflated explicitly, B -= sigma^2 (u.u) v v^T (:212).  Outputs: U (m x dim, ldu),
 // V (n x dim, ldv, v_i in column i), S (dim), *kept.  Work: Y (2 n), part (G (dim + 2)), sync (8).
-__global__ __launch_bounds__(kPgThreads) void power_grid_kernel(const double* __restrict__ A, int64_t lda, int64_t m,
+// General layouts (PowerGridIO): A(r, c) = A[r ar + c ac], B row r at B + r ldb, U(r, i) = U[r + i ldu],
+// V(c, i) = V[c + i ldv]; x0 (optional): start vector i is x0[i ldx0 + c] instead of the Philox
+// stream; zero_tail: the triplets past an early stop are written as zeros (the rSVD's layout).
+struct PowerGridIO {
+    int64_t ar, ac, ldb, ldu, ldv, ldx0;
+    const double* x0;
+    int zero_tail;
+};
+
+__global__ __launch_bounds__(kPgThreads) void power_grid_kernel(const double* __restrict__ A, PowerGridIO io, int64_t m,
                                                                 int64_t n, double* __restrict__ B, int dim, uint64_t seed,
-                                                                int iters, double* __restrict__ U, int64_t ldu,
-                                                                double* __restrict__ V, int64_t ldv,
+                                                                int iters, double* __restrict__ U,
+                                                                double* __restrict__ V,
                                                                 double* __restrict__ S, double* __restrict__ Y,
                                                                 double* __restrict__ part, unsigned* __restrict__ sync,
                                                                 int* __restrict__ kept, int* __restrict__ tmo) {
+    const int64_t ldu = io.ldu, ldv = io.ldv, ldb = io.ldb;
     __shared__ double red[kPgThreads / 64];
     __shared__ double coef_s[64];
     const int G = gridDim.x, g = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -611,10 +621,10 @@ __global__ __launch_bounds__(kPgThreads) void power_grid_kernel(const double* __
     double* y1 = Y + n;
     int k = dim;
     for (int i = 0; i < dim; ++i) {
-        // x0 = N(0,1) Philox stream (seed + i) (src/PM.cpp:15-22); |x0| over the grid
+        // x0 = N(0,1) Philox stream (seed + i) (src/PM.cpp:15-22), or the given start; |x0| over the grid
         double sq = 0.0;
         for (int64_t c = b0 + tid; c < b1; c += kPgThreads) {
-            const double v = gauss_elem((uint64_t)c, seed + (uint64_t)i);
+            const double v = io.x0 ? io.x0[(int64_t)i * io.ldx0 + c] : gauss_elem((uint64_t)c, seed + (uint64_t)i);
             y0[c] = v;
             sq += v * v;
         }
@@ -627,7 +637,7 @@ __global__ __launch_bounds__(kPgThreads) void power_grid_kernel(const double* __
             const double inv = 1.0 / nrm;
             double sq2 = 0.0;
             for (int64_t row = b0 + w; row < b1; row += kPgThreads / 64) {
-                const double* br = B + row * n;
+                const double* br = B + row * ldb;
                 double acc = 0.0;
                 for (int64_t c = lane; c < n; c += 64) acc += br[c] * y0[c];
 #pragma unroll
@@ -669,7 +679,7 @@ __global__ __launch_bounds__(kPgThreads) void power_grid_kernel(const double* __
             for (int64_t row = a0 + tid; row < a1; row += kPgThreads) {
                 double acc = 0.0;
                 if (j0 == 0)
-                    for (int64_t c = 0; c < n; ++c) acc += A[row + c * lda] * (y0[c] * vs);
+                    for (int64_t c = 0; c < n; ++c) acc += A[row * io.ar + c * io.ac] * (y0[c] * vs);
                 else
                     acc = U[row + (size_t)i * ldu];
                 for (int jj = 0; jj < jn; ++jj) acc -= coef_s[jj] * U[row + (size_t)(j0 + jj) * ldu];
@@ -693,12 +703,19 @@ __global__ __launch_bounds__(kPgThreads) void power_grid_kernel(const double* __
         const double f = sigma * sigma * vs * vs;  // sigma^2 (u.u) with u.u = 1, v = y0 vs
         for (int64_t row = b0 + w; row < b1; row += kPgThreads / 64) {
             const double xr = y0[row];
-            double* br = B + row * n;
+            double* br = B + row * ldb;
             for (int64_t c = lane; c < n; c += 64) br[c] -= f * xr * y0[c];
         }
         for (int64_t c = b0 + tid; c < b1; c += kPgThreads) V[c + (size_t)i * ldv] = y0[c] * vs;
         if (g == 0 && tid == 0) S[i] = sigma;
         if (!barrier()) return;
+    }
+    if (io.zero_tail) {  // (rSVD layout) triplets past an early stop are zero, as the one-workgroup kernel's
+        for (int i = k; i < dim; ++i) {
+            for (int64_t row = a0 + tid; row < a1; row += kPgThreads) U[row + (size_t)i * ldu] = 0.0;
+            for (int64_t c = b0 + tid; c < b1; c += kPgThreads) V[c + (size_t)i * ldv] = 0.0;
+            if (g == 0 && tid == 0) S[i] = 0.0;
+        }
     }
     if (g == 0 && tid == 0) *kept = k;
 }
@@ -945,8 +962,20 @@ hipError_t launch_power_grid(const double* A, int64_t lda, int64_t m, int64_t n,
                              double* part, unsigned* sync, int* kept, int* tmo, hipStream_t s) {
     hipError_t e = hipMemsetAsync(sync, 0, 8 * sizeof(unsigned), s);
     if (e != hipSuccess) return e;
-    return launch_coresident(power_grid_kernel, dim3(power_grid_size(n)), dim3(kPgThreads), 0, s, A, lda, m, n, B, dim,
-                             seed, iters, U, ldu, V, ldv, S, Y, part, sync, kept, tmo);
+    const PowerGridIO io{1, lda, n, ldu, ldv, 0, nullptr, 0};
+    return launch_coresident(power_grid_kernel, dim3(power_grid_size(n)), dim3(kPgThreads), 0, s, A, io, m, n, B, dim,
+                             seed, iters, U, V, S, Y, part, sync, kept, tmo);
+}
+
+hipError_t launch_power_grid_rsvd(const double* R, int l, double* B, const double* X0s, int iters, double* Up,
+                                  double* Vc, double* S, double* Y, double* part, unsigned* sync, int* kept, int* tmo,
+                                  hipStream_t s) {
+    hipError_t e = hipMemsetAsync(sync, 0, 8 * sizeof(unsigned), s);
+    if (e != hipSuccess) return e;
+    // P = R^T (P(r, c) = R[c + r l]); B, U_p, V_c, X0s all l x l with ld l
+    const PowerGridIO io{l, 1, l, l, l, l, X0s, 1};
+    return launch_coresident(power_grid_kernel, dim3(power_grid_size(l)), dim3(kPgThreads), 0, s, R, io, (int64_t)l,
+                             (int64_t)l, B, l, (uint64_t)0, iters, Up, Vc, S, Y, part, sync, kept, tmo);
 }
 
 int power_iterations(int64_t n) {

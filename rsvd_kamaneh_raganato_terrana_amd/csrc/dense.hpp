@@ -40,6 +40,13 @@ int power_grid_size(int64_t n);
 hipError_t launch_power_grid(const double* A, int64_t lda, int64_t m, int64_t n, double* B, int dim, uint64_t seed,
                              int iters, double* U, int64_t ldu, double* V, int64_t ldv, double* S, double* Y,
                              double* part, unsigned* sync, int* kept, int* tmo, hipStream_t s);
+// SVDMethod::Power of the rSVD in the coordinates of Q_B on the grid (any l; the one-workgroup
+// launch_power_svd holds l <= 512): P = R^T for the column-major l x l R = Q_B^T B^T (ld l), B = R R^T,
+// start vectors X0s (column i = Q_B^T x0_i), U_p / V_c column-major l x l (u_i, v_i in column i;
+// zero past an early stop), S (l).  Work as launch_power_grid (Y 2 l, part power_grid_size(l) (l + 2), sync 8).
+hipError_t launch_power_grid_rsvd(const double* R, int l, double* B, const double* X0s, int iters, double* Up,
+                                  double* Vc, double* S, double* Y, double* part, unsigned* sync, int* kept, int* tmo,
+                                  hipStream_t s);
 // SVD<ParallelJacobi> with the reference's iteration (weight-sorted sequential two-sided Jacobi,
 // SVD_class.hpp:223-333): W(p, q) = Win[p sp + q sq] (d x d; tri > 0 / < 0: upper / lower
 // triangular) copied to W (LP pitch); Jl / Jr (LP x

@@ -480,10 +480,45 @@ int big_rsvd_typed(rsvd_handle_t h, const rsvd_desc_t* d, const void* Av, const 
     double* Vw = reinterpret_cast<double*>(b + L.off_Vw);
     double* Sd = reinterpret_cast<double*>(b + L.off_S);
     unsigned* sync = reinterpret_cast<unsigned*>(b + L.off_sync);
+    const double asc = d->a_scale != 0.0 ? d->a_scale : 1.0;
+    if (d->method == RSVD_SVD_POWER) {
+        // SVDMethod::Power (src/rSVD.cpp:106-113) past 512 sketch columns, in the coordinates of Q_B as
+        // the wide engine's power stage (wide.cpp power_stage): start vectors Philox(power_seed(seed) + i)
+        // over the n coordinates, X0s = Q_B^T X0, then the power method with deflation on P = R^T,
+        // B = R R^T on the grid (dense.hip launch_power_grid_rsvd; the one-workgroup kernel holds l <= 512)
+        T* X0 = Om;  // (free after the sketch) X0[r l + i] = x0_i[r]: the column-major view is X0^T (l x n)
+        RSVD_CK(launch_power_start<T>(X0, n, (int)l, (int)l, power_seed(d->seed), s));
+        double* X0s = JXp;  // l x l: column i = Q_B^T x0_i
+        double* part = JXp + l * l;
+        double* Yw = part + (int64_t)power_grid_size(l) * (l + 2);
+        if constexpr (sizeof(T) == 8) {
+            RSVD_CK(launch_gemm<T>(1, 1, l, l, n, T(1), X, n, X0, l, T(0), reinterpret_cast<T*>(X0s), l, s));
+        } else {
+            T* y0 = reinterpret_cast<T*>(Vw);  // (free until the power method writes V_c)
+            RSVD_CK(launch_gemm<T>(1, 1, l, l, n, T(1), X, n, X0, l, T(0), y0, l, s));
+            RSVD_CK(launch_widen<T>(y0, l, l, l, X0s, s));
+        }
+        RSVD_CK(launch_gemm<double>(0, 1, l, l, l, 1.0, R64, l, R64, l, 0.0, JJp, l, s));  // B = R R^T
+        RSVD_CK(launch_power_grid_rsvd(R64, (int)l, JJp, X0s, power_iterations(n), Uw, Vw, Sd, Yw, part, sync,
+                                       h->dflags + 16, h->dflags + kFlagGramTimeout, s));
+        RSVD_CK(launch_convert_scale<T>(Sd, reinterpret_cast<T*>(S), (int)l, std::fabs(asc), s));
+        // U = Q U_p, V = Q_B V_c (column-major l x l, ld l)
+        const T* up = reinterpret_cast<const T*>(Uw);
+        const T* vc = reinterpret_cast<const T*>(Vw);
+        if (sizeof(T) == 4) {
+            float* u32 = reinterpret_cast<float*>(b + L.off_U32);
+            float* v32 = reinterpret_cast<float*>(JXp);  // X0s / part are spent
+            RSVD_CK(launch_convert_scale<float>(Uw, u32, (int)(l * l), 1.0, s));
+            RSVD_CK(launch_convert_scale<float>(Vw, v32, (int)(l * l), 1.0, s));
+            up = reinterpret_cast<const T*>(u32);
+            vc = reinterpret_cast<const T*>(v32);
+        }
+        RSVD_CK(launch_gemm<T>(0, 0, m, l, l, T(1), Q, m, up, l, T(0), reinterpret_cast<T*>(U), ldu, s));
+        RSVD_CK(launch_gemm<T>(0, 0, n, l, l, T(1), X, n, vc, l, T(0), reinterpret_cast<T*>(V), ldv, s));
+    } else {
     RSVD_CK(launch_block_jacobi_ex<double>(R64, l, 1, (int)l, (int)l, L.MR, L.LP, JXp, JJp, Uw, Vw, Sd, sync,
                                            h->dflags + 1, s, sizeof(T) == 4 ? 1e-8 : 1e-16,
                                            sizeof(T) == 4 ? kBJTolF32 : kBJTolF64));
-    const double asc = d->a_scale != 0.0 ? d->a_scale : 1.0;
     RSVD_CK(launch_convert_scale<T>(Sd, reinterpret_cast<T*>(S), (int)l, std::fabs(asc), s));
     // U = Q U_w, V = Q_B V_w (U_w, V_w row-major with pitch LP: their column-major views are the transposes)
     const T* uw = reinterpret_cast<const T*>(Uw);
@@ -498,6 +533,7 @@ int big_rsvd_typed(rsvd_handle_t h, const rsvd_desc_t* d, const void* Av, const 
     }
     RSVD_CK(launch_gemm<T>(0, 1, m, l, l, T(1), Q, m, uw, L.LP, T(0), reinterpret_cast<T*>(U), ldu, s));
     RSVD_CK(launch_gemm<T>(0, 1, n, l, l, T(1), X, n, vw, L.LP, T(0), reinterpret_cast<T*>(V), ldv, s));
+    }
     if (asc < 0.0) RSVD_CK(launch_scale_cols<T>(reinterpret_cast<T*>(V), n, (int)l, ldv, -1.0, s));
     RSVD_CK(launch_check_finite<T>(reinterpret_cast<const T*>(S), (int)l, h->dflags + kFlagNonFinite, s));
     return RSVD_OK;
@@ -551,8 +587,8 @@ int big_rsvd_run(rsvd_handle_t h, const rsvd_desc_t* d, const void* A, const voi
         h->err = "RSVD_FLAG_FORCE_NSHARD: the sharded n-side path is built for l <= 512";
         return RSVD_ERR_UNSUPPORTED;
     }
-    if (!Qout && (d->method == RSVD_SVD_POWER || d->method == RSVD_SVD_POWER_IC)) {
-        h->err = "SVDMethod::Power is built for l <= 512";
+    if (!Qout && d->method == RSVD_SVD_POWER_IC) {
+        h->err = "RSVD_SVD_POWER_IC (image_compression's power method) is built for l <= 512";
         return RSVD_ERR_UNSUPPORTED;
     }
     if (d->dtype == RSVD_F64) return big_rsvd_typed<double>(h, d, A, omega, ldo, U, ldu, S, V, ldv, Qout, ldq);
