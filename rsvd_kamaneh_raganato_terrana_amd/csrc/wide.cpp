@@ -312,31 +312,39 @@ struct WideEngine {
     int cholqr_pass(const T* P, int64_t rows, const GramPlan& gp, T* Out, bool sharded, bf16_t* hi, bf16_t* lo,
                     int* flag, const int* pred) {
         float* r32 = sizeof(T) == 4 ? Rinv32 : nullptr;
+        // the split panel product's pieces of R^-1, written by the factor with its fp32 copy (no
+        // split_mat launch per pass; bit-identical)
+        bf16_t* mt = (ms() && L.LP >= 128) ? ms() : nullptr;
         // LP = 256 / 512, l > LP / 2: the two-level factor (wide_qr.hip launch_chol_wide_2level; JX is
         // free scratch until the small SVD) for unpredicated passes
         const bool two = (chol2 & (L.LP == 512 ? 1 : (L.LP == 256 ? 2 : 0))) && L.l > L.LP / 2;
         auto factor = [&](int* fl, double ill_tol, int* ill) -> hipError_t {
             if (two)
                 return launch_chol_wide_2level(G, L.l, L.LP, tol(), R, Rinv, r32, colflag, fl, W, JX, s, ill_tol, ill,
-                                               nullptr, chol_depth());
-            return launch_chol_wide(G, L.l, L.LP, tol(), R, Rinv, r32, colflag, fl, W, nullptr, s, ill_tol, ill);
+                                               nullptr, chol_depth(), mt);
+            return launch_chol_wide(G, L.l, L.LP, tol(), R, Rinv, r32, colflag, fl, W, nullptr, s, ill_tol, ill,
+                                    nullptr, mt);
         };
         if (split_gram && !sharded && !pred) {
             int* ill = h->dflags + kFlagSplitIll;
             RSVD_CK(launch_gram_split(reinterpret_cast<const float*>(P), rows, L.LP, gp, gslab, G, s));
             RSVD_CK(factor(h->dflags + kFlagSplitScratch, kSplitIllTol, ill));
             RSVD_CK(launch_gram_wide<T>(P, nullptr, rows, L.LP, gp, gslab, G, ill, s));
-            RSVD_CK(launch_chol_wide(G, L.l, L.LP, tol(), R, Rinv, r32, colflag, flag, W, ill, s));
-            RSVD_CK(launch_panel_gemm<T>(P, rows, L.LP, mat(Rinv, Rinv32), 1, Out, 0, 0, hi, lo, nullptr, s, ms()));
+            RSVD_CK(launch_chol_wide(G, L.l, L.LP, tol(), R, Rinv, r32, colflag, flag, W, ill, s, 0.0, nullptr, nullptr,
+                                     mt));
+            RSVD_CK(launch_panel_gemm<T>(P, rows, L.LP, mat(Rinv, Rinv32), 1, Out, 0, 0, hi, lo, nullptr, s, ms(),
+                                         mt != nullptr));
             return RSVD_OK;
         }
         RSVD_CK(launch_gram_wide<T>(P, nullptr, rows, L.LP, gp, gslab, G, pred, s));
         if (sharded) RSVD_TRY(allreduce(G, (int64_t)L.LP * L.LP, RSVD_F64));
         if (pred)
-            RSVD_CK(launch_chol_wide(G, L.l, L.LP, tol(), R, Rinv, r32, colflag, flag, W, pred, s));
+            RSVD_CK(launch_chol_wide(G, L.l, L.LP, tol(), R, Rinv, r32, colflag, flag, W, pred, s, 0.0, nullptr, nullptr,
+                                     mt));
         else
             RSVD_CK(factor(flag, 0.0, nullptr));
-        RSVD_CK(launch_panel_gemm<T>(P, rows, L.LP, mat(Rinv, Rinv32), 1, Out, 0, 0, hi, lo, pred, s, ms()));
+        RSVD_CK(launch_panel_gemm<T>(P, rows, L.LP, mat(Rinv, Rinv32), 1, Out, 0, 0, hi, lo, pred, s, ms(),
+                                     mt != nullptr));
         return RSVD_OK;
     }
 

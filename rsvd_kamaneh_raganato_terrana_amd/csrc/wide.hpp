@@ -80,7 +80,8 @@ hipError_t launch_gram_wide(const T* P, const T* P2, int64_t rows, int LP, const
 // ill (nullable): set to 1 when a pivot d_k <= ill_tol * G_kk (else 0) -- the split-Gram fallback test.
 hipError_t launch_chol_wide(const double* G, int l, int LP, double tol, double* R, double* Rinv, float* Rinv32,
                             int* colflag, int* flag, double* work, const int* pred, hipStream_t s,
-                            double ill_tol = 0.0, int* ill = nullptr, const double* d0src = nullptr);
+                            double ill_tol = 0.0, int* ill = nullptr, const double* d0src = nullptr,
+                            bf16_t* Mt = nullptr);
 // The same factor at LP = 2 B (B = 128, 256; l > B) in two B-column levels: R11 = chol(G11) and
 // S = G22 - R12^T R12 (R12 = R11^-T G12), the off-diagonal blocks R12 and Rinv12 = -Rinv11 R12 Rinv22
 // on a B^3 fp64 MFMA GEMM, breakdowns judged against the diagonal of G (d0src when this factor is
@@ -89,7 +90,9 @@ hipError_t launch_chol_wide(const double* G, int l, int LP, double tol, double* 
 hipError_t launch_chol_wide_2level(const double* G, int l, int LP, double tol, double* R, double* Rinv,
                                    float* Rinv32, int* colflag, int* flag, double* work, double* scratch,
                                    hipStream_t s, double ill_tol = 0.0, int* ill = nullptr,
-                                   const double* d0src = nullptr, int depth = 0);
+                                   const double* d0src = nullptr, int depth = 0, bf16_t* Mt = nullptr);
+// (Mt, both factors, with Rinv32: R^-1's fp32 copy also as split_mat_kernel's three bf16 piece
+// images, 3 LP^2 -- launch_panel_gemm's msplit with msplit_ready)
 size_t chol_2level_scratch_doubles(int LP, int depth);
 // G = P^T P of an fp32 panel by the three-piece bf16 split on the bf16 MFMA (fp32 chunk sums added
 // in fp64; |dG| ~ 1e-8 |G|) -- same plan / slab layout as launch_gram_wide.  LP in {128, 256, 512}.
@@ -114,7 +117,7 @@ extern int chol_variant;
 template <typename T>
 hipError_t launch_panel_gemm(const T* In, int64_t rows, int LP, const T* M, int upper, T* Out, int64_t ldo,
                              int cols, bf16_t* hi, bf16_t* lo, const int* pred, hipStream_t s,
-                             bf16_t* msplit = nullptr);
+                             bf16_t* msplit = nullptr, bool msplit_ready = false);
 // y[0..n) = (T)(x * sc)
 template <typename T>
 hipError_t launch_convert_scale(const double* x, T* y, int n, double sc, hipStream_t s);

@@ -1676,10 +1676,31 @@ __global__ __launch_bounds__(64 * kCholRegWaves) void chol_reg_kernel(const doub
 // (An accumulator in MFMA output layout -- row h + 4 j, column r in lane (r, h) -- is already the
 // B operand of the next product: rows 4 kk + h.)  Also: zeros below the block diagonal of R and
 // R^-1, and the fp32 copy of this block column of R^-1.
+__device__ __forceinline__ bf16_t f2bf(float x) {  // round to nearest even
+    const uint32_t u = __float_as_uint(x);
+    if ((u & 0x7f800000u) == 0x7f800000u) return (bf16_t)(u >> 16);
+    return (bf16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+__device__ __forceinline__ float bf2f(bf16_t b) { return __uint_as_float((uint32_t)b << 16); }
+
+// The three bf16 pieces of the fp32 element (row k, column c) of an LP x LP matrix in split_mat_kernel's
+// transposed piece images (Mt[x][c][k], image pitch L2 = LP^2): the factor kernels that write R^-1's
+// fp32 copy also write its pieces, so the split panel product needs no split_mat launch.
+__device__ __forceinline__ void store_pieces(bf16_t* __restrict__ Mt, int64_t L2, int64_t idx, float v) {
+    const bf16_t bh = f2bf(v);
+    const float rm = v - bf2f(bh);
+    const bf16_t bm = f2bf(rm);
+    Mt[idx] = bh;
+    Mt[L2 + idx] = bm;
+    Mt[2 * L2 + idx] = f2bf(rm - bf2f(bm));
+}
+
 constexpr int kRinvSlots = 8;  // LP <= 512: 32 block rows over 4 waves
 
 __global__ __launch_bounds__(256) void rinv_wide_kernel(int LP, double* __restrict__ R, double* __restrict__ Rinv,
-                                                        float* __restrict__ Rinv32, const int* __restrict__ pred) {
+                                                        float* __restrict__ Rinv32, const int* __restrict__ pred,
+                                                        bf16_t* __restrict__ Mt) {
+    const int64_t L2 = (int64_t)LP * LP;
     if (pred && *pred == 0) return;
     __shared__ double Xs[2][256];  // X[k] of the current step (buffer k & 1), row-major
     const int jb = blockIdx.x;
@@ -1692,6 +1713,7 @@ __global__ __launch_bounds__(256) void rinv_wide_kernel(int LP, double* __restri
         R[(int64_t)i * LP + c] = 0.0;
         Rinv[(int64_t)i * LP + c] = 0.0;
         if (Rinv32) Rinv32[(int64_t)i * LP + c] = 0.0f;
+        if (Mt) store_pieces(Mt, L2, (int64_t)c * LP + i, 0.0f);
     }
     f64x4 T[kRinvSlots];
     double Rc[kRinvSlots][4], Rn[kRinvSlots][4], Dn[4];
@@ -1747,6 +1769,7 @@ __global__ __launch_bounds__(256) void rinv_wide_kernel(int LP, double* __restri
                 Xs[k & 1][i * 16 + r] = x[j];
                 if (k != jb) Rinv[(int64_t)(16 * k + i) * LP + c0 + r] = x[j];
                 if (Rinv32) Rinv32[(int64_t)(16 * k + i) * LP + c0 + r] = (float)x[j];
+                if (Mt) store_pieces(Mt, L2, (int64_t)(c0 + r) * LP + 16 * k + i, (float)x[j]);
             }
         }
         __syncthreads();
@@ -1790,12 +1813,6 @@ template <> struct PG<double> {
     typedef Mfma<double> M;
 };
 
-__device__ __forceinline__ bf16_t f2bf(float x) {  // round to nearest even
-    const uint32_t u = __float_as_uint(x);
-    if ((u & 0x7f800000u) == 0x7f800000u) return (bf16_t)(u >> 16);
-    return (bf16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
-}
-__device__ __forceinline__ float bf2f(bf16_t b) { return __uint_as_float((uint32_t)b << 16); }
 
 template <typename T, int CT>
 __global__ __launch_bounds__(256) void panel_gemm_kernel(const T* __restrict__ In, int64_t rows, int LP,
@@ -2393,7 +2410,7 @@ int chol_variant = 1;
 
 hipError_t launch_chol_wide(const double* G, int l, int LP, double tol, double* R, double* Rinv, float* Rinv32,
                             int* colflag, int* flag, double* work, const int* pred, hipStream_t s, double ill_tol,
-                            int* ill, const double* d0src) {
+                            int* ill, const double* d0src, bf16_t* Mt) {
     if (LP % 16 || LP > 512) return hipErrorInvalidValue;
     // LP = 256: chol_wide_kernel (its wave-0 look-ahead overlaps the diagonal factor with the other waves'
     // updates; the register-resident kernel spills there, 174 vs 161 us measured); LP <= 128: chol_reg_kernel
@@ -2412,7 +2429,7 @@ hipError_t launch_chol_wide(const double* G, int l, int LP, double tol, double* 
                            s, G, l, LP, tol, work, R, Rinv, colflag, flag, pred, ill_tol, ill, d0src);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(rinv_wide_kernel, dim3(LP / 16), dim3(256), 0, s, LP, R, Rinv, Rinv32, pred);
+    hipLaunchKernelGGL(rinv_wide_kernel, dim3(LP / 16), dim3(256), 0, s, LP, R, Rinv, Rinv32, pred, Mt);
     return hipGetLastError();
 }
 
@@ -2427,25 +2444,23 @@ __global__ void chol2_prep_kernel(const double* __restrict__ G, int B, double* _
     Sb[i * B + c] = G[(int64_t)(B + i) * LP + B + c];
     if (c == 0) d0b[i] = d0src ? d0src[B + i] : G[(int64_t)(B + i) * LP + B + i];
 }
-// rows of R12 (row-major, ld 2 B) whose first-level pivot broke down are zero, as the one-level
-// factor's strips are
-__global__ void chol2_zero_rows_kernel(double* __restrict__ R12, int B, const int* __restrict__ colflag) {
-    const int i = blockIdx.x, c = threadIdx.x;
-    if (colflag[i]) R12[(int64_t)i * 2 * B + c] = 0.0;
-}
 // R / Rinv (2B x 2B row-major) from the level blocks; Rinv32 the fp32 copy; ill = ill1 | ill2
 __global__ void chol2_assemble_kernel(const double* __restrict__ R11, const double* __restrict__ Ri11,
                                       const double* __restrict__ R22, const double* __restrict__ Ri22, int B,
                                       double* __restrict__ R, double* __restrict__ Rinv, float* __restrict__ Rinv32,
-                                      const int* __restrict__ ill2, int* __restrict__ ill) {
+                                      const int* __restrict__ ill2, int* __restrict__ ill, bf16_t* __restrict__ Mt) {
     const int i = blockIdx.x, c = threadIdx.x;  // 2B x B: columns c and c + B of row i
-    const int64_t o = (int64_t)i * 2 * B;
+    const int64_t o = (int64_t)i * 2 * B, L2 = (int64_t)4 * B * B;
     if (i < B) {
         R[o + c] = R11[i * B + c];
         Rinv[o + c] = Ri11[i * B + c];
         if (Rinv32) {
             Rinv32[o + c] = (float)Ri11[i * B + c];
             Rinv32[o + B + c] = (float)Rinv[o + B + c];
+        }
+        if (Mt) {
+            store_pieces(Mt, L2, (int64_t)c * 2 * B + i, (float)Ri11[i * B + c]);
+            store_pieces(Mt, L2, (int64_t)(B + c) * 2 * B + i, (float)Rinv[o + B + c]);
         }
     } else {
         const int i2 = i - B;
@@ -2456,6 +2471,10 @@ __global__ void chol2_assemble_kernel(const double* __restrict__ R11, const doub
         if (Rinv32) {
             Rinv32[o + c] = 0.f;
             Rinv32[o + B + c] = (float)Ri22[i2 * B + c];
+        }
+        if (Mt) {
+            store_pieces(Mt, L2, (int64_t)c * 2 * B + i, 0.0f);
+            store_pieces(Mt, L2, (int64_t)(B + c) * 2 * B + i, (float)Ri22[i2 * B + c]);
         }
     }
     if (ill && i == 0 && c == 0 && *ill2) *ill = 1;
@@ -2469,10 +2488,12 @@ __global__ void chol2_assemble_kernel(const double* __restrict__ R11, const doub
 // was a 16-deep dependent MFMA chain per accumulator behind L2 loads, 24 us per 256^3 product); the
 // wave partials are summed through LDS in wave order.
 constexpr int kGemmSqWaves = 4;
+// zrow (nullable): output rows i with zrow[i] != 0 are written as zeros (R12's broken-down rows).
 __global__ __launch_bounds__(64 * kGemmSqWaves) void gemmsq_f64_kernel(int N, int ta, double alpha,
                                                                        const double* __restrict__ A, int lda,
                                                                        const double* __restrict__ B, int ldb,
-                                                                       double beta, double* __restrict__ C, int ldc) {
+                                                                       double beta, double* __restrict__ C, int ldc,
+                                                                       const int* __restrict__ zrow) {
     __shared__ double part[kGemmSqWaves - 1][4][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 15, h = lane >> 4;
     const int nt = N / 16;
@@ -2503,15 +2524,15 @@ __global__ __launch_bounds__(64 * kGemmSqWaves) void gemmsq_f64_kernel(int N, in
         for (int q = 0; q < kGemmSqWaves - 1; ++q) v[j] += part[q][j][lane];
         double* c = C + (int64_t)(i0 + MD::row(h, j)) * ldc + j0 + r;
         const double o = alpha * v[j];
-        *c = beta == 0.0 ? o : o + beta * *c;
+        *c = (zrow && zrow[i0 + MD::row(h, j)]) ? 0.0 : (beta == 0.0 ? o : o + beta * *c);
     }
 }
 
 static hipError_t gemm_sq(int N, int ta, double alpha, const double* A, int lda, const double* B, int ldb, double beta,
-                          double* C, int ldc, hipStream_t s) {
+                          double* C, int ldc, hipStream_t s, const int* zrow = nullptr) {
     if (N % (16 * kGemmSqWaves)) return hipErrorInvalidValue;
     hipLaunchKernelGGL(gemmsq_f64_kernel, dim3((N / 16) * (N / 16)), dim3(64 * kGemmSqWaves), 0, s, N, ta, alpha, A, lda,
-                       B, ldb, beta, C, ldc);
+                       B, ldb, beta, C, ldc, zrow);
     return hipGetLastError();
 }
 
@@ -2534,7 +2555,8 @@ static hipError_t chol_level(const double* G, int l, int LP, double tol, double*
 
 hipError_t launch_chol_wide_2level(const double* G, int l, int LP, double tol, double* R, double* Rinv,
                                    float* Rinv32, int* colflag, int* flag, double* work, double* scratch,
-                                   hipStream_t s, double ill_tol, int* ill, const double* d0src, int depth) {
+                                   hipStream_t s, double ill_tol, int* ill, const double* d0src, int depth,
+                                   bf16_t* Mt) {
     if ((LP != 256 && LP != 512) || l <= LP / 2 || l > LP) return hipErrorInvalidValue;
     const int B = LP / 2, B2 = B * B;
     double *Ga = scratch, *R11 = Ga + B2, *Ri11 = R11 + B2, *Sb = Ri11 + B2, *R22 = Sb + B2, *Ri22 = R22 + B2,
@@ -2548,9 +2570,9 @@ hipError_t launch_chol_wide_2level(const double* G, int l, int LP, double tol, d
     // level 1: R11, Ri11 = chol(G11) (columns 0 .. B - 1 of colflag)
     e = chol_level(Ga, B, B, tol, R11, Ri11, colflag, flag, work, inner, s, ill_tol, ill, d0src, sub);
     if (e != hipSuccess) return e;
-    // R12 = Ri11^T G12 -> R[:B, B:] (ld LP), broken-down rows zeroed
-    if ((e = gemm_sq(B, 1, 1.0, Ri11, B, G + B, LP, 0.0, R + B, LP, s)) != hipSuccess) return e;
-    hipLaunchKernelGGL(chol2_zero_rows_kernel, dim3(B), dim3(B), 0, s, R + B, B, colflag);
+    // R12 = Ri11^T G12 -> R[:B, B:] (ld LP); the rows whose first-level pivot broke down are zero, as
+    // the one-level factor's strips are (written so by the product's epilogue)
+    if ((e = gemm_sq(B, 1, 1.0, Ri11, B, G + B, LP, 0.0, R + B, LP, s, colflag)) != hipSuccess) return e;
     // S = G22 - R12^T R12
     if ((e = gemm_sq(B, 1, -1.0, R + B, LP, R + B, LP, 1.0, Sb, B, s)) != hipSuccess) return e;
     // level 2 on the l - B valid columns of S, tested against diag(G22) (or the caller's d0src)
@@ -2561,7 +2583,7 @@ hipError_t launch_chol_wide_2level(const double* G, int l, int LP, double tol, d
     if ((e = gemm_sq(B, 0, 1.0, R + B, LP, Ri22, B, 0.0, T, B, s)) != hipSuccess) return e;
     if ((e = gemm_sq(B, 0, -1.0, Ri11, B, T, B, 0.0, Rinv + B, LP, s)) != hipSuccess) return e;
     hipLaunchKernelGGL(chol2_assemble_kernel, dim3(LP), dim3(B), 0, s, R11, Ri11, R22, Ri22, B, R, Rinv, Rinv32,
-                       ill2, ill);
+                       ill2, ill, Mt);
     return hipGetLastError();
 }
 
@@ -2579,14 +2601,16 @@ static int panel_split_variant() {
 
 template <typename T>
 hipError_t launch_panel_gemm(const T* In, int64_t rows, int LP, const T* Mm, int upper, T* Out, int64_t ldo,
-                             int cols, bf16_t* hi, bf16_t* lo, const int* pred, hipStream_t s, bf16_t* msplit) {
+                             int cols, bf16_t* hi, bf16_t* lo, const int* pred, hipStream_t s, bf16_t* msplit,
+                             bool msplit_ready) {
     if (!Mm || LP % 16 || (!Out && (ldo != 0 || !hi))) return hipErrorInvalidValue;
     const int64_t rb = (rows + 63) / 64;
     if constexpr (sizeof(T) == 4) {
         if (msplit && LP % 32 == 0 && LP >= 128) {  // the bf16-split product (panel_split_kernel)
             const int64_t L2 = (int64_t)LP * LP;
-            hipLaunchKernelGGL(split_mat_kernel, dim3((unsigned)std::min<int64_t>((L2 + 255) / 256, 1024)), dim3(256), 0,
-                               s, reinterpret_cast<const float*>(Mm), LP, msplit);
+            if (!msplit_ready)  // (else the factor that wrote M's fp32 copy wrote its pieces too)
+                hipLaunchKernelGGL(split_mat_kernel, dim3((unsigned)std::min<int64_t>((L2 + 255) / 256, 1024)), dim3(256),
+                                   0, s, reinterpret_cast<const float*>(Mm), LP, msplit);
 #define PSPLIT(RT2, CT)                                                                                        \
     {                                                                                                          \
         const int ncb = (LP + CT - 1) / CT;                                                                    \
@@ -2666,7 +2690,7 @@ hipError_t launch_convert_scale(const double* x, T* y, int n, double sc, hipStre
     template hipError_t launch_gram_wide<T>(const T*, const T*, int64_t, int, const GramPlan&, double*, double*,    \
                                             const int*, hipStream_t);                                               \
     template hipError_t launch_panel_gemm<T>(const T*, int64_t, int, const T*, int, T*, int64_t, int, bf16_t*,      \
-                                             bf16_t*, const int*, hipStream_t, bf16_t*);                            \
+                                             bf16_t*, const int*, hipStream_t, bf16_t*, bool);                      \
     template hipError_t launch_repair_panel<T>(const T*, int64_t, int, int, const int*, const int*, uint64_t,       \
                                                int64_t, int64_t, int64_t, T*, hipStream_t, int64_t);                \
     template hipError_t launch_split_bf16<T>(const T*, int64_t, int, bf16_t*, bf16_t*, hipStream_t);
