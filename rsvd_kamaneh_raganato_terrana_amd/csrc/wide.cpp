@@ -132,7 +132,8 @@ struct WideLayout {
         off_JX = take(sizeof(double) * std::max<size_t>(2 * L2, LP >= 256 ? chol_2level_scratch_doubles(LP, 1) : 0));
         off_JJ = take(sizeof(double) * 2 * L2);
         off_M32 = take(sizeof(float) * 3 * L2);  // Rinv, Uw, Vw in fp32 (panel_gemm operand for fp32 panels)
-        off_MS = take(sizeof(T) == 4 ? sizeof(bf16_t) * 3 * L2 : 0);  // the three bf16 pieces of panel_gemm's M
+        // the three bf16 pieces of panel_gemm's M (twice: U_w's and V_w's for the two final products)
+        off_MS = take(sizeof(T) == 4 ? sizeof(bf16_t) * 6 * L2 : 0);
         off_colflag = take(sizeof(int) * LP);
         off_sync = take(sizeof(unsigned) * kBJSyncWords);
         // the eigensolver's small SVD (fp32 results, 128 <= LP <= 512: wide_eig.hip)
@@ -490,22 +491,30 @@ struct WideEngine {
                                                 sizeof(T) == 4 ? 1e-8 : 1e-16, sizeof(T) == 4 ? kBJTolF32 : kBJTolF64,
                                                 bjg));
         }
-        RSVD_CK(launch_convert_scale<T>(Sd, S, L.l, std::fabs(a_scale(d)), s));
-        if (sizeof(T) == 4) {
-            const int L2 = L.LP * L.LP;
-            RSVD_CK(launch_convert_scale<float>(Uw, Uw32, L2, 1.0, s));
-            RSVD_CK(launch_convert_scale<float>(Vw, Vw32, L2, 1.0, s));
+        // U_w / V_w pieces for the split final products, written with their fp32 copies and S (one launch)
+        bf16_t* mu = (ms() && L.LP >= 128) ? Ms : nullptr;
+        bf16_t* mv = mu ? Ms + (size_t)3 * L.LP * L.LP : nullptr;
+        if (sizeof(T) == 4 && mu) {
+            RSVD_CK(launch_finish_convert(Sd, reinterpret_cast<float*>(S), L.l, std::fabs(a_scale(d)), Uw, Uw32, mu, Vw,
+                                          Vw32, mv, L.LP, s));
+        } else {
+            RSVD_CK(launch_convert_scale<T>(Sd, S, L.l, std::fabs(a_scale(d)), s));
+            if (sizeof(T) == 4) {
+                const int L2 = L.LP * L.LP;
+                RSVD_CK(launch_convert_scale<float>(Uw, Uw32, L2, 1.0, s));
+                RSVD_CK(launch_convert_scale<float>(Vw, Vw32, L2, 1.0, s));
+            }
         }
         RSVD_CK(launch_panel_gemm<T>(Qm, L.m, L.LP, mat(Uw, Uw32), 0, reinterpret_cast<T*>(U), ldu, L.l, nullptr,
-                                     nullptr, nullptr, s, ms()));
+                                     nullptr, nullptr, s, mu ? mu : ms(), mu != nullptr));
         if (nsh) {  // V rows of this shard as a panel (in Zn, free by now), all-gathered, then V
             RSVD_CK(launch_panel_gemm<T>(Xn + c0 * L.LP, L.nc, L.LP, mat(Vw, Vw32), 0, Zn + c0 * L.LP, 0, 0, nullptr,
-                                         nullptr, nullptr, s, ms()));
+                                         nullptr, nullptr, s, mv ? mv : ms(), mv != nullptr));
             RSVD_TRY(collective(RSVD_COLL_ALL_GATHER, Zn + c0 * L.LP, Zn, L.nc * L.LP, tdt()));
             RSVD_CK(launch_panel_to_colmajor<T>(Zn, L.n, L.l, L.LP, reinterpret_cast<T*>(V), ldv, s));
         } else {
             RSVD_CK(launch_panel_gemm<T>(Xn, L.n, L.LP, mat(Vw, Vw32), 0, reinterpret_cast<T*>(V), ldv, L.l, nullptr,
-                                         nullptr, nullptr, s, ms()));
+                                         nullptr, nullptr, s, mv ? mv : ms(), mv != nullptr));
         }
         return finish(d, S, V, ldv);
     }

@@ -118,6 +118,10 @@ template <typename T>
 hipError_t launch_panel_gemm(const T* In, int64_t rows, int LP, const T* M, int upper, T* Out, int64_t ldo,
                              int cols, bf16_t* hi, bf16_t* lo, const int* pred, hipStream_t s,
                              bf16_t* msplit = nullptr, bool msplit_ready = false);
+// S = (float)(sc Sd) (l), U_w / V_w (LP x LP fp64) -> fp32 copies and their three bf16 piece images (Mu,
+// Mv: 3 LP^2 each, launch_panel_gemm's msplit with msplit_ready) in one launch
+hipError_t launch_finish_convert(const double* Sd, float* S, int l, double sc, const double* Uw, float* Uw32, bf16_t* Mu,
+                                 const double* Vw, float* Vw32, bf16_t* Mv, int LP, hipStream_t s);
 // y[0..n) = (T)(x * sc)
 template <typename T>
 hipError_t launch_convert_scale(const double* x, T* y, int n, double sc, hipStream_t s);

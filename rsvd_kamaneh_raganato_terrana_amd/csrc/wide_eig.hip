@@ -973,10 +973,11 @@ __global__ __launch_bounds__(256) void wy_apply_kernel(const double* __restrict_
 // the MFMA k order is k0 + 4 h + s (step s, lane half h): the A and B operands only have to agree on
 // it, and then a transposed operand (op = T: contiguous along k) is read as 32-B runs per lane,
 // a plain one (contiguous along i / j) as 128-B rows per 16 lanes.
+// (Cin: the beta term's C when it is not the output, same ld -- C = alpha op(A) op(B) + beta Cin)
 template <int TA, int TB>
 __global__ __launch_bounds__(64) void sqgemm_f64_kernel(int M, int N, int K, double alpha, const double* __restrict__ A,
                                                         int lda, const double* __restrict__ B, int ldb, double beta,
-                                                        double* __restrict__ C, int ldc) {
+                                                        double* C, int ldc, const double* Cin) {
     const int lane = threadIdx.x, r = lane & 15, h = lane >> 4;
     const int tm = (M + 15) / 16;
     const int bi = blockIdx.x % tm, bj = blockIdx.x / tm;
@@ -1017,18 +1018,18 @@ __global__ __launch_bounds__(64) void sqgemm_f64_kernel(int M, int N, int K, dou
         if (ii < M && jv) {
             double* c = C + (int64_t)j * ldc + ii;
             const double v = alpha * (acc0[q] + acc1[q]);
-            *c = beta != 0.0 ? v + beta * *c : v;
+            *c = beta != 0.0 ? v + beta * (Cin ? Cin[(int64_t)j * ldc + ii] : *c) : v;
         }
     }
 }
 
 hipError_t launch_sqgemm(int ta, int tb, int M, int N, int K, double alpha, const double* A, int lda, const double* B,
-                         int ldb, double beta, double* C, int ldc, hipStream_t s) {
+                         int ldb, double beta, double* C, int ldc, hipStream_t s, const double* Cin = nullptr) {
     const dim3 grid(((M + 15) / 16) * ((N + 15) / 16));
 #define SQG(X, Y)                                                                                                    \
     if (ta == X && tb == Y) {                                                                                        \
         hipLaunchKernelGGL((sqgemm_f64_kernel<X, Y>), grid, dim3(64), 0, s, M, N, K, alpha, A, lda, B, ldb, beta, C, \
-                           ldc);                                                                                     \
+                           ldc, Cin);                                                                                \
         return hipGetLastError();                                                                                    \
     }
     SQG(0, 0) SQG(0, 1) SQG(1, 0) SQG(1, 1)
@@ -1045,6 +1046,16 @@ hipError_t launch_tridiag(const double* src, int lds, int n, int off, int kend, 
 }
 
 constexpr int kTailRows = 192;  // phase 2 (one workgroup) takes the last kTailRows rows
+
+// the tridiagonalisation's zeroed inputs in one launch: the reflector matrix Y (n1 doubles), tau (n2),
+// the hand-off counter words (nw)
+__global__ void tri_zero_kernel(double* __restrict__ Y, int64_t n1, double* __restrict__ taus, int n2,
+                                unsigned* __restrict__ ctr, int nw) {
+    const int64_t t0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x, st = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t e = t0; e < n1; e += st) Y[e] = 0.0;
+    for (int64_t e = t0; e < n2; e += st) taus[e] = 0.0;
+    for (int64_t e = t0; e < nw; e += st) ctr[e] = 0u;
+}
 
 }  // namespace
 
@@ -1085,9 +1096,9 @@ hipError_t launch_eig_svd(const double* R, int l, int LP, double* ews, double* X
     // 1. G = W^T W, W = the column-major view of R (ld LP)
     if ((er = launch_sqgemm(1, 0, n, n, n, 1.0, R, LP, R, LP, 0.0, G, LP, s)) != hipSuccess) return er;
     // 2. tridiagonalisation
-    if ((er = hipMemsetAsync(Y, 0, L2 * sizeof(double), s)) != hipSuccess) return er;
-    if ((er = hipMemsetAsync(taus, 0, LP * sizeof(double), s)) != hipSuccess) return er;
-    if ((er = hipMemsetAsync(sync + kTriCtr, 0, 2 * sizeof(unsigned), s)) != hipSuccess) return er;
+    hipLaunchKernelGGL(tri_zero_kernel, dim3((unsigned)std::min<size_t>((L2 + 255) / 256, 1024)), dim3(256), 0, s, Y,
+                       (int64_t)L2, taus, LP, sync + kTriCtr, 2);
+    if ((er = hipGetLastError()) != hipSuccess) return er;
     if (n <= 128) {
         er = launch_tridiag<2, 16, 8, 1>(G, LP, n, 0, n - 2, Y, LP, d, e, taus, nullptr, xch, sync, info, s);
     } else if (n <= kTailRows) {
@@ -1113,17 +1124,17 @@ hipError_t launch_eig_svd(const double* R, int l, int LP, double* ews, double* X
     double* M = scr;
     double* Z2 = scr + L2;
     if ((er = launch_sqgemm(0, 1, n, n, n, 1.0, Z, LP, Z, LP, 0.0, M, LP, s)) != hipSuccess) return er;
-    if ((er = hipMemcpyAsync(Z2, Z, L2 * sizeof(double), hipMemcpyDeviceToDevice, s)) != hipSuccess) return er;
-    if ((er = launch_sqgemm(0, 0, n, n, n, -0.5, M, LP, Z, LP, 1.5, Z2, LP, s)) != hipSuccess) return er;
+    if ((er = launch_sqgemm(0, 0, n, n, n, -0.5, M, LP, Z, LP, 1.5, Z2, LP, s, Z)) != hipSuccess) return er;
     Z = Z2;
     // 5. V_w = Q_H Z into J (buffer 0, column-major LP x LP; columns >= n zero)
-    if ((er = hipMemsetAsync(J, 0, L2 * sizeof(double), s)) != hipSuccess) return er;
+    // (wy_apply writes every row of the n columns; only columns past n need the zeros)
+    if (n < LP && (er = hipMemsetAsync(J, 0, L2 * sizeof(double), s)) != hipSuccess) return er;
     if (nref > 0) hipLaunchKernelGGL(wy_t_kernel, dim3((nref + kWY - 1) / kWY), dim3(256), 0, s, Y, LP, n, nref, taus, Tg);
     hipLaunchKernelGGL(wy_apply_kernel, dim3((n + 15) / 16), dim3(256), (size_t)n * 17 * sizeof(double), s, Y, LP, n,
                        nref, Tg, Z, LP, J, LP);
     if ((er = hipGetLastError()) != hipSuccess) return er;
     // 6. X = W V_w into X (buffer 0, column-major), then the checked block-Jacobi finish
-    if ((er = hipMemsetAsync(X, 0, L2 * sizeof(double), s)) != hipSuccess) return er;
+    if (n < LP && (er = hipMemsetAsync(X, 0, L2 * sizeof(double), s)) != hipSuccess) return er;
     if ((er = launch_sqgemm(0, 0, n, n, n, 1.0, R, LP, J, LP, 0.0, X, LP, s)) != hipSuccess) return er;
     return launch_block_jacobi_given<T>(l, LP, X, J, Uw, Vw, S, sync, info, s, tol_chk);
 }

@@ -2257,6 +2257,25 @@ __global__ void convert_scale_kernel(const double* __restrict__ x, T* __restrict
     if (i < n) y[i] = (T)(x[i] * sc);
 }
 
+// The small SVD's outputs for the fp32 final products in one launch: S (scaled), U_w and V_w in fp32
+// and, for the split panel products, their bf16 piece images (split_mat_kernel's layout)
+__global__ void finish_convert_kernel(const double* __restrict__ Sd, float* __restrict__ S, int l, double sc,
+                                      const double* __restrict__ Uw, float* __restrict__ Uw32, bf16_t* __restrict__ Mu,
+                                      const double* __restrict__ Vw, float* __restrict__ Vw32, bf16_t* __restrict__ Mv,
+                                      int LP) {
+    const int64_t L2 = (int64_t)LP * LP;
+    for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < L2; e += (int64_t)gridDim.x * blockDim.x) {
+        const int k = (int)(e / LP), c = (int)(e - (int64_t)k * LP);
+        const int64_t t = (int64_t)c * LP + k;
+        const float u = (float)Uw[e], v = (float)Vw[e];
+        Uw32[e] = u;
+        Vw32[e] = v;
+        store_pieces(Mu, L2, t, u);
+        store_pieces(Mv, L2, t, v);
+        if (e < l) S[e] = (float)(Sd[e] * sc);
+    }
+}
+
 inline int grid_1d(int64_t work) {
     int64_t g = (work + 255) / 256;
     return (int)(g > 8192 ? 8192 : (g < 1 ? 1 : g));
@@ -2676,6 +2695,14 @@ hipError_t launch_omega_lowp_from(const float* om, int64_t ld, int64_t n, int l,
                                   bf16_t* panel, hipStream_t s) {
     hipLaunchKernelGGL(omega_lowp_from_kernel, dim3(grid_1d(n * LP)), dim3(256), 0, s, om, ld, n, l, LP, round_fp8,
                        panel);
+    return hipGetLastError();
+}
+
+hipError_t launch_finish_convert(const double* Sd, float* S, int l, double sc, const double* Uw, float* Uw32, bf16_t* Mu,
+                                 const double* Vw, float* Vw32, bf16_t* Mv, int LP, hipStream_t s) {
+    const int64_t L2 = (int64_t)LP * LP;
+    hipLaunchKernelGGL(finish_convert_kernel, dim3((unsigned)std::min<int64_t>((L2 + 255) / 256, 1024)), dim3(256), 0, s,
+                       Sd, S, l, sc, Uw, Uw32, Mu, Vw, Vw32, Mv, LP);
     return hipGetLastError();
 }
 
