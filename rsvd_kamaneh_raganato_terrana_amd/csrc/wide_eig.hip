@@ -206,7 +206,7 @@ __global__ __launch_bounds__(kEigThreads) void tridiag_kernel(const double* __re
                                                               double* __restrict__ dvec, double* __restrict__ evec,
                                                               double* __restrict__ taus, double* __restrict__ dump,
                                                               double* __restrict__ xch, unsigned* __restrict__ sync,
-                                                              int* __restrict__ info) {
+                                                              int* __restrict__ info, int noskip) {
     constexpr int G = 64 / LPR;
     constexpr int RPW = 8 * G * RPL;                     // rows per member
     constexpr int XS = NW * RPW + 8 * NW + kEigMaxN;     // one parity's exchange slots: p, v.p partials, row
@@ -441,24 +441,38 @@ __global__ __launch_bounds__(kEigThreads) void tridiag_kernel(const double* __re
             wi[q] = ws[li];
             s[q] = 0.0;
         }
+        // Row slots die in order: slot q holds local rows [8 G NW q, 8 G NW (q + 1)), all dead (< l1)
+        // once 8 G NW (q + 1) <= l1 -- the same for every thread and member.  The loop runs from the
+        // first live slot Q0 (one instantiation per Q0: no per-row branches); a dead row is never read
+        // again (p is masked there, the pivot row and the dump take live rows), and its s stays 0.
+        auto update = [&](auto q0c) {
+            constexpr int Q0 = decltype(q0c)::value;
 #pragma unroll
-        for (int u0 = 0; u0 < CPL; u0 += 4) {
-            constexpr int dummy = 0;
-            (void)dummy;
-            const int u1 = u0 + 4 < CPL ? u0 + 4 : CPL;
-            if (LPR * (u1 - 1) + LPR - 1 > l1) {
+            for (int u0 = 0; u0 < CPL; u0 += 4) {
+                const int u1 = u0 + 4 < CPL ? u0 + 4 : CPL;
+                if (LPR * (u1 - 1) + LPR - 1 > l1) {
 #pragma unroll
-                for (int u = u0; u < u1; ++u) {
-                    const int jj = c + LPR * u;
-                    const double wj = ws[jj], vj = vc[jj], vnj = vnext(jj);
+                    for (int u = u0; u < u1; ++u) {
+                        const int jj = c + LPR * u;
+                        const double wj = ws[jj], vj = vc[jj], vnj = vnext(jj);
 #pragma unroll
-                    for (int q = 0; q < RPL; ++q) {
-                        a[q][u] -= vi[q] * wj + wi[q] * vj;
-                        s[q] += a[q][u] * vnj;
+                        for (int q = Q0; q < RPL; ++q) {
+                            a[q][u] -= vi[q] * wj + wi[q] * vj;
+                            s[q] += a[q][u] * vnj;
+                        }
                     }
                 }
+                asm volatile("" ::: "memory");
             }
-            asm volatile("" ::: "memory");
+        };
+        const int q0 = noskip ? 0 : l1 / (8 * G * NW);  // first slot with a live row
+        if (q0 <= 0) update(std::integral_constant<int, 0>{});
+        else if constexpr (RPL > 1) {
+            if (q0 == 1) update(std::integral_constant<int, 1>{});
+            else if constexpr (RPL > 2) {
+                if (q0 == 2) update(std::integral_constant<int, 2>{});
+                else if constexpr (RPL > 3) update(std::integral_constant<int, 3>{});
+            }
         }
         if (k == n - 3) {  // the last diagonal entry, from its owner
 #pragma unroll
@@ -1041,8 +1055,12 @@ template <int RPL, int CPL, int LPR, int NW>
 hipError_t launch_tridiag(const double* src, int lds, int n, int off, int kend, double* Y, int ldy, double* d, double* e,
                           double* taus, double* dump, double* xch, unsigned* sync, int* info, hipStream_t s) {
     static_assert(8 * (64 / LPR) * RPL * NW <= kEigMaxN && LPR * CPL <= kEigMaxN, "tridiag layout");
+    static const int noskip = [] {  // RSVD_TRI_NOSKIP=1 (A/B): update the dead row slots too
+        const char* v = std::getenv("RSVD_TRI_NOSKIP");
+        return v ? std::atoi(v) : 0;
+    }();
     return launch_coresident(tridiag_kernel<RPL, CPL, LPR, NW>, dim3(NW), dim3(kEigThreads), 0, s, src, lds, n, off,
-                             kend, Y, ldy, d, e, taus, dump, xch, sync, info);
+                             kend, Y, ldy, d, e, taus, dump, xch, sync, info, noskip);
 }
 
 constexpr int kTailRows = 192;  // phase 2 (one workgroup) takes the last kTailRows rows
