@@ -465,14 +465,11 @@ __global__ __launch_bounds__(kEigThreads) void tridiag_kernel(const double* __re
                 asm volatile("" ::: "memory");
             }
         };
-        const int q0 = noskip ? 0 : l1 / (8 * G * NW);  // first slot with a live row
-        if (q0 <= 0) update(std::integral_constant<int, 0>{});
+        // (the three-slot phase-2 shape keeps the one instantiation: a second one spilled it)
+        const int q0 = (noskip || RPL > 2) ? 0 : l1 / (8 * G * NW);  // first slot with a live row
+        if (RPL > 2 || q0 <= 0) update(std::integral_constant<int, 0>{});
         else if constexpr (RPL > 1) {
             if (q0 == 1) update(std::integral_constant<int, 1>{});
-            else if constexpr (RPL > 2) {
-                if (q0 == 2) update(std::integral_constant<int, 2>{});
-                else if constexpr (RPL > 3) update(std::integral_constant<int, 3>{});
-            }
         }
         if (k == n - 3) {  // the last diagonal entry, from its owner
 #pragma unroll
@@ -626,6 +623,8 @@ __device__ __forceinline__ double unit_hash(uint64_t x) {
 // store waits for it: the solve loops read the operands of the NEXT 8 steps before storing the
 // current 8, and the factorisation's multipliers come from a Newton reciprocal, not a division.
 
+constexpr int kInvitSets = 4;  // register sets of the solves' operand ring (3 chunks of 8 steps ahead)
+
 __global__ __launch_bounds__(64) void tridiag_invit_kernel(const double* __restrict__ dg, const double* __restrict__ eg,
                                                            const double* __restrict__ lam, const double* __restrict__ tnorm,
                                                            int n, int ldz, double* __restrict__ Z,
@@ -667,92 +666,108 @@ __global__ __launch_bounds__(64) void tridiag_invit_kernel(const double* __restr
     }
     U0i[at(n - 1)] = pivot_inv(cd);
     X[at(n - 1)] = yc;
-    // back substitution U z = y (z into X): max |z| and sum z^2
+    // back substitution U z = y (z into X): max |z| and sum z^2.  The operands are read in chunks of
+    // 8 steps through a ring of kInvitSets register sets, kInvitSets - 1 chunks ahead of the chunk being
+    // solved (one chunk ahead left one memory round trip exposed per 8 steps -- the solves were
+    // latency-bound).  Only whole chunks go through the ring, with unpredicated loads (a chunk past
+    // the end reads clamped rows it never uses): per-element guards there turned every chunk into
+    // branches and full vmcnt drains.  The last n % 8 steps run on their own; the arithmetic is
+    // unchanged, step by step.
+    constexpr int NS = kInvitSets;
     auto back = [&](double& norm2) {
         double z1 = 0.0, z2 = 0.0, zmax = 0.0, nn = 0.0;
-        double xa[8], ua[8], va[8], ia[8], xb[8], ub[8], vb2[8], ib[8];
-        auto load = [&](int i0, double (&x)[8], double (&u1)[8], double (&u2)[8], double (&ui)[8]) {
+        double xr[NS][8], u1r[NS][8], u2r[NS][8], uir[NS][8];
+        const int nfull = n / 8;  // whole chunks; chunk c: rows n - 1 - 8 c down to n - 8 - 8 c
+        auto load = [&](int c, auto sc) {
+            constexpr int st = decltype(sc)::value;
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
-                const int i = i0 - u;
-                if (i >= 0) {
-                    x[u] = X[at(i)];
-                    u1[u] = U1[at(i)];
-                    u2[u] = U2[at(i)];
-                    ui[u] = U0i[at(i)];
-                }
+                const int i = max(n - 1 - 8 * c - u, 0);
+                xr[st][u] = X[at(i)];
+                u1r[st][u] = U1[at(i)];
+                u2r[st][u] = U2[at(i)];
+                uir[st][u] = U0i[at(i)];
             }
         };
-        load(n - 1, xa, ua, va, ia);
-        for (int i0 = n - 1; i0 >= 0; i0 -= 16) {
-            if (i0 - 8 >= 0) load(i0 - 8, xb, ub, vb2, ib);
+        auto step = [&](int i, double x, double u1, double u2, double ui) {
+            const double z = (x - u1 * z1 - u2 * z2) * ui;
+            X[at(i)] = z;
+            zmax = fmax(zmax, fabs(z));
+            nn += z * z;
+            z2 = z1;
+            z1 = z;
+        };
+        auto chunk = [&](int c, auto sc) {
+            constexpr int st = decltype(sc)::value;
+            load(c + NS - 1, std::integral_constant<int, (st + NS - 1) % NS>{});
+            const int i0 = n - 1 - 8 * c;
 #pragma unroll
-            for (int u = 0; u < 8; ++u)
-                if (i0 - u >= 0) {
-                    const double z = (xa[u] - ua[u] * z1 - va[u] * z2) * ia[u];
-                    X[at(i0 - u)] = z;
-                    zmax = fmax(zmax, fabs(z));
-                    nn += z * z;
-                    z2 = z1;
-                    z1 = z;
-                }
-            if (i0 - 8 < 0) break;
-            if (i0 - 16 >= 0) load(i0 - 16, xa, ua, va, ia);
-#pragma unroll
-            for (int u = 0; u < 8; ++u)
-                if (i0 - 8 - u >= 0) {
-                    const double z = (xb[u] - ub[u] * z1 - vb2[u] * z2) * ib[u];
-                    X[at(i0 - 8 - u)] = z;
-                    zmax = fmax(zmax, fabs(z));
-                    nn += z * z;
-                    z2 = z1;
-                    z1 = z;
-                }
+            for (int u = 0; u < 8; ++u) step(i0 - u, xr[st][u], u1r[st][u], u2r[st][u], uir[st][u]);
+        };
+        load(0, std::integral_constant<int, 0>{});
+        load(1, std::integral_constant<int, 1>{});
+        load(2, std::integral_constant<int, 2>{});
+        int c = 0;
+        for (; c + NS <= nfull; c += NS) {
+            chunk(c, std::integral_constant<int, 0>{});
+            chunk(c + 1, std::integral_constant<int, 1>{});
+            chunk(c + 2, std::integral_constant<int, 2>{});
+            chunk(c + 3, std::integral_constant<int, 3>{});
         }
+        if (c < nfull) chunk(c++, std::integral_constant<int, 0>{});
+        if (c < nfull) chunk(c++, std::integral_constant<int, 1>{});
+        if (c < nfull) chunk(c++, std::integral_constant<int, 2>{});
+        for (int i = n - 1 - 8 * c; i >= 0; --i) step(i, X[at(i)], U1[at(i)], U2[at(i)], U0i[at(i)]);
         norm2 = nn;
         return zmax;
     };
     double nn;
     const double zmax = back(nn);
-    // pass 3: forward elimination of sc x (in place), sc = 1 / max |x|
+    // pass 3: forward elimination of sc x (in place), sc = 1 / max |x| (the same ring, whole chunks)
     const double sc = zmax > 0.0 ? 1.0 / zmax : 1.0;
-    {
+    if (n > 1) {
         double ycur = X[at(0)] * sc;
-        double xa[8], la[8], pa[8], xb[8], lb[8], pb[8];
-        auto load = [&](int i0, double (&x)[8], double (&l)[8], double (&pv)[8]) {
+        double xr[NS][8], lr[NS][8], pr[NS][8];
+        const int nfull = (n - 1) / 8;  // whole chunks; chunk c: steps i = 8 c .. 8 c + 7 (i < n - 1)
+        auto load = [&](int c, auto sc_) {
+            constexpr int st = decltype(sc_)::value;
 #pragma unroll
             for (int u = 0; u < 8; ++u) {
-                const int i = i0 + u;
-                if (i < n - 1) {
-                    x[u] = X[at(i + 1)];
-                    l[u] = Lm[at(i)];
-                    pv[u] = Pv[at(i)];
-                }
+                const int i = min(8 * c + u, n - 2);
+                xr[st][u] = X[at(i + 1)];
+                lr[st][u] = Lm[at(i)];
+                pr[st][u] = Pv[at(i)];
             }
         };
-        auto step = [&](int i, double xn, double lmv, double pvv) {
-            const double yn = xn * sc;
-            if (pvv != 0.0) {
-                X[at(i)] = yn;
-                ycur = ycur - lmv * yn;
-            } else {
-                X[at(i)] = ycur;
-                ycur = yn - lmv * ycur;
-            }
+        auto step = [&](int i, double x, double l, double p) {
+            const double yn = x * sc;
+            const bool pv = p != 0.0;
+            X[at(i)] = pv ? yn : ycur;
+            ycur = pv ? ycur - l * yn : yn - l * ycur;
         };
-        load(0, xa, la, pa);
-        for (int i0 = 0; i0 < n - 1; i0 += 16) {
-            if (i0 + 8 < n - 1) load(i0 + 8, xb, lb, pb);
+        auto chunk = [&](int c, auto sc_) {
+            constexpr int st = decltype(sc_)::value;
+            load(c + NS - 1, std::integral_constant<int, (st + NS - 1) % NS>{});
 #pragma unroll
-            for (int u = 0; u < 8; ++u)
-                if (i0 + u < n - 1) step(i0 + u, xa[u], la[u], pa[u]);
-            if (i0 + 8 >= n - 1) break;
-            if (i0 + 16 < n - 1) load(i0 + 16, xa, la, pa);
-#pragma unroll
-            for (int u = 0; u < 8; ++u)
-                if (i0 + 8 + u < n - 1) step(i0 + 8 + u, xb[u], lb[u], pb[u]);
+            for (int u = 0; u < 8; ++u) step(8 * c + u, xr[st][u], lr[st][u], pr[st][u]);
+        };
+        load(0, std::integral_constant<int, 0>{});
+        load(1, std::integral_constant<int, 1>{});
+        load(2, std::integral_constant<int, 2>{});
+        int c = 0;
+        for (; c + NS <= nfull; c += NS) {
+            chunk(c, std::integral_constant<int, 0>{});
+            chunk(c + 1, std::integral_constant<int, 1>{});
+            chunk(c + 2, std::integral_constant<int, 2>{});
+            chunk(c + 3, std::integral_constant<int, 3>{});
         }
+        if (c < nfull) chunk(c++, std::integral_constant<int, 0>{});
+        if (c < nfull) chunk(c++, std::integral_constant<int, 1>{});
+        if (c < nfull) chunk(c++, std::integral_constant<int, 2>{});
+        for (int i = 8 * c; i < n - 1; ++i) step(i, X[at(i + 1)], Lm[at(i)], Pv[at(i)]);
         X[at(n - 1)] = ycur;
+    } else {
+        X[at(0)] = X[at(0)] * sc;
     }
     back(nn);
     const double f = nn > 0.0 ? 1.0 / sqrt(nn) : 0.0;
