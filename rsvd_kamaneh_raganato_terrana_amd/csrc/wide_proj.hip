@@ -1420,6 +1420,200 @@ __global__ __launch_bounds__(512) void wproj3tn4_kernel(const uint8_t* __restric
         }
 }
 
+// v3 NN for e4m3 A (C5's NN products, LP = 512 as two 256-column halves).  The v2 e4m3 NN spent
+// 114 VALU per 64 MFMA (the XOR-swizzled S and A addresses rebuilt per tile and step); here S uses
+// v3's placed row images (per-lane bases + immediate tile offsets, as wproj3_kernel) and A keeps
+// v2's [32 k][256 i] byte image with its conflict-free unit swizzle (unit c of row k at c ^ (k & 15))
+// -- the tile index sits inside that XOR, so each lane keeps one base per 16-row tile (four VGPRs,
+// fixed for the launch; one v_add each per step).  A lane's fragment is ds_read_b64_tr_b8 of k rows
+// 8 h .. 8 h + 7 of its column, widened to bf16 exactly.  Rings: A NA x 8 KiB (read DA = NA - 1
+// steps ahead), S 2 x (hi + lo) images.  Same k order and MFMA order as v2: bit-identical.
+template <bool SPLIT>
+__global__ __launch_bounds__(512) void wproj3nn8_kernel(const uint8_t* __restrict__ A, int64_t lda, int64_t rows_out,
+                                                        int64_t K, int64_t arows, const bf16_t* __restrict__ Shi,
+                                                        const bf16_t* __restrict__ Slo, float* __restrict__ out,
+                                                        int64_t slab_stride, int64_t kchunk, int nrowblk, int s_pitch,
+                                                        int o_pitch, int halves) {
+    constexpr int LP = 256;
+    typedef W3Shape<LP, false, SPLIT, 1> SH;
+    typedef typename SH::SImg SImg;
+    constexpr int WR = SH::WR, G = SH::G, WI = SH::WI, NS = SH::NS;
+    constexpr int AIMG = KS * WI;  // 8 KiB: one 1-KiB piece per wave
+    static_assert(AIMG == 8 * 1024, "one A piece per wave");
+    constexpr int NA0 = (163840 - 2 * SH::SSLOT) / AIMG;
+    constexpr int NA = NA0 > 8 ? 8 : NA0, DA = NA - 1;
+    constexpr int SBASE = NA * AIMG;
+    extern __shared__ __attribute__((aligned(1024))) char smem_raw[];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int r = lane & 15, h = lane >> 4, q = r >> 2, p = r & 3;
+    const int wr = w % WR, wc = w / WR;
+    const int bid2 = xcd_remap(blockIdx.x, gridDim.x);  // halves: as wproj2_kernel
+    const int hf = bid2 % halves, bid = bid2 / halves;
+    if (hf) {
+        Shi += 256 * hf;
+        if (Slo) Slo += 256 * hf;
+        out += 256 * hf;
+    }
+    const int rb = bid % nrowblk, sp = bid / nrowblk;
+    const int64_t row0 = (int64_t)rb * WI;
+    const int64_t kbeg = (int64_t)sp * kchunk;
+    const int64_t kend = (kbeg + kchunk < K) ? kbeg + kchunk : K;
+    const int nsteps = (int)((kend - kbeg + KS - 1) / KS);
+
+    int32_t soff[SH::SPW];
+#pragma unroll
+    for (int t = 0; t < SH::SPW; ++t) {
+        constexpr int LPR = 64 / SImg::RP;
+        const int pc = t * 8 + w;
+        soff[t] = SImg::row_of(pc, lane / LPR) * s_pitch + 8 * (lane % LPR);
+    }
+    // A piece w: LDS units u = 64 w + lane -> k row u / 16, unit cp = u % 16 holding source rows
+    // row0 + 16 (cp ^ (k & 15)) .. + 15 of A column k0 + k
+    const int ka = (w * 64 + lane) >> 4, cpa = lane & 15;
+    int64_t ia = row0 + 16 * (cpa ^ (ka & 15));
+    ia = (ia + 16 <= arows) ? ia : arows - 16;
+    auto issueS = [&](int st) {
+        char* slot = smem_raw + SBASE + (st & 1) * SH::SSLOT;
+        const int64_t k0 = kbeg + (int64_t)st * KS;
+#pragma unroll
+        for (int a = 0; a < NS; ++a) {
+            const bf16_t* S = (a ? Slo : Shi) + k0 * s_pitch;
+#pragma unroll
+            for (int t = 0; t < SH::SPW; ++t) glds16(S + soff[t], slot + a * SH::SIMG + (t * 8 + w) * SImg::PITCH);
+        }
+    };
+    auto issueA = [&](int st) {
+        int64_t kk = kbeg + (int64_t)st * KS + ka;
+        kk = kk < K ? kk : K - 1;
+        glds16<2>(A + kk * lda + ia, smem_raw + (st % NA) * AIMG + w * 1024);  // read once: non-temporal
+    };
+
+    const int colS = wc * G * 16 + 4 * p;
+    const int k1 = 8 * h + q, k2 = k1 + 4;
+    const uint32_t lS1 = SImg::off(k1) + 2 * colS, lS2 = SImg::off(k2) + 2 * colS;
+    const int kr = 8 * h + (r >> 1);
+    uint32_t lA[RT];
+#pragma unroll
+    for (int t = 0; t < RT; ++t) lA[t] = kr * WI + 16 * ((4 * wr + t) ^ (kr & 15)) + 8 * (r & 1);
+
+    f32x4 acc[RT][G];
+#pragma unroll
+    for (int t = 0; t < RT; ++t)
+#pragma unroll
+        for (int g = 0; g < G; ++g) acc[t][g] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    if (w >= 4) __builtin_amdgcn_s_setprio(1);
+    // prologue: A(0 .. DA - 1) and S(0), in the order the steady-state wait counts
+    for (int i = -DA; i < 0; ++i) {
+        if (i == -1 && nsteps > 0) issueS(0);
+        if (i + DA < nsteps) issueA(i + DA);
+    }
+    const uint32_t lds0 = lds_addr(smem_raw);
+    for (int st = 0; st < nsteps; ++st) {
+        // S(st) and A(st) have landed once at most A(st - 1 + DA), issued behind S(st), is in flight
+        if (st - 1 + DA < nsteps) wait_vm<1>();
+        else wait_vm<0>();
+        __builtin_amdgcn_s_barrier();
+        if (st + 1 < nsteps) issueS(st + 1);
+        if (st + DA < nsteps) issueA(st + DA);
+        const uint32_t sS = lds0 + SBASE + (uint32_t)((st & 1) * SH::SSLOT);
+        const uint32_t sA = lds0 + (uint32_t)((st % NA) * AIMG);
+        const uint32_t bS1 = sS + lS1, bS2 = sS + lS2;
+        auto wait_b = [&](i32x2* b) {
+            if (SPLIT) wait_lgkm0(b[0], b[1], b[2], b[3]);
+            else wait_lgkm0(b[0], b[1]);
+        };
+        i32x2 a2[RT];
+        bf16x8_t af[RT];
+#pragma unroll
+        for (int t = 0; t < RT; ++t) a2[t] = tr8_read_a(sA + lA[t]);
+        auto bread = [&](auto gc, i32x2* b) {
+            constexpr int g = decltype(gc)::value;
+            b[0] = tr_read_o<32 * g>(bS1);
+            b[1] = tr_read_o<32 * g>(bS2);
+            if constexpr (SPLIT) {
+                b[2] = tr_read_o<SH::SIMG + 32 * g>(bS1);
+                b[3] = tr_read_o<SH::SIMG + 32 * g>(bS2);
+            }
+        };
+        i32x2 bb[2][4];
+        bread(std::integral_constant<int, 0>{}, bb[0]);
+        wait_b(bb[0]);
+#pragma unroll
+        for (int t = 0; t < RT; ++t) {
+            wait_lgkm0(a2[t]);
+            af[t] = fp8x8_to_bf16x8(a2[t]);
+        }
+        auto gstep = [&](auto gc) {
+            constexpr int g = decltype(gc)::value;
+            if constexpr (g + 1 < G) bread(std::integral_constant<int, g + 1>{}, bb[(g + 1) & 1]);
+            __builtin_amdgcn_sched_barrier(0);
+            const i32x2* b = bb[g & 1];
+            const bf16x8_t bh = join2(b[0], b[1]);
+#pragma unroll
+            for (int t = 0; t < RT; ++t) acc[t][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[t], bh, acc[t][g], 0, 0, 0);
+            if constexpr (SPLIT) {
+                const bf16x8_t bl = join2(b[2], b[3]);
+#pragma unroll
+                for (int t = 0; t < RT; ++t) acc[t][g] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[t], bl, acc[t][g], 0, 0, 0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (g + 1 < G) wait_b(bb[(g + 1) & 1]);
+        };
+        static_for<G>(gstep);
+    }
+
+    float* dst = out + (int64_t)sp * slab_stride;
+#pragma unroll
+    for (int t = 0; t < RT; ++t)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int64_t row = row0 + wr * 64 + 16 * t + 4 * h + j;
+            if (row < rows_out) {
+#pragma unroll
+                for (int g = 0; g < G; ++g) dst[row * o_pitch + wc * G * 16 + 16 * g + r] = acc[t][g][j];
+            }
+        }
+}
+
+template <bool SPLIT>
+constexpr size_t nn8_lds() {
+    typedef W3Shape<256, false, SPLIT, 1> SH;
+    constexpr int NA0 = (163840 - 2 * SH::SSLOT) / (KS * 256);
+    return (size_t)(NA0 > 8 ? 8 : NA0) * KS * 256 + 2 * (size_t)SH::SSLOT;
+}
+
+// e4m3 NN through wproj3nn8_kernel: LP = 512 as two 256-column halves (merged: one launch)
+template <bool SPLIT>
+hipError_t wproj3nn8_go(const void* A, int64_t lda, int64_t m, int64_t n, const bf16_t* Shi, const bf16_t* Slo,
+                        const WProjPlan& p, float* slabs, float* Out, hipStream_t s, hipEvent_t done) {
+    constexpr size_t lds = nn8_lds<SPLIT>();
+    static_assert(lds <= 163840, "NN8 LDS");
+    const int64_t rows_out = m, K = n;
+    float* o = p.splits == 1 ? Out : slabs;
+    const int64_t stride = rows_out * 512;
+    if (p.merge) {
+        hipLaunchKernelGGL((wproj3nn8_kernel<SPLIT>), dim3(2 * p.blocks * p.splits), dim3(512), lds, s,
+                           reinterpret_cast<const uint8_t*>(A), lda, rows_out, K, m, Shi, Slo, o, stride, p.chunk,
+                           p.blocks, 512, 512, 2);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    } else {
+        for (int hf = 0; hf < 2; ++hf) {
+            hipLaunchKernelGGL((wproj3nn8_kernel<SPLIT>), dim3(p.blocks * p.splits), dim3(512), lds, s,
+                               reinterpret_cast<const uint8_t*>(A), lda, rows_out, K, m, Shi + 256 * hf,
+                               Slo ? Slo + 256 * hf : nullptr, o + 256 * hf, stride, p.chunk, p.blocks, 512, 512, 1);
+            hipError_t e = hipGetLastError();
+            if (e != hipSuccess) return e;
+        }
+    }
+    hipError_t e = hipSuccess;
+    if (done) e = hipEventRecord(done, s);
+    if (e != hipSuccess || p.splits == 1) return e;
+    return launch_sum_slabs<float>(slabs, stride, p.splits, stride, Out, s);
+}
+
 // e4m3 TN through wproj3tn4_kernel: LP = 256 in one dispatch, LP = 512 as two 256-column halves
 // (S columns 256 hf .., pitch 512, into output columns 256 hf ..).
 template <bool SPLIT>
@@ -1804,6 +1998,9 @@ hipError_t wproj_lp(int nn, int fp8, const void* A, int64_t lda, int64_t m, int6
     }
     if constexpr (LP == 512) {
         if (p.v2 && p.half && fp8) {
+            if (nn && p.nn8)
+                return split ? wproj3nn8_go<true>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d)
+                             : wproj3nn8_go<false>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d);
             if (nn) return split ? wproj2_half_go<true, true, true>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d)
                                  : wproj2_half_go<true, true, false>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d);
             return split ? wproj2_half_go<true, false, true>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d)
@@ -1861,6 +2058,14 @@ static int tn128_mode() {  // RSVD_TN128: 0 the v2 double-step LP = 128 TN, 1 ri
     return env;
 }
 
+static bool nn8_enabled() {  // RSVD_NN8=0 in the environment: the v2 e4m3 NN (A/B)
+    static const int env = [] {
+        const char* v = std::getenv("RSVD_NN8");
+        return v ? std::atoi(v) : 1;
+    }();
+    return env != 0;
+}
+
 static bool half_merge_enabled() {
     static const int env = [] {
         const char* v = std::getenv("RSVD_HALF_MERGE");
@@ -1877,6 +2082,7 @@ WProjPlan plan_wproj(int64_t rows_out, int64_t K, int LP, bool v2, bool nn, bool
     p.ds = p.v2 && LP == 128 && !nn && !fp8 && K % 64 == 0;  // double-step TN stages (whole 64-row K chunks)
     p.tn3 = p.ds ? tn128_mode() : 0;
     p.half = p.v2 && fp8 && LP == 512;  // two LP = 256 column halves (wproj2_half_go)
+    p.nn8 = p.half && nn && nn8_enabled();  // ... the e4m3 NN on wproj3nn8_kernel
     // e4m3 TN: four k-steps per A slot (wproj3tn4_kernel; K chunks of whole 128-row slots)
     p.tn4 = p.v2 && fp8 && !nn && (LP == 256 || LP == 512) && tn4_enabled();
     const int WI = p.v2 ? (LP == 128 ? (p.ds ? 256 : 512) : ((LP == 256 || p.half) ? 256 : 128))
