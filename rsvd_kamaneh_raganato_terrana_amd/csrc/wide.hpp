@@ -31,6 +31,7 @@ struct WProjPlan {
     bool v2;         // LDS-DMA pipelined kernel (bf16 / e4m3 A, LP >= 128, 16-B aligned columns)
     bool ds = false; // v2 TN at LP = 128 with two k-steps per stage (128-B A runs; K a multiple of 64)
     int tn3 = 0;      // ds with separate A / S rings (wproj3tn128_kernel): 1 = 4 A / 2 S slots, 2 = 3 / 3 (lab)
+    bool nn3 = false;  // bf16 NN at LP = 128 on wproj3_kernel (RSVD_NN3_128=0: the v2 kernel)
     bool nn8 = false;  // e4m3 NN halves on the v3-style wproj3nn8_kernel (RSVD_NN8=0: the v2 kernel)
     bool v3 = false; // v2 with launch-constant LDS read bases (bf16 A, LP 256 / 512; wide_proj.hip)
     int sd = 1;       // v3: S-panel prefetch distance in k-steps (1 or 2; A runs as far ahead as LDS allows)

@@ -1956,6 +1956,11 @@ hipError_t wproj_lp(int nn, int fp8, const void* A, int64_t lda, int64_t m, int6
                     const bf16_t* Slo, const WProjPlan& p, float* slabs, float* Out, hipStream_t s, hipEvent_t d) {
     const bool split = Slo != nullptr;
     if constexpr (LP == 128) {
+        // the v3 NN at LP = 128 (WI = 512 rows, A 3 / S 2 slots) for the hi / lo products: C3 5.40 ->
+        // 5.35 ms (gpurun_out r6d, bit-identical); the single-pass sketch measured 468 -> 473 us on it
+        // and keeps v2
+        if (p.v2 && nn && !fp8 && p.nn3 && split)
+            return wproj3_go<true, 128, true, 1>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d);
         if (p.v2 && p.ds && !nn && !fp8 && p.tn3)
             return split ? wproj3tn128_go<true>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d)
                          : wproj3tn128_go<false>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d);
@@ -2066,6 +2071,14 @@ static bool nn8_enabled() {  // RSVD_NN8=0 in the environment: the v2 e4m3 NN (A
     return env != 0;
 }
 
+static bool nn3_128_enabled() {  // RSVD_NN3_128=0 in the environment: the v2 bf16 NN at LP = 128 (A/B)
+    static const int env = [] {
+        const char* v = std::getenv("RSVD_NN3_128");
+        return v ? std::atoi(v) : 1;
+    }();
+    return env != 0;
+}
+
 static bool half_merge_enabled() {
     static const int env = [] {
         const char* v = std::getenv("RSVD_HALF_MERGE");
@@ -2081,6 +2094,7 @@ WProjPlan plan_wproj(int64_t rows_out, int64_t K, int LP, bool v2, bool nn, bool
     p.tn2 = p.v3 && !nn && LP == 256;  // two k-steps per A slot: K chunks of whole 64-row pairs
     p.ds = p.v2 && LP == 128 && !nn && !fp8 && K % 64 == 0;  // double-step TN stages (whole 64-row K chunks)
     p.tn3 = p.ds ? tn128_mode() : 0;
+    p.nn3 = p.v2 && LP == 128 && nn && !fp8 && nn3_128_enabled();
     p.half = p.v2 && fp8 && LP == 512;  // two LP = 256 column halves (wproj2_half_go)
     p.nn8 = p.half && nn && nn8_enabled();  // ... the e4m3 NN on wproj3nn8_kernel
     // e4m3 TN: four k-steps per A slot (wproj3tn4_kernel; K chunks of whole 128-row slots)
