@@ -909,13 +909,19 @@ __global__ __launch_bounds__(256) void wy_t_kernel(const double* __restrict__ Y,
 
 // V = Q_H Z for one 16-column block of the row-major Z (ld ldz), held in LDS: blocks of 32
 // reflectors from the last to the first, Z <- Z - Y_b (T_b (Y_b^T Z)) on the fp64 MFMA, Y_b staged
-// through LDS in coalesced 128-row chunks (the next chunk read into registers while the current one
-// is multiplied); then V into the column-major Vout (ld ldv; rows >= n written as zero).
+// through LDS in 128-row chunks; then V into the column-major Vout (ld ldv; rows >= n written as
+// zero).  A whole Y block (rows k0 + 1 .. n - 1, up to kWYCh chunks) lives in registers; both
+// passes over it (Y_b^T Z, then Z -= Y_b M2) put its chunks from there, and pass 2 refills each
+// chunk's registers with the next block's chunk as soon as it has been put, so the loads of block
+// b - 1 (and its T) fly while block b finishes (round 5: one chunk ahead left a round trip
+// exposed per chunk and pass -- 223 us at n = 512; a second register block spilled to AGPRs and
+// drained every load).  Same operations in the same order: bit-identical.
+constexpr int kWYCh = kEigMaxN / kWYRows;  // Y chunks per block, at most
 __global__ __launch_bounds__(256) void wy_apply_kernel(const double* __restrict__ Y, int ld, int n, int nref,
                                                        const double* __restrict__ Tg, const double* __restrict__ Z,
                                                        int ldz, double* __restrict__ Vout, int ldv) {
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
-    constexpr int ZP = 17, YP = kWY + 1;
+    constexpr int ZP = 17, YP = kWY + 1, NV = kWYRows * kWY / 256;
     double* Zs = reinterpret_cast<double*>(smem_raw);  // [n][17]
     __shared__ double Ys[kWYRows * YP];
     __shared__ double Ms[2][kWY][17];
@@ -928,68 +934,113 @@ __global__ __launch_bounds__(256) void wy_apply_kernel(const double* __restrict_
         Zs[i * ZP + c] = c0 + c < n ? Z[(int64_t)i * ldz + c0 + c] : 0.0;
     }
     const int nb = (nref + kWY - 1) / kWY;
-    double v[kWYRows * kWY / 256];
-    for (int b = nb - 1; b >= 0; --b) {
+    double ya[kWYCh][NV];
+    // unpredicated loads: every load is issued before its first use, so the waits count them
+    // (loads under a branch made the compiler drain vmcnt(0) after each one).  Rows past n read row
+    // n - 1 scaled by 0.0 (Y is finite); columns nref .. 32 nb - 1 < LP are zero in Y (tri_zero)
+    auto load_chunk = [&](int b, int c, double (&yc)[NV]) {
+        const int k0 = kWY * b, j0 = k0 + 1;
+#pragma unroll
+        for (int q = 0; q < NV; ++q) {
+            const int e = tid + 256 * q, rr = e % kWYRows, cc = e / kWYRows;
+            const int row = j0 + kWYRows * c + rr;
+            const double x = Y[(int64_t)(k0 + cc) * ld + (row < n ? row : n - 1)];
+            yc[q] = x * (row < n ? 1.0 : 0.0);
+        }
+    };
+    double tsv[kWY * kWY / 256];
+    auto load_t = [&](int b) {
+#pragma unroll
+        for (int q = 0; q < kWY * kWY / 256; ++q) tsv[q] = Tg[(int64_t)b * kWY * kWY + tid + 256 * q];
+    };
+    // block b from ya (loaded while block b + 1 was applied); ya is refilled with block max(b - 1, 0)
+    // chunk by chunk as pass 2 releases it, and tsv with its T
+    auto apply_blk = [&](int b) {
         const int k0 = kWY * b;
         const int j0 = k0 + 1;  // first row any reflector of the block touches
-        for (int e = tid; e < kWY * kWY; e += 256) Ts[e / kWY][e % kWY] = Tg[(int64_t)b * kWY * kWY + e];
+        const int bn = b > 0 ? b - 1 : 0;
+#pragma unroll
+        for (int q = 0; q < kWY * kWY / 256; ++q) {
+            const int e = tid + 256 * q;
+            Ts[e / kWY][e % kWY] = tsv[q];
+        }
         // M = Y_b^T Z (32 x 16): per chunk, wave w -> reflector tile (w & 1), chunk rows half (w >> 1)
         f64x4 acc = MD::zero();
         const int rt = w & 1, half = w >> 1;
-        wy_stage(Y, ld, n, nref, k0, j0, v);
-        for (int r0 = j0; r0 < n; r0 += kWYRows) {
-            __syncthreads();
-            wy_put(Ys, v);
-            __syncthreads();
-            if (r0 + kWYRows < n) wy_stage(Y, ld, n, nref, k0, r0 + kWYRows, v);
+#pragma unroll
+        for (int c = 0; c < kWYCh; ++c) {
+            const int r0 = j0 + kWYRows * c;
+            if (r0 < n) {
+                __syncthreads();
+                wy_put(Ys, ya[c]);
+                __syncthreads();
 #pragma unroll 4
-            for (int j = 64 * half; j < 64 * half + 64; j += 4) {
-                const int row = r0 + j + h;
-                const double av = Ys[(j + h) * YP + 16 * rt + r];
-                const double bv = row < n ? Zs[row * ZP + r] : 0.0;
-                acc = MD::mma(av, bv, acc);
+                for (int j = 64 * half; j < 64 * half + 64; j += 4) {
+                    const int row = r0 + j + h;
+                    const double av = Ys[(j + h) * YP + 16 * rt + r];
+                    const double bv = row < n ? Zs[row * ZP + r] : 0.0;
+                    acc = MD::mma(av, bv, acc);
+                }
             }
         }
 #pragma unroll
         for (int q = 0; q < 4; ++q) Ms[half][16 * rt + MD::row(h, q)][r] = acc[q];
         __syncthreads();
-        // M2 = T_b M (upper triangular T), into Ms[0]
+        // M2 = T_b M (upper triangular T), into Ms[0].  The sum runs over all 32 p, the terms below
+        // the diagonal skipped by a select (the same terms in the same order), so the loop unrolls
+        // and its LDS reads pipeline (the triangular bound left an LDS round trip per term exposed)
         double m2[2];
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
             const int e = tid + 256 * q, rr = e >> 4, cc = e & 15;
             double a = 0.0;
-            for (int p = rr; p < kWY; ++p) a += Ts[rr][p] * (Ms[0][p][cc] + Ms[1][p][cc]);
+#pragma unroll
+            for (int p = 0; p < kWY; ++p) {
+                const double t = Ts[rr][p], mm = Ms[0][p][cc] + Ms[1][p][cc];
+                a = p >= rr ? a + t * mm : a;
+            }
             m2[q] = a;
         }
         __syncthreads();
+        load_t(bn);
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
             const int e = tid + 256 * q;
             Ms[0][e >> 4][e & 15] = m2[q];
         }
         // Z -= Y_b M2: per chunk, wave w -> 16-row tiles w, w + 4 of the 128 chunk rows
-        wy_stage(Y, ld, n, nref, k0, j0, v);
-        for (int r0 = j0; r0 < n; r0 += kWYRows) {
-            __syncthreads();
-            wy_put(Ys, v);
-            __syncthreads();
-            if (r0 + kWYRows < n) wy_stage(Y, ld, n, nref, k0, r0 + kWYRows, v);
 #pragma unroll
-            for (int t = 0; t < 2; ++t) {
-                const int tr = 16 * (w + 4 * t);
-                f64x4 a = MD::zero();
+        for (int c = 0; c < kWYCh; ++c) {
+            const int r0 = j0 + kWYRows * c;
+            if (r0 < n) {
+                __syncthreads();
+                wy_put(Ys, ya[c]);
+                __syncthreads();
+            }
+            load_chunk(bn, c, ya[c]);  // (the put above has read ya[c])
+            if (r0 < n) {
 #pragma unroll
-                for (int s = 0; s < kWY / 4; ++s) a = MD::mma(Ys[(tr + r) * YP + 4 * s + h], Ms[0][4 * s + h][r], a);
+                for (int t = 0; t < 2; ++t) {
+                    const int tr = 16 * (w + 4 * t);
+                    f64x4 a = MD::zero();
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const int row = r0 + tr + MD::row(h, q);
-                    if (row < n) Zs[row * ZP + r] -= a[q];
+                    for (int s = 0; s < kWY / 4; ++s) a = MD::mma(Ys[(tr + r) * YP + 4 * s + h], Ms[0][4 * s + h][r], a);
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const int row = r0 + tr + MD::row(h, q);
+                        if (row < n) Zs[row * ZP + r] -= a[q];
+                    }
                 }
             }
         }
         __syncthreads();
+    };
+    if (nb > 0) {
+#pragma unroll
+        for (int c = 0; c < kWYCh; ++c) load_chunk(nb - 1, c, ya[c]);
+        load_t(nb - 1);
     }
+    for (int b = nb - 1; b >= 0; --b) apply_blk(b);
     for (int c = 0; c < 16; ++c) {
         if (c0 + c >= n) break;
         for (int i = tid; i < ldv; i += 256) Vout[(int64_t)(c0 + c) * ldv + i] = i < n ? Zs[i * ZP + c] : 0.0;
