@@ -137,7 +137,23 @@ __device__ long long g_tri_prof[8];
 #define TRI_DONE() \
     do {           \
     } while (0)
+#define INV_INIT() long long inv_last_ = __builtin_amdgcn_s_memtime()
+#define INV_TS(i)                                                        \
+    do {                                                                 \
+        if (blockIdx.x == 0 && threadIdx.x == 0) {                       \
+            __builtin_amdgcn_s_waitcnt(0);                               \
+            const long long now_ = __builtin_amdgcn_s_memtime();         \
+            g_tri_prof[(i)] += now_ - inv_last_;                         \
+            inv_last_ = now_;                                            \
+        }                                                                \
+    } while (0)
 #else
+#define INV_INIT() \
+    do {           \
+    } while (0)
+#define INV_TS(i) \
+    do {          \
+    } while (0)
 #define TRI_INIT() \
     do {           \
     } while (0)
@@ -629,6 +645,14 @@ __global__ __launch_bounds__(64) void tridiag_invit_kernel(const double* __restr
                                                            const double* __restrict__ lam, const double* __restrict__ tnorm,
                                                            int n, int ldz, double* __restrict__ Z,
                                                            double* __restrict__ scr) {
+    // T's diagonal and off-diagonal in LDS: the factorisation reads d[i + 1], e[i], e[i + 1] every
+    // step, and from global memory each step's loads sat on an L2 round trip
+    __shared__ double sdg[kEigMaxN], seg[kEigMaxN];
+    for (int i = threadIdx.x; i < n; i += 64) {
+        sdg[i] = dg[i];
+        seg[i] = i < n - 1 ? eg[i] : 0.0;
+    }
+    __syncthreads();
     const int k = blockIdx.x * 64 + threadIdx.x;
     if (k >= n) return;
     const int64_t S = (int64_t)n * ldz;
@@ -646,10 +670,12 @@ __global__ __launch_bounds__(64) void tridiag_invit_kernel(const double* __restr
         return 1.0 / u;
     };
     auto rnd = [&](int i) { return unit_hash(((uint64_t)k << 32) ^ (uint64_t)i ^ 0x5EED5EEDull); };
+    INV_INIT();
     // pass 1: factor, forward elimination of the random right-hand side on the fly (y into X)
-    double cd = dg[0] - lk, cu = n > 1 ? eg[0] : 0.0, yc = rnd(0);
+    double cd = sdg[0] - lk, cu = n > 1 ? seg[0] : 0.0, yc = rnd(0);
+#pragma unroll 4
     for (int i = 0; i < n - 1; ++i) {
-        const double bi = eg[i], an = dg[i + 1] - lk, cn = i + 1 < n - 1 ? eg[i + 1] : 0.0, yn = rnd(i + 1);
+        const double bi = seg[i], an = sdg[i + 1] - lk, cn = i + 1 < n - 1 ? seg[i + 1] : 0.0, yn = rnd(i + 1);
         const bool piv = fabs(bi) > fabs(cd);
         const double m = piv ? cd * rcp_f64(bi) : (cd != 0.0 ? bi * rcp_f64(cd) : 0.0);
         U0i[at(i)] = pivot_inv(piv ? bi : cd);
@@ -665,6 +691,7 @@ __global__ __launch_bounds__(64) void tridiag_invit_kernel(const double* __restr
         yc = ycn;
     }
     U0i[at(n - 1)] = pivot_inv(cd);
+    INV_TS(4);
     X[at(n - 1)] = yc;
     // back substitution U z = y (z into X): max |z| and sum z^2.  The operands are read in chunks of
     // 8 steps through a ring of kInvitSets register sets, kInvitSets - 1 chunks ahead of the chunk being
@@ -723,6 +750,7 @@ __global__ __launch_bounds__(64) void tridiag_invit_kernel(const double* __restr
     };
     double nn;
     const double zmax = back(nn);
+    INV_TS(5);
     // pass 3: forward elimination of sc x (in place), sc = 1 / max |x| (the same ring, whole chunks)
     const double sc = zmax > 0.0 ? 1.0 / zmax : 1.0;
     if (n > 1) {
@@ -769,7 +797,9 @@ __global__ __launch_bounds__(64) void tridiag_invit_kernel(const double* __restr
     } else {
         X[at(0)] = X[at(0)] * sc;
     }
+    INV_TS(6);
     back(nn);
+    INV_TS(7);
     const double f = nn > 0.0 ? 1.0 / sqrt(nn) : 0.0;
     for (int i = 0; i < n; i += 8) {
         double xv[8];

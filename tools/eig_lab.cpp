@@ -79,6 +79,8 @@ int main(int argc, char** argv) {
         tri_prof_read(p);
         printf("  tridiag phases (Mcycles, wg 0): A %.3f B %.3f C %.3f D %.3f\n", p[0] * 1e-6, p[1] * 1e-6,
                p[2] * 1e-6, p[3] * 1e-6);
+        printf("  inverse iteration (Mcycles, thread 0): factor %.3f back %.3f forward %.3f back %.3f\n",
+               p[4] * 1e-6, p[5] * 1e-6, p[6] * 1e-6, p[7] * 1e-6);
 #endif
     }
     return 0;
