@@ -1948,8 +1948,21 @@ __global__ void split_mat_kernel(const float* __restrict__ M, int LP, bf16_t* __
 // wrote it in one place before the MFMAs, exposing the L2 latency every step, and transposed
 // column-major outputs through LDS.  Same shape (RT2 = 2, CT = 128), same box: C5 m-side product
 // 454 -> 318 us, n side 51 -> 31 us, C4 74 -> 59 us (C5 31.0 -> 30.1 ms, C3 7.90 -> 7.50 ms).
-template <int RT2, int CT>
-__global__ __launch_bounds__(256) void panel_split_kernel(const float* __restrict__ In, int64_t rows, int LP,
+template <typename F, int... I>
+__device__ __forceinline__ void qr_static_for_impl(F& f, std::integer_sequence<int, I...>) {
+    (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void qr_static_for(F& f) {
+    qr_static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+// PD: In's fragments come through a ring of PD register sets, PD - 1 k-steps ahead (round 5: one
+// step ahead left an HBM round trip exposed in every step of the short LP = 128 products).  The
+// loads are unpredicated so the waits count them: rows past `rows` read the last row again, which
+// only reaches output rows that are never stored (an MFMA output row depends on its A row alone).
+template <int RT2, int CT, int PD = 2>
+__global__ __launch_bounds__(256, 2) void panel_split_kernel(const float* __restrict__ In, int64_t rows, int LP,
                                                           const bf16_t* __restrict__ Mt, int upper,
                                                           float* __restrict__ Out, int64_t ldo, int cols,
                                                           bf16_t* __restrict__ hi, bf16_t* __restrict__ lo, int ncb,
@@ -1990,35 +2003,31 @@ __global__ __launch_bounds__(256) void panel_split_kernel(const float* __restric
             *reinterpret_cast<uint4*>(img + x * IMG + c * 64 + 16 * (un ^ ((c >> 1) & 3))) = mreg[t];
         }
     };
-    // In vectors of this / the next k-step (swapped, never indexed at run time)
-    float4 cur[RT2][2], nxt[RT2][2];
+    // In's fragments (8 consecutive k of the lane's row per row tile), ring of PD sets
+    float4 ab[PD][RT2][2];
     auto loadA = [&](int ks, float4 (&a)[RT2][2]) {
-        const int k = 32 * ks + 8 * h;
+        const int k = 32 * (ks < nk ? ks : nk - 1) + 8 * h;
 #pragma unroll
         for (int t = 0; t < RT2; ++t) {
             const int64_t row = row0 + 16 * RT2 * w + 16 * t + r;
-            if (row < rows && k < LP) {
-                a[t][0] = *reinterpret_cast<const float4*>(In + row * LP + k);
-                a[t][1] = *reinterpret_cast<const float4*>(In + row * LP + k + 4);
-            } else {
-                a[t][0] = a[t][1] = make_float4(0.f, 0.f, 0.f, 0.f);
-            }
+            const float* src = In + (row < rows ? row : rows - 1) * LP + k;
+            a[t][0] = *reinterpret_cast<const float4*>(src);
+            a[t][1] = *reinterpret_cast<const float4*>(src + 4);
         }
     };
     const uint32_t lofs = (uint32_t)(r * 64 + 16 * (h ^ ((r >> 1) & 3)));
     if (nk > 0) {
-        loadA(0, cur);
+#pragma unroll
+        for (int j = 0; j < PD - 1; ++j) loadA(j, ab[j]);
         loadM(0);
         writeM(smem_raw);
     }
-    for (int ks = 0; ks < nk; ++ks) {
+    auto step = [&](int ks, float4 (&cur)[RT2][2], float4 (&ahead)[RT2][2]) __attribute__((always_inline)) {
         const char* img = smem_raw + (ks & 1) * STEPB;
         __syncthreads();  // chunk ks written; the readers of chunk ks - 1 (the other buffer) are done
         const bool more = ks + 1 < nk;
-        if (more) {
-            loadA(ks + 1, nxt);
-            loadM(ks + 1);
-        }
+        loadA(ks + PD - 1, ahead);
+        if (more) loadM(ks + 1);
         // In fragments of this k-step: three pieces of 8 consecutive k of the lane's row, per row tile
         bf16x8s fa[RT2][3];
 #pragma unroll
@@ -2056,11 +2065,22 @@ __global__ __launch_bounds__(256) void panel_split_kernel(const float* __restric
             }
         }
         if (more) writeM(smem_raw + ((ks + 1) & 1) * STEPB);
-#pragma unroll
-        for (int t = 0; t < RT2; ++t) {
-            cur[t][0] = nxt[t][0];
-            cur[t][1] = nxt[t][1];
-        }
+    };
+    // whole groups of PD steps (each set at a fixed position in the ring), then the rest
+    int ks0 = 0;
+    for (; ks0 + PD <= nk; ks0 += PD) {
+        auto one = [&](auto jc) {
+            constexpr int j = decltype(jc)::value;
+            step(ks0 + j, ab[j], ab[(j + PD - 1) % PD]);
+        };
+        qr_static_for<PD>(one);
+    }
+    {
+        auto one = [&](auto jc) {
+            constexpr int j = decltype(jc)::value;
+            if (ks0 + j < nk) step(ks0 + j, ab[j], ab[(j + PD - 1) % PD]);
+        };
+        qr_static_for<PD>(one);
     }
     // epilogue.  bf16 MFMA D: col = r (output column c0 + 16 g + r), row = 4 h + j within the 16-row tile.
     // Row-major outputs go through LDS, 64 rows at a time (in the M buffers): a lane then owns 8
@@ -2630,19 +2650,28 @@ hipError_t launch_panel_gemm(const T* In, int64_t rows, int LP, const T* Mm, int
             if (!msplit_ready)  // (else the factor that wrote M's fp32 copy wrote its pieces too)
                 hipLaunchKernelGGL(split_mat_kernel, dim3((unsigned)std::min<int64_t>((L2 + 255) / 256, 1024)), dim3(256),
                                    0, s, reinterpret_cast<const float*>(Mm), LP, msplit);
-#define PSPLIT(RT2, CT)                                                                                        \
+#define PSPLIT(RT2, CT, PD)                                                                                    \
     {                                                                                                          \
         const int ncb = (LP + CT - 1) / CT;                                                                    \
         const int64_t rb2 = (rows + 64 * RT2 - 1) / (64 * RT2);                                                \
-        hipLaunchKernelGGL((panel_split_kernel<RT2, CT>), dim3((unsigned)(rb2 * ncb)), dim3(256),              \
+        hipLaunchKernelGGL((panel_split_kernel<RT2, CT, PD>), dim3((unsigned)(rb2 * ncb)), dim3(256),          \
                            (size_t)2 * 3 * CT * 64, s, reinterpret_cast<const float*>(In), rows, LP, msplit,   \
                            upper, reinterpret_cast<float*>(Out), ldo, cols, hi, lo, ncb, pred);                \
         return hipGetLastError();                                                                              \
     }
             const int v = panel_split_variant();
-            if (v == 1) PSPLIT(4, 128)
-            if (v == 2) PSPLIT(4, 64)
-            PSPLIT(2, 128)
+            if (v == 1) PSPLIT(4, 128, 2)
+            if (v == 2) PSPLIT(4, 64, 2)
+            // In prefetch ring depth (RSVD_PANEL_PD overrides): 4 at LP = 512 (16 k-steps: C5 18.38 ->
+            // 18.19 ms, gpurun_out r6k), 2 (one step ahead) below, where 3 / 4 measured no gain
+            static const int pd_env = [] {
+                const char* e = std::getenv("RSVD_PANEL_PD");
+                return e ? std::atoi(e) : 0;
+            }();
+            const int pd = pd_env ? pd_env : (LP >= 512 ? 4 : 2);
+            if (pd == 3) PSPLIT(2, 128, 3)
+            if (pd == 4) PSPLIT(2, 128, 4)
+            PSPLIT(2, 128, 2)
 #undef PSPLIT
         }
     }
