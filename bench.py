@@ -442,6 +442,13 @@ def main():
         LPk = lp_pad(l)
         if dt == "bf16" and LPk == 256 and not nn:
             kpref = "wproj3tn2_kernel<true"
+        elif dt == "bf16" and LPk == 128 and not nn and os.environ.get("RSVD_TN128", "1") != "0":
+            kpref = "wproj3tn128_kernel<true"  # C3's TN on separate A / S rings (K chunks of 64 rows)
+        elif dt == "bf16" and LPk == 128 and nn and os.environ.get("RSVD_NN3_128", "1") != "0":
+            kpref = "wproj3_kernel<true, 128, true"  # the hi / lo NN at LP = 128 on the v3 kernel
+        elif dt == "fp8" and LPk == 512 and nn and os.environ.get("RSVD_NN8", "1") != "0":
+            kpref = "wproj3nn8_kernel<true"  # e4m3 NN halves on the v3 addressing, one dispatch
+            per_op = 2 if merged_off else 1
         elif dt == "fp8" and LPk in (256, 512) and not nn and os.environ.get("RSVD_FP8_TN4") != "0":
             kpref = "wproj3tn4_kernel<true"  # e4m3 TN, 128-B A lines; LP = 512 as two column halves
             per_op = LPk // 256 if merged_off else 1  # (both halves in one dispatch by default)
