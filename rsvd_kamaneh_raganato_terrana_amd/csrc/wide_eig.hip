@@ -124,13 +124,13 @@ __device__ __forceinline__ double rsqrt_f64(double d) {
 // RSVD_TRI_PROF (lab builds only): shader-cycle totals of the step phases of tridiag_kernel,
 // workgroup 0 thread 0, read back by tri_prof_read (tools/eig_lab.cpp)
 #ifdef RSVD_TRI_PROF
-__device__ long long g_tri_prof[8];
+__device__ long long g_tri_prof[16];  // [0, 4): multi-workgroup steps, [8, 12): one workgroup; [4, 8): inverse iteration
 #define TRI_INIT() long long tri_last_ = __builtin_amdgcn_s_memtime()
 #define TRI_TS(i)                                                        \
     do {                                                                 \
         if (blockIdx.x == 0 && threadIdx.x == 0) {                       \
             const long long now_ = __builtin_amdgcn_s_memtime();         \
-            g_tri_prof[(i)] += now_ - tri_last_;                         \
+            g_tri_prof[(i) + (NW == 1 ? 8 : 0)] += now_ - tri_last_;     \
             tri_last_ = now_;                                            \
         }                                                                \
     } while (0)
@@ -1175,8 +1175,8 @@ __global__ void tri_zero_kernel(double* __restrict__ Y, int64_t n1, double* __re
 
 #ifdef RSVD_TRI_PROF
 void tri_prof_read(long long* out) {
-    (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tri_prof), sizeof(long long) * 8);
-    long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    (void)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tri_prof), sizeof(long long) * 16);
+    long long z[16] = {};
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_tri_prof), z, sizeof(z));
 }
 #endif

@@ -59,7 +59,7 @@ int main(int argc, char** argv) {
     CK(hipEventCreate(&b));
     for (int r = 0; r < reps; ++r) {
 #ifdef RSVD_TRI_PROF
-        long long junk[8];
+        long long junk[16];
         tri_prof_read(junk);
 #endif
         CK(hipEventRecord(a, s));
@@ -75,10 +75,12 @@ int main(int argc, char** argv) {
         printf("l=%d LP=%d rep %d: %.1f us, sweeps %d, timeout %d, S[0] %.6g S[l-1] %.6g\n", l, LP, r, ms * 1e3,
                hinfo[0], hinfo[2], Sh[0], Sh[l - 1]);
 #ifdef RSVD_TRI_PROF
-        long long p[8];
+        long long p[16];
         tri_prof_read(p);
-        printf("  tridiag phases (Mcycles, wg 0): A %.3f B %.3f C %.3f D %.3f\n", p[0] * 1e-6, p[1] * 1e-6,
-               p[2] * 1e-6, p[3] * 1e-6);
+        printf("  tridiag phases (Mcycles, wg 0), multi-workgroup steps: A %.3f B %.3f C %.3f D %.3f\n", p[0] * 1e-6,
+               p[1] * 1e-6, p[2] * 1e-6, p[3] * 1e-6);
+        printf("  tridiag phases (Mcycles), one-workgroup steps: A %.3f B %.3f C %.3f D %.3f\n", p[8] * 1e-6,
+               p[9] * 1e-6, p[10] * 1e-6, p[11] * 1e-6);
         printf("  inverse iteration (Mcycles, thread 0): factor %.3f back %.3f forward %.3f back %.3f\n",
                p[4] * 1e-6, p[5] * 1e-6, p[6] * 1e-6, p[7] * 1e-6);
 #endif
