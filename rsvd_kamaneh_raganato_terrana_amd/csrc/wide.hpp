@@ -83,7 +83,7 @@ hipError_t launch_gram_wide(const T* P, const T* P2, int64_t rows, int LP, const
 hipError_t launch_chol_wide(const double* G, int l, int LP, double tol, double* R, double* Rinv, float* Rinv32,
                             int* colflag, int* flag, double* work, const int* pred, hipStream_t s,
                             double ill_tol = 0.0, int* ill = nullptr, const double* d0src = nullptr,
-                            bf16_t* Mt = nullptr);
+                            bf16_t* Mt = nullptr, int ldg = 0);  // ldg: G's row pitch (0: LP)
 // The same factor at LP = 2 B (B = 128, 256; l > B) in two B-column levels: R11 = chol(G11) and
 // S = G22 - R12^T R12 (R12 = R11^-T G12), the off-diagonal blocks R12 and Rinv12 = -Rinv11 R12 Rinv22
 // on a B^3 fp64 MFMA GEMM, breakdowns judged against the diagonal of G (d0src when this factor is
@@ -92,7 +92,8 @@ hipError_t launch_chol_wide(const double* G, int l, int LP, double tol, double* 
 hipError_t launch_chol_wide_2level(const double* G, int l, int LP, double tol, double* R, double* Rinv,
                                    float* Rinv32, int* colflag, int* flag, double* work, double* scratch,
                                    hipStream_t s, double ill_tol = 0.0, int* ill = nullptr,
-                                   const double* d0src = nullptr, int depth = 0, bf16_t* Mt = nullptr);
+                                   const double* d0src = nullptr, int depth = 0, bf16_t* Mt = nullptr,
+                                   int ldg = 0);  // ldg: G's row pitch (0: LP)
 // (Mt, both factors, with Rinv32: R^-1's fp32 copy also as split_mat_kernel's three bf16 piece
 // images, 3 LP^2 -- launch_panel_gemm's msplit with msplit_ready)
 size_t chol_2level_scratch_doubles(int LP, int depth);

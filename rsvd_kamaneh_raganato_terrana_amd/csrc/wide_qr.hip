@@ -1317,7 +1317,8 @@ __global__ __launch_bounds__(NT) void chol_wide_kernel(const double* __restrict_
                                                                  double* __restrict__ R, double* __restrict__ Rinv,
                                                                  int* __restrict__ colflag, int* __restrict__ flag,
                                                                  const int* __restrict__ pred, double ill_tol,
-                                                                 int* __restrict__ ill, const double* __restrict__ d0src) {
+                                                                 int* __restrict__ ill, const double* __restrict__ d0src,
+                                                                 int ldg) {
     if (pred && *pred == 0) return;
     extern __shared__ __attribute__((aligned(16))) char smem_raw[];
     __shared__ int ill_s;
@@ -1348,7 +1349,7 @@ __global__ __launch_bounds__(NT) void chol_wide_kernel(const double* __restrict_
 #pragma unroll
                     for (int j = 0; j < 4; ++j) {
                         const int i = 16 * tw.ib + h + 4 * j;
-                        v[b][j] = (i < l && c < l) ? G[(int64_t)i * LP + c] : 0.0;
+                        v[b][j] = (i < l && c < l) ? G[(int64_t)i * ldg + c] : 0.0;
                     }
                 }
                 tw.advance(nw);
@@ -1363,7 +1364,7 @@ __global__ __launch_bounds__(NT) void chol_wide_kernel(const double* __restrict_
         }
     }
     for (int i = tid; i < LP; i += NT) {
-        d0[i] = (i < l) ? (d0src ? d0src[i] : G[(int64_t)i * LP + i]) : 0.0;
+        d0[i] = (i < l) ? (d0src ? d0src[i] : G[(int64_t)i * ldg + i]) : 0.0;
         colflag[i] = 0;
     }
     if (tid == 0) ill_s = 0;
@@ -1529,7 +1530,8 @@ __global__ __launch_bounds__(64 * kCholRegWaves) void chol_reg_kernel(const doub
                                                                       double* __restrict__ R, double* __restrict__ Rinv,
                                                                       int* __restrict__ colflag, int* __restrict__ flag,
                                                                       const int* __restrict__ pred, double ill_tol,
-                                                                      int* __restrict__ ill, const double* __restrict__ d0src) {
+                                                                      int* __restrict__ ill, const double* __restrict__ d0src,
+                                                                      int ldg) {
     if (pred && *pred == 0) return;
     typedef CholReg<NP> C;
     __shared__ int ill_s;
@@ -1559,7 +1561,7 @@ __global__ __launch_bounds__(64 * kCholRegWaves) void chol_reg_kernel(const doub
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const int i = 16 * tib[s] + h + 4 * j, c = 16 * tjb[s] + r;
-            v[j] = (t < NT && i < l && c < l) ? G[(int64_t)i * LP + c] : 0.0;
+            v[j] = (t < NT && i < l && c < l) ? G[(int64_t)i * ldg + c] : 0.0;
         }
         if (s < SL) {
             *reinterpret_cast<double2*>(wlw + s * 256) = make_double2(v[0], v[1]);
@@ -1580,7 +1582,7 @@ __global__ __launch_bounds__(64 * kCholRegWaves) void chol_reg_kernel(const doub
         }
     };
     for (int i = tid; i < LP; i += 64 * NW) {
-        d0[i] = (i < l) ? (d0src ? d0src[i] : G[(int64_t)i * LP + i]) : 0.0;
+        d0[i] = (i < l) ? (d0src ? d0src[i] : G[(int64_t)i * ldg + i]) : 0.0;
         colflag[i] = 0;
     }
     if (tid == 0) ill_s = 0;
@@ -2449,23 +2451,24 @@ int chol_variant = 1;
 
 hipError_t launch_chol_wide(const double* G, int l, int LP, double tol, double* R, double* Rinv, float* Rinv32,
                             int* colflag, int* flag, double* work, const int* pred, hipStream_t s, double ill_tol,
-                            int* ill, const double* d0src, bf16_t* Mt) {
+                            int* ill, const double* d0src, bf16_t* Mt, int ldg) {
     if (LP % 16 || LP > 512) return hipErrorInvalidValue;
+    if (ldg == 0) ldg = LP;
     // LP = 256: chol_wide_kernel (its wave-0 look-ahead overlaps the diagonal factor with the other waves'
     // updates; the register-resident kernel spills there, 174 vs 161 us measured); LP <= 128: chol_reg_kernel
     // (LP = 128: 63 vs 71 us, LP = 64: 31 vs 37 us, tools/wide_lab chol)
     if (chol_variant >= 1 && LP == 128)
         hipLaunchKernelGGL(chol_reg_kernel<8>, dim3(1), dim3(64 * kCholRegWaves), CholReg<8>::lds_bytes, s, G, l, tol,
-                           R, Rinv, colflag, flag, pred, ill_tol, ill, d0src);
+                           R, Rinv, colflag, flag, pred, ill_tol, ill, d0src, ldg);
     else if (chol_variant >= 1 && LP == 64)
         hipLaunchKernelGGL(chol_reg_kernel<4>, dim3(1), dim3(64 * kCholRegWaves), CholReg<4>::lds_bytes, s, G, l, tol,
-                           R, Rinv, colflag, flag, pred, ill_tol, ill, d0src);
+                           R, Rinv, colflag, flag, pred, ill_tol, ill, d0src, ldg);
     else if (chol_variant == 2 && LP == 256)  // lab only
         hipLaunchKernelGGL(chol_reg_kernel<16>, dim3(1), dim3(64 * kCholRegWaves), CholReg<16>::lds_bytes, s, G, l,
-                           tol, R, Rinv, colflag, flag, pred, ill_tol, ill, d0src);
+                           tol, R, Rinv, colflag, flag, pred, ill_tol, ill, d0src, ldg);
     else
         hipLaunchKernelGGL((chol_wide_kernel<kCholThreads, kCholBatch>), dim3(1), dim3(kCholThreads), chol_lds_bytes(LP),
-                           s, G, l, LP, tol, work, R, Rinv, colflag, flag, pred, ill_tol, ill, d0src);
+                           s, G, l, LP, tol, work, R, Rinv, colflag, flag, pred, ill_tol, ill, d0src, ldg);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(rinv_wide_kernel, dim3(LP / 16), dim3(256), 0, s, LP, R, Rinv, Rinv32, pred, Mt);
@@ -2528,11 +2531,16 @@ __global__ void chol2_assemble_kernel(const double* __restrict__ R11, const doub
 // wave partials are summed through LDS in wave order.
 constexpr int kGemmSqWaves = 4;
 // zrow (nullable): output rows i with zrow[i] != 0 are written as zeros (R12's broken-down rows).
+// Cin (nullable): the beta term's C when it is not the output (ld ldcin); d0out (nullable): the
+// diagonal-tile workgroups also write d0out[i] = d0in ? d0in[i] : Cin[i][i] (a level's pivot reference)
 __global__ __launch_bounds__(64 * kGemmSqWaves) void gemmsq_f64_kernel(int N, int ta, double alpha,
                                                                        const double* __restrict__ A, int lda,
                                                                        const double* __restrict__ B, int ldb,
                                                                        double beta, double* __restrict__ C, int ldc,
-                                                                       const int* __restrict__ zrow) {
+                                                                       const int* __restrict__ zrow,
+                                                                       const double* __restrict__ Cin, int ldcin,
+                                                                       double* __restrict__ d0out,
+                                                                       const double* __restrict__ d0in) {
     __shared__ double part[kGemmSqWaves - 1][4][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 15, h = lane >> 4;
     const int nt = N / 16;
@@ -2561,17 +2569,21 @@ __global__ __launch_bounds__(64 * kGemmSqWaves) void gemmsq_f64_kernel(int N, in
     for (int j = 0; j < 4; ++j) {  // f64 D: col = r, row = h + 4 j
 #pragma unroll
         for (int q = 0; q < kGemmSqWaves - 1; ++q) v[j] += part[q][j][lane];
-        double* c = C + (int64_t)(i0 + MD::row(h, j)) * ldc + j0 + r;
+        const int ii = i0 + MD::row(h, j), jj = j0 + r;
+        double* c = C + (int64_t)ii * ldc + jj;
         const double o = alpha * v[j];
-        *c = (zrow && zrow[i0 + MD::row(h, j)]) ? 0.0 : (beta == 0.0 ? o : o + beta * *c);
+        const double cin = beta == 0.0 ? 0.0 : (Cin ? Cin[(int64_t)ii * ldcin + jj] : *c);
+        *c = (zrow && zrow[ii]) ? 0.0 : (beta == 0.0 ? o : o + beta * cin);
+        if (d0out && ii == jj) d0out[ii] = d0in ? d0in[ii] : Cin[(int64_t)ii * ldcin + ii];
     }
 }
 
 static hipError_t gemm_sq(int N, int ta, double alpha, const double* A, int lda, const double* B, int ldb, double beta,
-                          double* C, int ldc, hipStream_t s, const int* zrow = nullptr) {
+                          double* C, int ldc, hipStream_t s, const int* zrow = nullptr, const double* Cin = nullptr,
+                          int ldcin = 0, double* d0out = nullptr, const double* d0in = nullptr) {
     if (N % (16 * kGemmSqWaves)) return hipErrorInvalidValue;
     hipLaunchKernelGGL(gemmsq_f64_kernel, dim3((N / 16) * (N / 16)), dim3(64 * kGemmSqWaves), 0, s, N, ta, alpha, A, lda,
-                       B, ldb, beta, C, ldc, zrow);
+                       B, ldb, beta, C, ldc, zrow, Cin, ldcin, d0out, d0in);
     return hipGetLastError();
 }
 
@@ -2583,39 +2595,42 @@ size_t chol_2level_scratch_doubles(int LP, int depth) {
 
 // One level of the factor: the two-level form (recursing `depth` more times) when LP >= 256 and more
 // than half the columns are valid, else the one-workgroup kernel.
-static hipError_t chol_level(const double* G, int l, int LP, double tol, double* R, double* Rinv, int* colflag,
-                             int* flag, double* work, double* scratch, hipStream_t s, double ill_tol, int* ill,
-                             const double* d0src, int depth) {
+static hipError_t chol_level(const double* G, int ldg, int l, int LP, double tol, double* R, double* Rinv,
+                             int* colflag, int* flag, double* work, double* scratch, hipStream_t s, double ill_tol,
+                             int* ill, const double* d0src, int depth) {
     if (depth >= 0 && LP >= 256 && l > LP / 2)
         return launch_chol_wide_2level(G, l, LP, tol, R, Rinv, nullptr, colflag, flag, work, scratch, s, ill_tol, ill,
-                                       d0src, depth);
-    return launch_chol_wide(G, l, LP, tol, R, Rinv, nullptr, colflag, flag, work, nullptr, s, ill_tol, ill, d0src);
+                                       d0src, depth, nullptr, ldg);
+    return launch_chol_wide(G, l, LP, tol, R, Rinv, nullptr, colflag, flag, work, nullptr, s, ill_tol, ill, d0src,
+                            nullptr, ldg);
 }
 
 hipError_t launch_chol_wide_2level(const double* G, int l, int LP, double tol, double* R, double* Rinv,
                                    float* Rinv32, int* colflag, int* flag, double* work, double* scratch,
                                    hipStream_t s, double ill_tol, int* ill, const double* d0src, int depth,
-                                   bf16_t* Mt) {
+                                   bf16_t* Mt, int ldg) {
     if ((LP != 256 && LP != 512) || l <= LP / 2 || l > LP) return hipErrorInvalidValue;
+    if (ldg == 0) ldg = LP;
     const int B = LP / 2, B2 = B * B;
     double *Ga = scratch, *R11 = Ga + B2, *Ri11 = R11 + B2, *Sb = Ri11 + B2, *R22 = Sb + B2, *Ri22 = R22 + B2,
            *T = Ri22 + B2, *d0b = T + B2;
     int* ill2 = reinterpret_cast<int*>(d0b + B);
     double* inner = d0b + B + 64;  // the next level's scratch (depth > 0)
     const int sub = depth - 1;     // < 0: the levels below are one-workgroup factors
-    hipLaunchKernelGGL(chol2_prep_kernel, dim3(B), dim3(B), 0, s, G, B, Ga, Sb, d0b, d0src);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    // level 1: R11, Ri11 = chol(G11) (columns 0 .. B - 1 of colflag)
-    e = chol_level(Ga, B, B, tol, R11, Ri11, colflag, flag, work, inner, s, ill_tol, ill, d0src, sub);
+    (void)Ga;  // (round 5: the levels read G11 and G22 in place -- no copy launch)
+    // level 1: R11, Ri11 = chol(G11) (columns 0 .. B - 1 of colflag), G11 read in place (pitch ldg)
+    hipError_t e = chol_level(G, ldg, B, B, tol, R11, Ri11, colflag, flag, work, inner, s, ill_tol, ill, d0src, sub);
     if (e != hipSuccess) return e;
     // R12 = Ri11^T G12 -> R[:B, B:] (ld LP); the rows whose first-level pivot broke down are zero, as
     // the one-level factor's strips are (written so by the product's epilogue)
-    if ((e = gemm_sq(B, 1, 1.0, Ri11, B, G + B, LP, 0.0, R + B, LP, s, colflag)) != hipSuccess) return e;
-    // S = G22 - R12^T R12
-    if ((e = gemm_sq(B, 1, -1.0, R + B, LP, R + B, LP, 1.0, Sb, B, s)) != hipSuccess) return e;
+    if ((e = gemm_sq(B, 1, 1.0, Ri11, B, G + B, ldg, 0.0, R + B, LP, s, colflag)) != hipSuccess) return e;
+    // S = G22 - R12^T R12 into Sb (the beta term read from G22 in place), and d0b = diag(G22) (or the
+    // caller's d0src[B ..]) from the diagonal tiles
+    if ((e = gemm_sq(B, 1, -1.0, R + B, LP, R + B, LP, 1.0, Sb, B, s, nullptr, G + (int64_t)B * ldg + B, ldg, d0b,
+                     d0src ? d0src + B : nullptr)) != hipSuccess)
+        return e;
     // level 2 on the l - B valid columns of S, tested against diag(G22) (or the caller's d0src)
-    e = chol_level(Sb, l - B, B, tol, R22, Ri22, colflag + B, flag, work, inner, s, ill_tol, ill ? ill2 : nullptr,
+    e = chol_level(Sb, B, l - B, B, tol, R22, Ri22, colflag + B, flag, work, inner, s, ill_tol, ill ? ill2 : nullptr,
                    d0b, sub);
     if (e != hipSuccess) return e;
     // Rinv12 = -Ri11 (R12 Ri22) -> Rinv[:B, B:]
