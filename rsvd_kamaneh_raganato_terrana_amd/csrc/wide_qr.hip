@@ -2476,50 +2476,51 @@ hipError_t launch_chol_wide(const double* G, int l, int LP, double tol, double* 
 }
 
 // ---- two-level factor, LP = 2 B (launch_chol_wide_2level) ----------------------------------------
-// Ga = G11, Sb = G22 (B x B, ld B), d0b = diag(G22): the breakdown / ill tests of the second level
-// judge S's pivots against G's own diagonal, as the one-level factor does
-// (d0src: the diagonal the tests judge against when this factor is itself a second level)
-__global__ void chol2_prep_kernel(const double* __restrict__ G, int B, double* __restrict__ Ga, double* __restrict__ Sb,
-                                  double* __restrict__ d0b, const double* __restrict__ d0src) {
-    const int i = blockIdx.x, c = threadIdx.x, LP = 2 * B;  // B x B
-    Ga[i * B + c] = G[(int64_t)i * LP + c];
-    Sb[i * B + c] = G[(int64_t)(B + i) * LP + B + c];
-    if (c == 0) d0b[i] = d0src ? d0src[B + i] : G[(int64_t)(B + i) * LP + B + i];
-}
-// R / Rinv (2B x 2B row-major) from the level blocks; Rinv32 the fp32 copy; ill = ill1 | ill2
-__global__ void chol2_assemble_kernel(const double* __restrict__ R11, const double* __restrict__ Ri11,
-                                      const double* __restrict__ R22, const double* __restrict__ Ri22, int B,
-                                      double* __restrict__ R, double* __restrict__ Rinv, float* __restrict__ Rinv32,
-                                      const int* __restrict__ ill2, int* __restrict__ ill, bf16_t* __restrict__ Mt) {
-    const int i = blockIdx.x, c = threadIdx.x;  // 2B x B: columns c and c + B of row i
+// The levels read G11 and G22 in place (row pitch ldg); d0b = diag(G22), written by the S product's
+// diagonal tiles: the breakdown / ill tests of the second level judge S's pivots against G's own
+// diagonal, as the one-level factor does (d0src: that diagonal when this factor is itself a level).
+
+// R / Rinv (2B x 2B row-major) from the level blocks; Rinv32 the fp32 copy; ill = ill1 | ill2.
+// Run by extra workgroups of the Rinv12 GEMM (gemmsq_f64_kernel with a Chol2Asm job, round 5: one
+// launch fewer per two-level block); the GEMM's own workgroups write Rinv12's fp32 copy and pieces.
+struct Chol2Asm {
+    const double* R11;
+    const double* Ri11;
+    const double* R22;
+    const double* Ri22;
+    int B;  // 0: no assembly job
+    double* R;
+    double* Rinv;
+    float* Rinv32;
+    const int* ill2;
+    int* ill;
+    bf16_t* Mt;
+};
+// element (row i of 2B, column c of B): columns c (and c + B for i >= B) of row i
+__device__ __forceinline__ void chol2_assemble_elem(const Chol2Asm& a, int i, int c) {
+    const int B = a.B;
     const int64_t o = (int64_t)i * 2 * B, L2 = (int64_t)4 * B * B;
     if (i < B) {
-        R[o + c] = R11[i * B + c];
-        Rinv[o + c] = Ri11[i * B + c];
-        if (Rinv32) {
-            Rinv32[o + c] = (float)Ri11[i * B + c];
-            Rinv32[o + B + c] = (float)Rinv[o + B + c];
-        }
-        if (Mt) {
-            store_pieces(Mt, L2, (int64_t)c * 2 * B + i, (float)Ri11[i * B + c]);
-            store_pieces(Mt, L2, (int64_t)(B + c) * 2 * B + i, (float)Rinv[o + B + c]);
-        }
+        a.R[o + c] = a.R11[i * B + c];
+        a.Rinv[o + c] = a.Ri11[i * B + c];
+        if (a.Rinv32) a.Rinv32[o + c] = (float)a.Ri11[i * B + c];
+        if (a.Mt) store_pieces(a.Mt, L2, (int64_t)c * 2 * B + i, (float)a.Ri11[i * B + c]);
     } else {
         const int i2 = i - B;
-        R[o + c] = 0.0;
-        Rinv[o + c] = 0.0;
-        R[o + B + c] = R22[i2 * B + c];
-        Rinv[o + B + c] = Ri22[i2 * B + c];
-        if (Rinv32) {
-            Rinv32[o + c] = 0.f;
-            Rinv32[o + B + c] = (float)Ri22[i2 * B + c];
+        a.R[o + c] = 0.0;
+        a.Rinv[o + c] = 0.0;
+        a.R[o + B + c] = a.R22[i2 * B + c];
+        a.Rinv[o + B + c] = a.Ri22[i2 * B + c];
+        if (a.Rinv32) {
+            a.Rinv32[o + c] = 0.f;
+            a.Rinv32[o + B + c] = (float)a.Ri22[i2 * B + c];
         }
-        if (Mt) {
-            store_pieces(Mt, L2, (int64_t)c * 2 * B + i, 0.0f);
-            store_pieces(Mt, L2, (int64_t)(B + c) * 2 * B + i, (float)Ri22[i2 * B + c]);
+        if (a.Mt) {
+            store_pieces(a.Mt, L2, (int64_t)c * 2 * B + i, 0.0f);
+            store_pieces(a.Mt, L2, (int64_t)(B + c) * 2 * B + i, (float)a.Ri22[i2 * B + c]);
         }
     }
-    if (ill && i == 0 && c == 0 && *ill2) *ill = 1;
+    if (a.ill && i == 0 && c == 0 && *a.ill2) *a.ill = 1;
 }
 
 // row-major C (N x N, ldc) = alpha op(A) B + beta C, N = K in {128, 256} (op(A) = A or A^T; A, B
@@ -2540,10 +2541,15 @@ __global__ __launch_bounds__(64 * kGemmSqWaves) void gemmsq_f64_kernel(int N, in
                                                                        const int* __restrict__ zrow,
                                                                        const double* __restrict__ Cin, int ldcin,
                                                                        double* __restrict__ d0out,
-                                                                       const double* __restrict__ d0in) {
+                                                                       const double* __restrict__ d0in, Chol2Asm aj) {
     __shared__ double part[kGemmSqWaves - 1][4][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 15, h = lane >> 4;
     const int nt = N / 16;
+    if (aj.B && (int)blockIdx.x >= nt * nt) {  // an assembly workgroup (the Rinv12 product's launch)
+        const int e = ((int)blockIdx.x - nt * nt) * 64 * kGemmSqWaves + (int)threadIdx.x;
+        if (e < 2 * aj.B * aj.B) chol2_assemble_elem(aj, e / aj.B, e % aj.B);
+        return;
+    }
     const int i0 = 16 * (blockIdx.x / nt), j0 = 16 * (blockIdx.x % nt);
     const int kq = N / kGemmSqWaves;  // N % 64 == 0
     f64x4 acc[4] = {MD::zero(), MD::zero(), MD::zero(), MD::zero()};
@@ -2573,17 +2579,29 @@ __global__ __launch_bounds__(64 * kGemmSqWaves) void gemmsq_f64_kernel(int N, in
         double* c = C + (int64_t)ii * ldc + jj;
         const double o = alpha * v[j];
         const double cin = beta == 0.0 ? 0.0 : (Cin ? Cin[(int64_t)ii * ldcin + jj] : *c);
-        *c = (zrow && zrow[ii]) ? 0.0 : (beta == 0.0 ? o : o + beta * cin);
+        const double out = (zrow && zrow[ii]) ? 0.0 : (beta == 0.0 ? o : o + beta * cin);
+        *c = out;
         if (d0out && ii == jj) d0out[ii] = d0in ? d0in[ii] : Cin[(int64_t)ii * ldcin + ii];
+        if (aj.B) {  // (the Rinv12 product: C = Rinv + B, ldc = 2 B) its fp32 copy and pieces
+            if (aj.Rinv32) aj.Rinv32[(int64_t)ii * ldc + aj.B + jj] = (float)out;
+            if (aj.Mt) store_pieces(aj.Mt, (int64_t)4 * aj.B * aj.B, (int64_t)(aj.B + jj) * 2 * aj.B + ii, (float)out);
+        }
     }
 }
 
 static hipError_t gemm_sq(int N, int ta, double alpha, const double* A, int lda, const double* B, int ldb, double beta,
                           double* C, int ldc, hipStream_t s, const int* zrow = nullptr, const double* Cin = nullptr,
-                          int ldcin = 0, double* d0out = nullptr, const double* d0in = nullptr) {
+                          int ldcin = 0, double* d0out = nullptr, const double* d0in = nullptr,
+                          const Chol2Asm* aj = nullptr) {
     if (N % (16 * kGemmSqWaves)) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(gemmsq_f64_kernel, dim3((N / 16) * (N / 16)), dim3(64 * kGemmSqWaves), 0, s, N, ta, alpha, A, lda,
-                       B, ldb, beta, C, ldc, zrow, Cin, ldcin, d0out, d0in);
+    Chol2Asm job{};
+    int extra = 0;
+    if (aj) {
+        job = *aj;
+        extra = (2 * job.B * job.B + 64 * kGemmSqWaves - 1) / (64 * kGemmSqWaves);
+    }
+    hipLaunchKernelGGL(gemmsq_f64_kernel, dim3((N / 16) * (N / 16) + extra), dim3(64 * kGemmSqWaves), 0, s, N, ta, alpha,
+                       A, lda, B, ldb, beta, C, ldc, zrow, Cin, ldcin, d0out, d0in, job);
     return hipGetLastError();
 }
 
@@ -2635,10 +2653,9 @@ hipError_t launch_chol_wide_2level(const double* G, int l, int LP, double tol, d
     if (e != hipSuccess) return e;
     // Rinv12 = -Ri11 (R12 Ri22) -> Rinv[:B, B:]
     if ((e = gemm_sq(B, 0, 1.0, R + B, LP, Ri22, B, 0.0, T, B, s)) != hipSuccess) return e;
-    if ((e = gemm_sq(B, 0, -1.0, Ri11, B, T, B, 0.0, Rinv + B, LP, s)) != hipSuccess) return e;
-    hipLaunchKernelGGL(chol2_assemble_kernel, dim3(LP), dim3(B), 0, s, R11, Ri11, R22, Ri22, B, R, Rinv, Rinv32,
-                       ill2, ill, Mt);
-    return hipGetLastError();
+    // ... with the blocks' assembly into R / Rinv (+ Rinv32, pieces, ill) on extra workgroups
+    const Chol2Asm job{R11, Ri11, R22, Ri22, B, R, Rinv, Rinv32, ill2, ill, Mt};
+    return gemm_sq(B, 0, -1.0, Ri11, B, T, B, 0.0, Rinv + B, LP, s, nullptr, nullptr, 0, nullptr, nullptr, &job);
 }
 
 
