@@ -1213,10 +1213,29 @@ hipError_t launch_eig_svd(const double* R, int l, int LP, double* ews, double* X
     hipLaunchKernelGGL(tri_zero_kernel, dim3((unsigned)std::min<size_t>((L2 + 255) / 256, 1024)), dim3(256), 0, s, Y,
                        (int64_t)L2, taus, LP, sync + kTriCtr, 2);
     if ((er = hipGetLastError()) != hipSuccess) return er;
+    // the one-workgroup steps on a local block of n - off <= kTailRows rows: the three-slot shape while
+    // more than 128 rows are active, then the two-slot shape <2, 16, 8, 1> on the last 128 (its steps
+    // do 32 instead of 72 elements per thread: round 5, RSVD_TRI_SPLIT2=0 keeps one launch)
+    static const bool split2 = [] {
+        const char* v = std::getenv("RSVD_TRI_SPLIT2");
+        return v ? std::atoi(v) != 0 : true;
+    }();
+    auto one_wg = [&](const double* src, int off) -> hipError_t {
+        if (split2 && n - off > 128) {
+            const int kend2 = n - 128 - 1;
+            double* dump2 = scr + L2;  // (scr: free until the inverse iteration)
+            hipError_t e2 = launch_tridiag<3, 24, 8, 1>(src, LP, n, off, kend2, Y, LP, d, e, taus, dump2, xch, sync,
+                                                        info, s);
+            if (e2 != hipSuccess) return e2;
+            return launch_tridiag<2, 16, 8, 1>(dump2, LP, n, kend2 + 1, n - 2, Y, LP, d, e, taus, nullptr, xch, sync,
+                                               info, s);
+        }
+        return launch_tridiag<3, 24, 8, 1>(src, LP, n, off, n - 2, Y, LP, d, e, taus, nullptr, xch, sync, info, s);
+    };
     if (n <= 128) {
         er = launch_tridiag<2, 16, 8, 1>(G, LP, n, 0, n - 2, Y, LP, d, e, taus, nullptr, xch, sync, info, s);
     } else if (n <= kTailRows) {
-        er = launch_tridiag<3, 24, 8, 1>(G, LP, n, 0, n - 2, Y, LP, d, e, taus, nullptr, xch, sync, info, s);
+        er = one_wg(G, 0);
     } else {
         // phase 1 on NW workgroups up to the step that leaves kTailRows trailing rows, phase 2 on one
         double* dump = scr;  // free until the inverse iteration
@@ -1226,7 +1245,7 @@ hipError_t launch_eig_svd(const double* R, int l, int LP, double* ews, double* X
         else
             er = launch_tridiag<2, 16, 32, 16>(G, LP, n, 0, kend, Y, LP, d, e, taus, dump, xch, sync, info, s);
         if (er != hipSuccess) return er;
-        er = launch_tridiag<3, 24, 8, 1>(dump, LP, n, kend + 1, n - 2, Y, LP, d, e, taus, nullptr, xch, sync, info, s);
+        er = one_wg(dump, kend + 1);
     }
     if (er != hipSuccess) return er;
     // 3. eigenvalues (descending), 4. eigenvectors of T (row-major Z), cluster re-orthogonalisation
