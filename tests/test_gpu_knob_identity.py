@@ -11,6 +11,7 @@ U, S, V bytes must be identical:
 * RSVD_TN128=0     the LP = 128 TN on the v2 double-step kernel instead of wproj3tn128_kernel
 * RSVD_PANEL_PD=2  the split panel products with In one step ahead (the default is 4 at LP = 512)
 * RSVD_TRI_NOSKIP=1  the tridiagonalisation updating the dead row slots too (wide_eig.hip)
+* RSVD_TRI_SPLIT2=0  its one-workgroup phase in one launch (no hand-over to the two-slot shape)
 
 The oracle parity of the default path is what test_gpu_wide / test_gpu_eig / test_gpu_bench_pin
 check; this test pins that none of these kernels changed a single output bit.
@@ -67,6 +68,6 @@ def _digests(env_extra):
 def test_round5_kernels_bit_identical_to_previous():
     new = _digests({})
     old = _digests({"RSVD_NN8": "0", "RSVD_NN3_128": "0", "RSVD_TN128": "0", "RSVD_PANEL_PD": "2",
-                    "RSVD_TRI_NOSKIP": "1"})
+                    "RSVD_TRI_NOSKIP": "1", "RSVD_TRI_SPLIT2": "0"})
     assert new == old, (new, old)
     assert len(set(new)) == 4  # four different problems, four different digests
