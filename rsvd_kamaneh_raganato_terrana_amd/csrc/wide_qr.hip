@@ -1525,13 +1525,153 @@ template <int NP> struct CholReg {
     static constexpr size_t lds_bytes = (size_t)(512 + 256 + LP + 16 * LDR + NW * SL * 256) * 8 + 32 * 4;
 };
 
+__device__ __forceinline__ bf16_t f2bf(float x) {  // round to nearest even
+    const uint32_t u = __float_as_uint(x);
+    if ((u & 0x7f800000u) == 0x7f800000u) return (bf16_t)(u >> 16);
+    return (bf16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+__device__ __forceinline__ float bf2f(bf16_t b) { return __uint_as_float((uint32_t)b << 16); }
+
+// The three bf16 pieces of the fp32 element (row k, column c) of an LP x LP matrix in split_mat_kernel's
+// transposed piece images (Mt[x][c][k], image pitch L2 = LP^2): the factor kernels that write R^-1's
+// fp32 copy also write its pieces, so the split panel product needs no split_mat launch.
+__device__ __forceinline__ void store_pieces(bf16_t* __restrict__ Mt, int64_t L2, int64_t idx, float v) {
+    const bf16_t bh = f2bf(v);
+    const float rm = v - bf2f(bh);
+    const bf16_t bm = f2bf(rm);
+    Mt[idx] = bh;
+    Mt[L2 + idx] = bm;
+    Mt[2 * L2 + idx] = f2bf(rm - bf2f(bm));
+}
+
+// R^-1 inside the factor's own launch (round 5; NP <= 8, every leaf of the two- and three-level
+// factors): the products of rinv_wide_kernel in the same order, bit-identical, but one WAVE per
+// 16-column block column jb instead of one workgroup.  X[k] never leaves the wave -- its MFMA output
+// layout (row h + 4 j, column r) is the B operand (rows 4 kk + h) of the next product -- so the steps
+// need no workgroup barrier, and R's upper block triangle (diagonal slots: D^-1 from Rinv) is staged
+// once in LDS in A-operand order (tile t of the triangle at img + 256 t, lane L's four k-values
+// contiguous).  Saves the rinv_wide launch (~14 us per leaf) for ~4 us here.
+template <int NP> struct CholRegInv {
+    static constexpr int NT = NP * (NP + 1) / 2, NTH = 64 * kCholRegWaves;
+    static constexpr int NE = (NT * 256 + NTH - 1) / NTH;  // staged doubles per thread
+    static constexpr size_t lds_bytes = (size_t)NT * 256 * 8;
+};
+__device__ __forceinline__ int tri_index(int p, int k, int np) { return p * np - p * (p - 1) / 2 + (k - p); }
+
+// Below the block diagonal of an LP x LP factor: zeros in R, Rinv, Rinv32 (row-major) and the pieces
+// (transposed), each array walked in its own layout so every store instruction is contiguous.
+__device__ __forceinline__ void chol_lower_zeros(int LP, double* __restrict__ R, double* __restrict__ Rinv,
+                                                 float* __restrict__ Rinv32, bf16_t* __restrict__ Mt, int t0,
+                                                 int nthr) {
+    const int64_t L2 = (int64_t)LP * LP;
+    for (int e = t0; e < LP * LP; e += nthr) {
+        const int a = e / LP, b = e % LP;
+        if (a >= 16 * (b / 16 + 1)) {  // row a, column b
+            R[e] = 0.0;
+            Rinv[e] = 0.0;
+            if (Rinv32) Rinv32[e] = 0.0f;
+        }
+        if (Mt && b >= 16 * (a / 16 + 1)) {  // column a, row b
+            Mt[e] = 0;
+            Mt[L2 + e] = 0;
+            Mt[2 * L2 + e] = 0;
+        }
+    }
+}
+
+template <int NP>
+__device__ __forceinline__ void chol_reg_rinv(double* __restrict__ img, double* __restrict__ R,
+                                              double* __restrict__ Rinv, float* __restrict__ Rinv32,
+                                              bf16_t* __restrict__ Mt, int tid, int wv, int lane) {
+    typedef CholRegInv<NP> C;
+    constexpr int LP = 16 * NP;
+    const int64_t L2 = (int64_t)LP * LP;
+    const int r = lane & 15, h = lane >> 4;
+    __syncthreads();  // the factor's LDS is dead; its R / Rinv stores are visible workgroup-wide
+    {
+        // the full NP x NP tile grid, upper triangle kept: shifts only, every load issued before any store
+        constexpr int NF = NP * NP * 256 / C::NTH;
+        double v[NF];
+#pragma unroll
+        for (int i = 0; i < NF; ++i) {
+            const int e = tid + i * C::NTH;
+            const int t2 = e >> 8, p = t2 / NP, k = t2 % NP, L = (e >> 2) & 63, kk = e & 3;
+            const int64_t src = (int64_t)(16 * p + (L & 15)) * LP + 16 * k + 4 * kk + (L >> 4);
+            v[i] = 0.0;
+            if (p < k) v[i] = R[src];
+            else if (p == k) v[i] = Rinv[src];
+        }
+#pragma unroll
+        for (int i = 0; i < NF; ++i) {
+            const int e = tid + i * C::NTH;
+            const int t2 = e >> 8, p = t2 / NP, k = t2 % NP;
+            if (p <= k) img[tri_index(p, k, NP) * 256 + (e & 255)] = v[i];
+        }
+    }
+    __syncthreads();
+    CHOL_TS(210);
+    // column jb's 2 jb^2 + 6 jb MFMAs: waves w and w + 4 share a SIMD, so pair the long columns with
+    // the short ones (NP = 8: 7 + 0, 6 + 1, 5 + 2, 4 + 3; 140 MFMAs on the busiest SIMD instead of 176)
+    const int jb = NP == 8 ? (wv < 4 ? 7 - wv : wv - 4) : wv, c0 = 16 * jb;
+    if (jb >= NP) return;
+    f64x4 T[NP];
+#pragma unroll
+    for (int s = 0; s < NP; ++s) T[s] = MD::zero();
+    for (int k = jb; k >= 0; --k) {
+        const double* dk = img + tri_index(k, k, NP) * 256;
+        f64x4 x;
+        if (k == jb) {  // D_jb^-1 in output layout: element (h + 4 j, r) sits in lane (h + 4 j) + 16 (r & 3), slot r >> 2
+#pragma unroll
+            for (int j = 0; j < 4; ++j) x[j] = dk[((h + 4 * j) + 16 * (r & 3)) * 4 + (r >> 2)];
+        } else {
+            f64x4 t = MD::zero();
+#pragma unroll
+            for (int s = 0; s < NP; ++s)
+                if (s == k) t = T[s];
+            const double2 d01 = *reinterpret_cast<const double2*>(dk + lane * 4);
+            const double2 d23 = *reinterpret_cast<const double2*>(dk + lane * 4 + 2);
+            f64x4 o = MD::zero();
+            o = MD::mma(d01.x, t[0], o);
+            o = MD::mma(d01.y, t[1], o);
+            o = MD::mma(d23.x, t[2], o);
+            o = MD::mma(d23.y, t[3], o);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) x[j] = -o[j];
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int i = h + 4 * j;
+            if (k != jb) Rinv[(int64_t)(16 * k + i) * LP + c0 + r] = x[j];
+            if (Rinv32) Rinv32[(int64_t)(16 * k + i) * LP + c0 + r] = (float)x[j];
+            if (Mt) store_pieces(Mt, L2, (int64_t)(c0 + r) * LP + 16 * k + i, (float)x[j]);
+        }
+#pragma unroll
+        for (int s = NP - 1; s >= 0; --s)  // T[k - 1] first: the next step's product waits on it
+            if (s < k) {
+                const double* a = img + tri_index(s, k, NP) * 256 + lane * 4;
+                const double2 a01 = *reinterpret_cast<const double2*>(a);
+                const double2 a23 = *reinterpret_cast<const double2*>(a + 2);
+                T[s] = MD::mma(a01.x, x[0], T[s]);
+                T[s] = MD::mma(a01.y, x[1], T[s]);
+                T[s] = MD::mma(a23.x, x[2], T[s]);
+                T[s] = MD::mma(a23.y, x[3], T[s]);
+            }
+    }
+#ifdef RSVD_CHOL_PROF
+    if (lane == 0) g_chol_prof[211 + jb] = wall_clock64();
+#endif
+    // the zeros below the block diagonal: on the waves of the short columns, after their column
+    if (2 * jb < NP) chol_lower_zeros(LP, R, Rinv, Rinv32, Mt, jb * 64 + lane, NP / 2 * 64);
+}
+
 template <int NP>
 __global__ __launch_bounds__(64 * kCholRegWaves) void chol_reg_kernel(const double* __restrict__ G, int l, double tol,
                                                                       double* __restrict__ R, double* __restrict__ Rinv,
                                                                       int* __restrict__ colflag, int* __restrict__ flag,
                                                                       const int* __restrict__ pred, double ill_tol,
                                                                       int* __restrict__ ill, const double* __restrict__ d0src,
-                                                                      int ldg) {
+                                                                      int ldg, float* __restrict__ Rinv32,
+                                                                      bf16_t* __restrict__ Mt, int fuse_rinv) {
     if (pred && *pred == 0) return;
     typedef CholReg<NP> C;
     __shared__ int ill_s;
@@ -1668,6 +1808,9 @@ __global__ __launch_bounds__(64 * kCholRegWaves) void chol_reg_kernel(const doub
             }
         if (p < 32) CHOL_TS(3 + 3 * p);
     }
+    if constexpr (NP <= 8) {
+        if (fuse_rinv) chol_reg_rinv<NP>(reinterpret_cast<double*>(smem_raw), R, Rinv, Rinv32, Mt, tid, wv, lane);
+    }
 }
 
 // R^-1 = blocked back substitution, one workgroup (4 waves) per 16-column block jb, all block
@@ -1678,25 +1821,6 @@ __global__ __launch_bounds__(64 * kCholRegWaves) void chol_reg_kernel(const doub
 // (An accumulator in MFMA output layout -- row h + 4 j, column r in lane (r, h) -- is already the
 // B operand of the next product: rows 4 kk + h.)  Also: zeros below the block diagonal of R and
 // R^-1, and the fp32 copy of this block column of R^-1.
-__device__ __forceinline__ bf16_t f2bf(float x) {  // round to nearest even
-    const uint32_t u = __float_as_uint(x);
-    if ((u & 0x7f800000u) == 0x7f800000u) return (bf16_t)(u >> 16);
-    return (bf16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
-}
-__device__ __forceinline__ float bf2f(bf16_t b) { return __uint_as_float((uint32_t)b << 16); }
-
-// The three bf16 pieces of the fp32 element (row k, column c) of an LP x LP matrix in split_mat_kernel's
-// transposed piece images (Mt[x][c][k], image pitch L2 = LP^2): the factor kernels that write R^-1's
-// fp32 copy also write its pieces, so the split panel product needs no split_mat launch.
-__device__ __forceinline__ void store_pieces(bf16_t* __restrict__ Mt, int64_t L2, int64_t idx, float v) {
-    const bf16_t bh = f2bf(v);
-    const float rm = v - bf2f(bh);
-    const bf16_t bm = f2bf(rm);
-    Mt[idx] = bh;
-    Mt[L2 + idx] = bm;
-    Mt[2 * L2 + idx] = f2bf(rm - bf2f(bm));
-}
-
 constexpr int kRinvSlots = 8;  // LP <= 512: 32 block rows over 4 waves
 
 __global__ __launch_bounds__(256) void rinv_wide_kernel(int LP, double* __restrict__ R, double* __restrict__ Rinv,
@@ -2457,20 +2581,28 @@ hipError_t launch_chol_wide(const double* G, int l, int LP, double tol, double* 
     // LP = 256: chol_wide_kernel (its wave-0 look-ahead overlaps the diagonal factor with the other waves'
     // updates; the register-resident kernel spills there, 174 vs 161 us measured); LP <= 128: chol_reg_kernel
     // (LP = 128: 63 vs 71 us, LP = 64: 31 vs 37 us, tools/wide_lab chol)
+    // RSVD_CHOL_RINV_FUSED=0: R^-1 on its own rinv_wide launch after the register-resident factor too
+    static const int fused_env = [] {
+        const char* e = std::getenv("RSVD_CHOL_RINV_FUSED");
+        return e ? std::atoi(e) : 1;
+    }();
+    const int fuse = (fused_env && chol_variant >= 1 && (LP == 128 || LP == 64)) ? 1 : 0;
     if (chol_variant >= 1 && LP == 128)
-        hipLaunchKernelGGL(chol_reg_kernel<8>, dim3(1), dim3(64 * kCholRegWaves), CholReg<8>::lds_bytes, s, G, l, tol,
-                           R, Rinv, colflag, flag, pred, ill_tol, ill, d0src, ldg);
+        hipLaunchKernelGGL(chol_reg_kernel<8>, dim3(1), dim3(64 * kCholRegWaves),
+                           std::max(CholReg<8>::lds_bytes, fuse ? CholRegInv<8>::lds_bytes : 0), s, G, l, tol, R, Rinv,
+                           colflag, flag, pred, ill_tol, ill, d0src, ldg, Rinv32, Mt, fuse);
     else if (chol_variant >= 1 && LP == 64)
-        hipLaunchKernelGGL(chol_reg_kernel<4>, dim3(1), dim3(64 * kCholRegWaves), CholReg<4>::lds_bytes, s, G, l, tol,
-                           R, Rinv, colflag, flag, pred, ill_tol, ill, d0src, ldg);
+        hipLaunchKernelGGL(chol_reg_kernel<4>, dim3(1), dim3(64 * kCholRegWaves),
+                           std::max(CholReg<4>::lds_bytes, fuse ? CholRegInv<4>::lds_bytes : 0), s, G, l, tol, R, Rinv,
+                           colflag, flag, pred, ill_tol, ill, d0src, ldg, Rinv32, Mt, fuse);
     else if (chol_variant == 2 && LP == 256)  // lab only
         hipLaunchKernelGGL(chol_reg_kernel<16>, dim3(1), dim3(64 * kCholRegWaves), CholReg<16>::lds_bytes, s, G, l,
-                           tol, R, Rinv, colflag, flag, pred, ill_tol, ill, d0src, ldg);
+                           tol, R, Rinv, colflag, flag, pred, ill_tol, ill, d0src, ldg, Rinv32, Mt, 0);
     else
         hipLaunchKernelGGL((chol_wide_kernel<kCholThreads, kCholBatch>), dim3(1), dim3(kCholThreads), chol_lds_bytes(LP),
                            s, G, l, LP, tol, work, R, Rinv, colflag, flag, pred, ill_tol, ill, d0src, ldg);
     const hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
+    if (e != hipSuccess || fuse) return e;
     hipLaunchKernelGGL(rinv_wide_kernel, dim3(LP / 16), dim3(256), 0, s, LP, R, Rinv, Rinv32, pred, Mt);
     return hipGetLastError();
 }
@@ -2878,6 +3010,12 @@ void chol_prof_dump(int LP) {
     }
     printf("  LP=%d reg phases (us, wave 0): init %.1f  diag+wait %.1f  strip %.1f  update %.1f\n", LP,
            (t[200] - t[97]) * us, A, B, Cc);
+    if (np <= 8) {
+        const long long f = t[1 + 3 * (np - 1)];
+        printf("  LP=%d fused R^-1 (us after the factor): staged %.2f, columns", LP, (t[210] - f) * us);
+        for (int j = 0; j < np; ++j) printf(" %.2f", (t[211 + j] - f) * us);
+        printf("\n");
+    }
 }
 }  // namespace rsvd
 #endif

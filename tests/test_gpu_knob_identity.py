@@ -12,6 +12,7 @@ U, S, V bytes must be identical:
 * RSVD_PANEL_PD=2  the split panel products with In one step ahead (the default is 4 at LP = 512)
 * RSVD_TRI_NOSKIP=1  the tridiagonalisation updating the dead row slots too (wide_eig.hip)
 * RSVD_TRI_SPLIT2=0  its one-workgroup phase in one launch (no hand-over to the two-slot shape)
+* RSVD_CHOL_RINV_FUSED=0  the leaves' R^-1 on a separate rinv_wide launch (wide_qr.hip)
 
 The oracle parity of the default path is what test_gpu_wide / test_gpu_eig / test_gpu_bench_pin
 check; this test pins that none of these kernels changed a single output bit.
@@ -68,6 +69,7 @@ def _digests(env_extra):
 def test_round5_kernels_bit_identical_to_previous():
     new = _digests({})
     old = _digests({"RSVD_NN8": "0", "RSVD_NN3_128": "0", "RSVD_TN128": "0", "RSVD_PANEL_PD": "2",
-                    "RSVD_TRI_NOSKIP": "1", "RSVD_TRI_SPLIT2": "0"})
+                    "RSVD_TRI_NOSKIP": "1", "RSVD_TRI_SPLIT2": "0",
+                    "RSVD_CHOL_RINV_FUSED": "0"})
     assert new == old, (new, old)
     assert len(set(new)) == 4  # four different problems, four different digests
