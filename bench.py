@@ -284,6 +284,10 @@ def main():
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="N > 1: torch.distributed backend (nccl = RCCL; gloo with --comm torch runs the whole "
                          "multi-rank path with every rank on one GPU, for the one-GPU test box)")
+    ap.add_argument("--emulate-world", type=int, default=0,
+                    help="diagnostics, one process: run rank 0 of an N-rank strong-scaled job alone (its rows of A, "
+                         "its n shard, the sharded-panel kernels) with no-op collectives -- prices the per-rank "
+                         "kernels of the N-GPU step on one GPU (outputs are not an SVD; no self-check, no CPU line)")
     argv = json.loads(os.environ["RSVD_BENCH_ARGV"]) if "RSVD_BENCH_ARGV" in os.environ and "WORLD_SIZE" in os.environ else None
     args = ap.parse_args(argv)
 
@@ -322,9 +326,10 @@ def main():
         else:
             dist.init_process_group("gloo")
 
+    emu = args.emulate_world if world == 1 and args.emulate_world > 1 else 0
     if strong:  # global m x n, rows partitioned (src/rSVD.cpp:20-23)
         m_global = m_cfg
-        m_local, row0 = R.row_partition(m_global, world, rank)
+        m_local, row0 = R.row_partition(m_global, emu or world, rank)
     else:
         m_local, row0 = m_cfg, m_cfg * rank
         m_global = m_cfg * world
@@ -347,6 +352,10 @@ def main():
             eng.comm_init(uid[0], rank, world, shard_n=True)
         else:
             eng.set_comm(rank, world)
+    if emu:  # the rank's kernels alone; the workspace zeroed once so the never-exchanged rows are finite
+        eng.emulate_world(0, emu)
+        eng.reserve(eng.desc(A, l, q, seed=0x5EED0002, a_scale=a_scale))
+        eng._ws.zero_()
     torch.cuda.synchronize()
 
     def step():
@@ -404,11 +413,14 @@ def main():
     tm = eng.timing()
     eng.set_timing(False)
     info = eng.info()
-    U_, S_, V_ = step()
-    check = self_check(torch, dist, A, a_scale, U_, S_, V_, world)
-    del U_, S_, V_
+    if emu:
+        check = {"skipped": f"--emulate-world {emu}: no-op collectives, the outputs are not an SVD"}
+    else:
+        U_, S_, V_ = step()
+        check = self_check(torch, dist, A, a_scale, U_, S_, V_, world)
+        del U_, S_, V_
 
-    f_proj, f_qr, f_small = algorithmic_flops(m_global, n, l, q)
+    f_proj, f_qr, f_small = algorithmic_flops(m_local if emu else m_global, n, l, q)
     f_total = f_proj + f_qr + f_small
     ms_per_step = elapsed / args.steps * 1e3
     value = f_total * args.steps / elapsed / 1e12
@@ -505,7 +517,7 @@ def main():
         roof["sketch"] = sk
 
     cpu = None
-    if rank == 0 and world == 1 and args.cpu_budget > 0:
+    if rank == 0 and world == 1 and args.cpu_budget > 0 and not emu:
         rows = m_local if cpu_rows is None else min(cpu_rows, m_local)
         Ah = A[:rows]
         Ah = (Ah.float() * a_scale if dt == "fp8" else Ah).double().cpu().numpy()
@@ -517,6 +529,9 @@ def main():
 
     if rank == 0:
         par = "single-gpu" if world == 1 else (f"row-partition x{world}" if strong else f"row-shard x{world}")
+        if emu:
+            par = (f"EMULATED rank 0 of {emu} on one GPU (no-op collectives; n shard {info.get('n_shard_rows')} "
+                   f"rows): per-rank kernel time only, not an N-GPU measurement")
         if world > 1 and info.get("n_shard_rows"):
             par += f", n side sharded ({info['n_shard_rows']} rows/GPU)"
         if world > 1:

@@ -221,6 +221,17 @@ class Engine:
         check(lib().rsvd_set_collectives(self.h, self._coll if self._coll is not None else _capi.COLLECTIVE_FN(), None),
               self.h)
 
+    def emulate_world(self, rank: int, world: int):
+        """Diagnostics (bench.py --emulate-world): run rank `rank` of a `world`-rank row-sharded rSVD
+        on this one handle -- the kernels a rank of the N-GPU job runs, at its shapes (its rows of A,
+        its n shard, the fp64 Grams of sharded panels) -- with every collective a no-op.  The
+        exchanged values are then not the other ranks' (the outputs are not the SVD of any matrix), so
+        this only prices the per-rank kernels; the collectives are priced apart."""
+        self._hook = _capi.ALLREDUCE_FN(lambda buf, count, dt, stream, user: 0)
+        self._coll = _capi.COLLECTIVE_FN(lambda op, send, recv, count, dt, stream, user: 0)
+        check(lib().rsvd_set_comm(self.h, rank, world, self._hook, None), self.h)
+        check(lib().rsvd_set_collectives(self.h, self._coll, None), self.h)
+
     @staticmethod
     def comm_unique_id() -> bytes:
         """rsvd_comm_unique_id: the RCCL id one rank draws and every rank passes to comm_init."""

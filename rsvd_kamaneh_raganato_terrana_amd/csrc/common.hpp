@@ -84,12 +84,15 @@ inline bool coop_launch_enabled() {
 
 // How many workgroups of `kernel` (block threads, lds bytes of dynamic LDS) the device holds at
 // once: the occupancy calculator's per-CU count times the CU count.  A persistent grid larger
-// than this cannot be co-resident -- the caller shrinks it or refuses the size.
+// than this cannot be co-resident -- the caller shrinks it or refuses the size.  A failing HIP
+// query returns its error code negated (< 0), which launch_coresident passes through (ADVICE r05:
+// it is not a size the device cannot hold).
 // (Cached per device, kernel, block and LDS size: the persistent kernels launch once per rSVD.)
 template <typename... P>
 int64_t coresident_capacity(void (*kernel)(P...), int block, size_t lds) {
     int dev = 0, per_cu = 0, cus = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return -(int64_t)e;
     static std::mutex mu;
     static std::map<std::tuple<int, const void*, int, size_t>, int64_t> cache;
     const auto key = std::make_tuple(dev, reinterpret_cast<const void*>(kernel), block, lds);
@@ -98,10 +101,10 @@ int64_t coresident_capacity(void (*kernel)(P...), int block, size_t lds) {
         auto it = cache.find(key);
         if (it != cache.end()) return it->second;
     }
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(kernel), block, lds) !=
-        hipSuccess)
-        return 0;
+    e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e != hipSuccess) return -(int64_t)e;
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(kernel), block, lds);
+    if (e != hipSuccess) return -(int64_t)e;
     const int64_t cap = (int64_t)per_cu * cus;
     std::lock_guard<std::mutex> g(mu);
     cache[key] = cap;
@@ -113,6 +116,7 @@ hipError_t launch_coresident(void (*kernel)(P...), dim3 grid, dim3 block, size_t
     // refuse a grid the device cannot hold at once (a plain launch of it would deadlock in the
     // kernel's grid barriers until the bounded spins gave up)
     const int64_t cap = coresident_capacity(kernel, (int)(block.x * block.y * block.z), lds);
+    if (cap < 0) return (hipError_t)(-cap);  // the occupancy query itself failed
     if ((int64_t)grid.x * grid.y * grid.z > cap) return hipErrorCooperativeLaunchTooLarge;
     if (!coop_launch_enabled()) {
         hipLaunchKernelGGL(kernel, grid, block, lds, s, static_cast<P>(a)...);

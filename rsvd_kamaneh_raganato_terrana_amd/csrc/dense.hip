@@ -480,7 +480,7 @@ hipError_t launch_shift_diag(double* G, int LP, int l, int64_t rows, double u, h
 // (32 contiguous bytes) per fragment.
 namespace {
 
-constexpr int kPgThreads = 256;
+constexpr int kPgThreads = 256;  // four waves (power_grid_kernel's quarter sums assume it)
 
 __global__ __launch_bounds__(256) void gram_cm_kernel(const double* __restrict__ A, int64_t lda, int64_t m, int64_t n,
                                                       double* __restrict__ B) {
@@ -601,6 +601,7 @@ __global__ __launch_bounds__(kPgThreads) void power_grid_kernel(const double* __
     const int64_t ldu = io.ldu, ldv = io.ldv, ldb = io.ldb;
     __shared__ double red[kPgThreads / 64];
     __shared__ double coef_s[64];
+    __shared__ double qsum[kPgThreads / 64][64];
     const int G = gridDim.x, g = blockIdx.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     int64_t b0, b1, a0, a1;
     pg_rows(n, G, g, b0, b1);
@@ -612,9 +613,15 @@ __global__ __launch_bounds__(kPgThreads) void power_grid_kernel(const double* __
         if (g == 0 && tid == 0) atomicOr(tmo, 1);
         return false;
     };
-    auto grid_sum = [&](int slot) {  // fixed-order sum of the workgroups' partials in `slot`
+    // Fixed-order sum of the workgroups' partials in `slot`, called by every thread: each wave loads the
+    // G partials across its lanes (all in flight) and folds them by a butterfly, so every lane of every
+    // workgroup gets the same bits (a serial loop over G cross-XCD loads per thread cost ~G L2-miss
+    // latencies per iteration: ADVICE r05, l = 2048 took 19 s).
+    auto grid_sum = [&](int slot) {
         double t = 0.0;
-        for (int q = 0; q < G; ++q) t += part[(size_t)q * P + slot];
+        for (int q = lane; q < G; q += 64) t += part[(size_t)q * P + slot];
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o);
         return t;
     };
     double* y0 = Y;
@@ -638,8 +645,16 @@ __global__ __launch_bounds__(kPgThreads) void power_grid_kernel(const double* __
             double sq2 = 0.0;
             for (int64_t row = b0 + w; row < b1; row += kPgThreads / 64) {
                 const double* br = B + row * ldb;
-                double acc = 0.0;
-                for (int64_t c = lane; c < n; c += 64) acc += br[c] * y0[c];
+                double a4[4] = {0.0, 0.0, 0.0, 0.0};  // four loads in flight per lane
+                int64_t c = lane;
+                for (; c + 192 < n; c += 256) {
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) a4[u] += br[c + 64 * u] * y0[c + 64 * u];
+                }
+                if (c < n) a4[0] += br[c] * y0[c];  // (at most three 64-column steps remain)
+                if (c + 64 < n) a4[1] += br[c + 64] * y0[c + 64];
+                if (c + 128 < n) a4[2] += br[c + 128] * y0[c + 128];
+                double acc = (a4[0] + a4[1]) + (a4[2] + a4[3]);
 #pragma unroll
                 for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
                 acc *= inv;
@@ -655,37 +670,64 @@ __global__ __launch_bounds__(kPgThreads) void power_grid_kernel(const double* __
             y1 = t;
         }
         // v = x0.normalized() (:72-73); coef_j = sigma_j (v_j . v) for the implicit deflation of A
+        // (thread (quarter w, slot lane): its quarter of this workgroup's rows, the quarters summed in
+        // order through LDS -- all 64 slots of a chunk at once instead of one wave-wide dot per slot)
         const double vs = 1.0 / nrm;
         for (int j0 = 0; j0 < i; j0 += 64) {
             const int jn = (i - j0) < 64 ? (i - j0) : 64;
-            for (int jj = w; jj < jn; jj += kPgThreads / 64) {
-                const double* vj = V + (size_t)(j0 + jj) * ldv;
-                double d = 0.0;
-                for (int64_t c = b0 + lane; c < b1; c += 64) d += vj[c] * y0[c];
-#pragma unroll
-                for (int o = 32; o > 0; o >>= 1) d += __shfl_xor(d, o);
-                if (lane == 0) part[(size_t)g * P + j0 + jj] = d * vs;
+            double d = 0.0;
+            if (lane < jn) {
+                const double* vj = V + (size_t)(j0 + lane) * ldv;
+                for (int64_t c = b0 + w; c < b1; c += kPgThreads / 64) d += vj[c] * y0[c];
             }
+            __syncthreads();
+            qsum[w][lane] = d;
+            __syncthreads();
+            if (tid < jn) part[(size_t)g * P + j0 + tid] = ((qsum[0][tid] + qsum[1][tid]) + (qsum[2][tid] + qsum[3][tid])) * vs;
         }
         if (!barrier()) return;
-        // u = A_i v = A v - sum_j coef_j u_j over this workgroup's rows of A; |u| over the grid
-        double su = 0.0;
-        for (int j0 = 0; j0 <= i; j0 += 64) {  // coefficients in chunks of 64 (LDS)
-            const int jn = (i - j0) < 64 ? (i - j0) : 64;
-            if (jn <= 0 && j0 > 0) break;
-            __syncthreads();
-            if (tid < jn) coef_s[tid] = S[j0 + tid] * grid_sum(j0 + tid);
-            __syncthreads();
+        // u = A_i v = A v - sum_j coef_j u_j over this workgroup's rows of A; |u| over the grid.
+        // A v: row-major A (ac = 1: the rSVD's R^T, ar = l) takes a wave per row, lanes along the
+        // row and a shuffle sum (a thread per row left l / 256 threads of a workgroup
+        // busy on serial l-long dots); otherwise (column-major A, ar = 1) a thread per row, whose
+        // loads are coalesced down each column.
+        if (io.ac == 1) {
+            for (int64_t row = a0 + w; row < a1; row += kPgThreads / 64) {
+                const double* arow = A + row * io.ar;
+                double acc = 0.0;
+                for (int64_t c = lane; c < n; c += 64) acc += arow[c] * (y0[c] * vs);
+#pragma unroll
+                for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o);
+                if (lane == 0) U[row + (size_t)i * ldu] = acc;
+            }
+        } else {
             for (int64_t row = a0 + tid; row < a1; row += kPgThreads) {
                 double acc = 0.0;
-                if (j0 == 0)
-                    for (int64_t c = 0; c < n; ++c) acc += A[row * io.ar + c * io.ac] * (y0[c] * vs);
-                else
-                    acc = U[row + (size_t)i * ldu];
+                for (int64_t c = 0; c < n; ++c) acc += A[row * io.ar + c * io.ac] * (y0[c] * vs);
+                U[row + (size_t)i * ldu] = acc;
+            }
+        }
+        double su = 0.0;
+        for (int j0 = 0; j0 < i; j0 += 64) {  // coefficients in chunks of 64 (LDS)
+            const int jn = (i - j0) < 64 ? (i - j0) : 64;
+            // coefficient j0 + lane summed over the workgroups: quarter w takes every fourth partial
+            double cq = 0.0;
+            if (lane < jn) {
+#pragma unroll 8
+                for (int q = w; q < G; q += kPgThreads / 64) cq += part[(size_t)q * P + j0 + lane];
+            }
+            __syncthreads();  // (also orders the A v stores before the reads below)
+            qsum[w][lane] = cq;
+            __syncthreads();
+            if (tid < jn) coef_s[tid] = S[j0 + tid] * ((qsum[0][tid] + qsum[1][tid]) + (qsum[2][tid] + qsum[3][tid]));
+            __syncthreads();
+            for (int64_t row = a0 + tid; row < a1; row += kPgThreads) {
+                double acc = U[row + (size_t)i * ldu];
                 for (int jj = 0; jj < jn; ++jj) acc -= coef_s[jj] * U[row + (size_t)(j0 + jj) * ldu];
                 U[row + (size_t)i * ldu] = acc;
             }
         }
+        __syncthreads();
         for (int64_t row = a0 + tid; row < a1; row += kPgThreads) {
             const double u = U[row + (size_t)i * ldu];
             su += u * u;

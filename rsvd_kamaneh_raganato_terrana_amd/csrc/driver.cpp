@@ -409,7 +409,7 @@ static int sync_flags(rsvd_handle_t h, int* flags) {
     RSVD_TRY(set_device(h));
     RSVD_CK(hipMemcpyAsync(flags, h->dflags, kFlagWords * sizeof(int), hipMemcpyDeviceToHost, h->stream));
     RSVD_CK(hipStreamSynchronize(h->stream));
-    const int sticky[4] = {kFlagGramTimeout, kFlagJacobiTimeout, kFlagUnrepaired, kFlagNonFinite};
+    const int sticky[5] = {kFlagGramTimeout, kFlagJacobiTimeout, kFlagUnrepaired, kFlagNonFinite, kFlagFewRows};
     bool any = false;
     for (int w : sticky) any = any || flags[w] != 0;
     if (!any) return RSVD_OK;
@@ -420,8 +420,13 @@ static int sync_flags(rsvd_handle_t h, int* flags) {
         return RSVD_ERR_HIP;
     }
     if (flags[kFlagJacobiTimeout]) {
-        h->err = "the block Jacobi grid barrier timed out";
+        h->err = "a persistent grid's barrier timed out (block Jacobi grid barrier or the tridiagonalisation's "
+                 "hand-off: the abort word was raised and every workgroup left)";
         return RSVD_ERR_HIP;
+    }
+    if (flags[kFlagFewRows]) {  // (wide.cpp: every rank sums the same count, so all of them report it)
+        h->err = "l > min(m, n) not supported (m: the global row count of the sharded A)";
+        return RSVD_ERR_UNSUPPORTED;
     }
     if (flags[kFlagUnrepaired]) {
         h->err = "a rank-deficient panel could not be re-orthonormalised";

@@ -22,7 +22,8 @@ struct rsvd_handle_s {
     // power-method triplets kept -- reset at the start of every run; and the STICKY error words
     // (kept across queued runs, cleared when rsvd_sync / rsvd_get_info report them):
     // [2] Gram hand-off timeout, [3] block-Jacobi barrier timeout, [20] a rank-deficiency repair
-    // pass that broke down again, [21] non-finite singular values.
+    // pass that broke down again, [21] non-finite singular values, [22] a row-sharded run whose global
+    // row count is below l.
     int* dflags = nullptr;
     rsvd_info_t info{};
     int rank = 0, world = 1;
@@ -63,7 +64,8 @@ struct rsvd_handle_s {
     } while (0)
 
 constexpr int kFlagWords = 32;
-constexpr int kFlagGramTimeout = 2, kFlagJacobiTimeout = 3, kFlagUnrepaired = 20, kFlagNonFinite = 21;
+constexpr int kFlagGramTimeout = 2, kFlagJacobiTimeout = 3, kFlagUnrepaired = 20, kFlagNonFinite = 21,
+              kFlagFewRows = 22;
 // the split-Gram fallback test (wide.cpp cholqr_pass) and its factor's breakdown count (never read)
 constexpr int kFlagSplitIll = 24, kFlagSplitScratch = 25;
 

@@ -29,6 +29,10 @@ hipError_t launch_scale_cols(T* X, int64_t rows, int cols, int64_t ld, double f,
 // *flag |= 1 when any of x[0..n) is not finite
 template <typename T>
 hipError_t launch_check_finite(const T* x, int n, int* flag, hipStream_t s);
+// *cnt = v (one fp64 word; the row count a sharded run sums with its first m-side Gram all-reduce)
+hipError_t launch_set_count(double* cnt, int64_t v, hipStream_t s);
+// *flag = 1 when *cnt (the summed global row count) is below l
+hipError_t launch_check_rows(const double* cnt, int l, int* flag, hipStream_t s);
 
 // Fallback re-orthonormalisation of P into Q (CGS2 + deterministic random completion) when
 // *flag != 0; returns immediately otherwise.  One workgroup.

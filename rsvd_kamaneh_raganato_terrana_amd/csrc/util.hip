@@ -87,6 +87,13 @@ __global__ void check_finite_kernel(const T* __restrict__ x, int n, int* __restr
     if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
 }
 
+// The global row count of a row-sharded A: *cnt = this rank's rows, summed by the
+// first m-side Gram all-reduce; the check flags l > m_global (every rank sees the same sum).
+__global__ void set_count_kernel(double* __restrict__ cnt, double v) { *cnt = v; }
+__global__ void check_rows_kernel(const double* __restrict__ cnt, int l, int* __restrict__ flag) {
+    if (*cnt + 0.5 < (double)l) *flag = 1;
+}
+
 inline int grid_for(int64_t work, int block) {
     int64_t g = (work + block - 1) / block;
     if (g > 4096) g = 4096;
@@ -135,6 +142,16 @@ hipError_t launch_scale_cols(T* X, int64_t rows, int cols, int64_t ld, double f,
 template <typename T>
 hipError_t launch_check_finite(const T* x, int n, int* flag, hipStream_t s) {
     hipLaunchKernelGGL((check_finite_kernel<T>), dim3(std::min(64, (n + 255) / 256)), dim3(256), 0, s, x, n, flag);
+    return hipGetLastError();
+}
+
+hipError_t launch_set_count(double* cnt, int64_t v, hipStream_t s) {
+    hipLaunchKernelGGL(set_count_kernel, dim3(1), dim3(1), 0, s, cnt, (double)v);
+    return hipGetLastError();
+}
+
+hipError_t launch_check_rows(const double* cnt, int l, int* flag, hipStream_t s) {
+    hipLaunchKernelGGL(check_rows_kernel, dim3(1), dim3(1), 0, s, cnt, l, flag);
     return hipGetLastError();
 }
 

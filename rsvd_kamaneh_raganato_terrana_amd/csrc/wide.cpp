@@ -121,7 +121,7 @@ struct WideLayout {
         off_X8 = take(s8 ? (size_t)npad * LP : 0);
         off_pslab = take(sizeof(T) * std::max<int64_t>(pslab, 1) * LP);
         off_gslab = take(sizeof(double) * gslab);
-        off_G = take(sizeof(double) * L2);
+        off_G = take(sizeof(double) * (L2 + 1));  // (+1: the global row count rides the first m-side all-reduce)
         off_R = take(sizeof(double) * L2);
         off_Rinv = take(sizeof(double) * L2);
         off_W = take(sizeof(double) * L2);
@@ -197,6 +197,10 @@ struct WideEngine {
         colflag = reinterpret_cast<int*>(b + L.off_colflag);
         sync = reinterpret_cast<unsigned*>(b + L.off_sync);
     }
+
+    // world > 1: G[LP^2] holds this rank's row count until the first m-side Gram all-reduce sums it
+    // with the Gram; a global count below l then raises kFlagFewRows (rsvd_sync: RSVD_ERR_UNSUPPORTED)
+    bool count_pending = false;
 
     int allreduce(void* buf, int64_t count, int32_t dt) {
         if (h->world <= 1 || !h->allreduce) return RSVD_OK;
@@ -338,7 +342,14 @@ struct WideEngine {
             return RSVD_OK;
         }
         RSVD_CK(launch_gram_wide<T>(P, nullptr, rows, L.LP, gp, gslab, G, pred, s));
-        if (sharded) RSVD_TRY(allreduce(G, (int64_t)L.LP * L.LP, RSVD_F64));
+        if (sharded) {
+            const bool cnt = count_pending && rows == L.m && !pred;
+            RSVD_TRY(allreduce(G, (int64_t)L.LP * L.LP + (cnt ? 1 : 0), RSVD_F64));
+            if (cnt) {
+                count_pending = false;
+                RSVD_CK(launch_check_rows(G + (size_t)L.LP * L.LP, L.l, h->dflags + kFlagFewRows, s));
+            }
+        }
         if (pred)
             RSVD_CK(launch_chol_wide(G, L.l, L.LP, tol(), R, Rinv, r32, colflag, flag, W, pred, s, 0.0, nullptr, nullptr,
                                      mt));
@@ -594,6 +605,10 @@ int wide_typed(rsvd_handle_t h, const rsvd_desc_t* d, const void* A, const void*
         E.m_total = d->m;
     }
     E.m_norm = (int64_t)h->world * d->m;
+    if (h->world > 1 && h->allreduce) {
+        RSVD_CK(launch_set_count(E.G + (size_t)L.LP * L.LP, d->m, h->stream));
+        E.count_pending = true;
+    }
     RSVD_TRY(E.load_omega(omega, ldo, d->seed));
     if (Qout) {
         RSVD_TRY(E.range_finder(A, d->lda, d->q));

@@ -84,7 +84,9 @@ __device__ __forceinline__ double block_sum512(double x, double* red, int& tog) 
 
 // The fence-free group hand-off of wide_svd.hip (MI355X_MICROARCH.md "Hand-offs measured with sc1
 // loads", first row): sc1 stores, vmcnt(0) in every storing wave, one agent-scope add, sc1 poll.
-__device__ bool tri_barrier(unsigned* sync, unsigned target) {
+// `inject` (RSVD_TRI_FORCE_ABORT, fault injection for the tests): this member arrives, then takes the
+// timeout branch at once -- the abort word goes up and every other member leaves at its next spin check.
+__device__ bool tri_barrier(unsigned* sync, unsigned target, bool inject = false) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     __shared__ int ok;
@@ -93,7 +95,11 @@ __device__ bool tri_barrier(unsigned* sync, unsigned target) {
         __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         int good = 1;
         long spins = 0;
-        while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+        if (inject) {
+            __hip_atomic_store(sync + kTriAbort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            good = 0;
+        }
+        while (good && __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
             __builtin_amdgcn_s_sleep(1);
             if ((++spins & 1023) == 0 &&
                 (__hip_atomic_load(sync + kTriAbort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0 ||
@@ -222,7 +228,7 @@ __global__ __launch_bounds__(kEigThreads) void tridiag_kernel(const double* __re
                                                               double* __restrict__ dvec, double* __restrict__ evec,
                                                               double* __restrict__ taus, double* __restrict__ dump,
                                                               double* __restrict__ xch, unsigned* __restrict__ sync,
-                                                              int* __restrict__ info, int noskip) {
+                                                              int* __restrict__ info, int noskip, int abort_at) {
     constexpr int G = 64 / LPR;
     constexpr int RPW = 8 * G * RPL;                     // rows per member
     constexpr int XS = NW * RPW + 8 * NW + kEigMaxN;     // one parity's exchange slots: p, v.p partials, row
@@ -364,7 +370,7 @@ __global__ __launch_bounds__(kEigThreads) void tridiag_kernel(const double* __re
         double pj = 0.0, rj = 0.0, pl1, kk = 0.0;
         const int j = tid;  // t <= 512 = kEigThreads
         if constexpr (NW > 1) {
-            if (!tri_barrier(sync, (unsigned)NW * (unsigned)(k - kbeg + 1))) {
+            if (!tri_barrier(sync, (unsigned)NW * (unsigned)(k - kbeg + 1), k == abort_at && wg == 0)) {
                 if (tid == 0) info[2] = 1;
                 return;
             }
@@ -1155,8 +1161,15 @@ hipError_t launch_tridiag(const double* src, int lds, int n, int off, int kend, 
         const char* v = std::getenv("RSVD_TRI_NOSKIP");
         return v ? std::atoi(v) : 0;
     }();
+    // RSVD_TRI_FORCE_ABORT=k (fault injection, tests/test_gpu_eig.py): member 0 of the multi-workgroup
+    // phase takes the hand-off's timeout branch at step k, as if a member had stalled -- the abort word,
+    // the sticky timeout flag (rsvd_sync: RSVD_ERR_HIP) and every member's exit are exercised
+    static const int abort_at = [] {
+        const char* v = std::getenv("RSVD_TRI_FORCE_ABORT");
+        return v ? std::atoi(v) : -1;
+    }();
     return launch_coresident(tridiag_kernel<RPL, CPL, LPR, NW>, dim3(NW), dim3(kEigThreads), 0, s, src, lds, n, off,
-                             kend, Y, ldy, d, e, taus, dump, xch, sync, info, noskip);
+                             kend, Y, ldy, d, e, taus, dump, xch, sync, info, noskip, abort_at);
 }
 
 constexpr int kTailRows = 192;  // phase 2 (one workgroup) takes the last kTailRows rows

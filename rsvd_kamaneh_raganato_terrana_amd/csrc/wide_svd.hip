@@ -1011,11 +1011,14 @@ hipError_t bj_launch(const double* src, int64_t lds, int src_rowmajor, int mrv, 
     // the persistent grid (LP / 32 pair slots x G row-group members) must be co-resident: fewer
     // members per pair when the device cannot hold it (LP = 4096: 128 x 4 workgroups of 512
     // threads), and a refusal when even one member per pair does not fit
-    while (G > 1 && (int64_t)(LP / 32) * G > coresident_capacity(block_jacobi_kernel, kBJThreads,
-                                                                   block_jacobi_lds(MR / G)))
+    auto cap = [&](int g) { return coresident_capacity(block_jacobi_kernel, kBJThreads, block_jacobi_lds(MR / g)); };
+    int64_t c = cap(G);
+    while (c >= 0 && G > 1 && (int64_t)(LP / 32) * G > c) {
         G = G / 2 >= 1 && block_jacobi_groups(MR, LP, G / 2) ? G / 2 : 1;
-    if ((int64_t)(LP / 32) * G > coresident_capacity(block_jacobi_kernel, kBJThreads, block_jacobi_lds(MR / G)))
-        return hipErrorCooperativeLaunchTooLarge;
+        c = cap(G);
+    }
+    if (c < 0) return (hipError_t)(-c);  // the occupancy query failed (not a size problem)
+    if ((int64_t)(LP / 32) * G > c) return hipErrorCooperativeLaunchTooLarge;
     hipError_t e = hipMemsetAsync(sync, 0, kSyncWords * sizeof(unsigned), s);
     if (e != hipSuccess) return e;
     e = launch_coresident(block_jacobi_kernel, dim3(LP / 32 * G), dim3(kBJThreads), block_jacobi_lds(MR / G), s, src,

@@ -221,3 +221,61 @@ def test_row_sharded_world2_shard_smaller_than_l(case):
     dense_big.cpp path: its m-side basis workspace is sized by l, not by the local rows) and 200 rows
     per rank at l = 256 (the wide engine, n side sharded).  Against the oracle, 1e-4."""
     _check_world2(case, case[2] <= 512)
+
+
+def _worker_refused(rank, port, m_local, n, l, q):
+    try:
+        sys.path.insert(0, REPO)
+        import torch
+        import torch.distributed as dist
+
+        import rsvd_kamaneh_raganato_terrana_amd as R
+
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=2)
+        torch.cuda.set_device(0)
+        g = torch.Generator().manual_seed(rank)
+        Ag = torch.randn(n, m_local, generator=g).cuda().to(torch.bfloat16).t()
+        eng = R.Engine(0)
+        eng.set_comm(rank, 2, shard_n=True)
+        msg = None
+        try:
+            eng.rsvd(Ag, l, q=1, seed=7)
+        except Exception as e:  # the expected refusal (RSVD_ERR_UNSUPPORTED)
+            msg = str(e)
+        # the handle is usable afterwards: a legal request on the same ranks runs
+        U, S, V = eng.rsvd(Ag, 32, q=1, seed=7)
+        torch.cuda.synchronize()
+        ok_after = bool(torch.isfinite(S).all())
+        eng.close()
+        dist.destroy_process_group()
+        q.put((rank, msg, ok_after))
+    except Exception:  # pragma: no cover - reported through the queue
+        import traceback
+
+        q.put((rank, "worker failed: " + traceback.format_exc(), False))
+
+
+@pytest.mark.parametrize("l", [256, 600])
+def test_row_sharded_world2_global_rows_below_l(l):
+    """two shards of 100 (l = 256, the wide engine) or 250 rows (l = 600, dense_big.cpp)
+    whose GLOBAL row count is below l.  The reference needs l <= min(m, n) of the global A
+    (src/rSVD.cpp:20-23 partitions m); both ranks must refuse with RSVD_ERR_UNSUPPORTED, not run into
+    a CholeskyQR breakdown.  The wide engine sums the count with its first m-side Gram all-reduce and
+    reports it through rsvd_sync; the handle stays usable for the next (legal) request."""
+    import torch.multiprocessing as mp
+
+    m_local = 100 if l == 256 else 250
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_refused, args=(r, port, m_local, 700, l, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, msg, ok_after in res:
+        assert msg is not None and "global row count" in msg, (rank, msg)
+        assert ok_after, rank

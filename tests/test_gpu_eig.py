@@ -223,3 +223,54 @@ def test_eig_small_svd_small_sigma(engine):
     err = np.abs(S - So)
     assert np.all(err[small] <= bound[small]), (err[small].max(), np.argmax(err[small] / bound[small]), sweeps)
     assert rel_fro(S, So) < 1e-4
+
+
+_ABORT = r"""
+import json, sys
+sys.path.insert(0, {repo!r})
+import numpy as np, torch
+import rsvd_kamaneh_raganato_terrana_amd as R
+from rsvd_kamaneh_raganato_terrana_amd._capi import RSVDError
+rng = np.random.default_rng(3)
+m, n, l = 1200, 900, 256
+A = np.linalg.qr(rng.standard_normal((m, 400)))[0] * 0.97 ** np.arange(400) @ np.linalg.qr(rng.standard_normal((n, 400)))[0].T
+eng = R.Engine(0)
+msgs = []
+for rep in range(2):
+    try:
+        eng.rsvd(torch.from_numpy(A.astype(np.float32)).cuda().t().contiguous().t(), l, q=1, seed=9)
+        msgs.append(None)
+    except RSVDError as e:
+        msgs.append((e.status, str(e)))
+# the handle and the device are healthy afterwards: an fp64 run (block-Jacobi small SVD) is exact
+U, S, V = eng.rsvd(torch.from_numpy(A).cuda().t().contiguous().t(), 64, q=1, seed=9)
+torch.cuda.synchronize()
+Ud = U.cpu().numpy()
+print("RESULT " + json.dumps({{"msgs": msgs, "orth": float(np.linalg.norm(Ud.T @ Ud - np.eye(64))),
+                              "s0": float(S[0])}}))
+eng.close()
+"""
+
+
+def test_tridiag_abort_path_is_reported():
+    """the tridiagonalisation's multi-workgroup hand-off has a bounded spin and
+    an abort word that had never executed.  RSVD_TRI_FORCE_ABORT=3 (read once per process, so in a
+    child) makes member 0 take the timeout branch at step 3 of phase 1 (l = 256 > 192: four
+    workgroups).  The other members must leave at their next spin check (no hang: the child finishes
+    inside the timeout), the run must fail with a named status (RSVD_ERR_HIP, "timed out") through
+    rsvd_sync -- twice in a row, since the sticky word is cleared when reported -- and the same
+    handle must then run an fp64 rSVD (block-Jacobi small SVD, no tridiagonalisation) correctly."""
+    import json
+    import subprocess
+
+    env = dict(os.environ, RSVD_TRI_FORCE_ABORT="3")
+    p = subprocess.run([sys.executable, "-c", _ABORT.format(repo=REPO)], env=env, capture_output=True, text=True,
+                       timeout=110)
+    assert p.returncode == 0, p.stderr[-3000:]
+    line = [x for x in p.stdout.splitlines() if x.startswith("RESULT ")][-1]
+    r = json.loads(line[7:])
+    for msg in r["msgs"]:
+        assert msg is not None, r
+        status, text = msg
+        assert status == 3 and "timed out" in text, r  # RSVD_ERR_HIP
+    assert r["orth"] < 1e-10 and abs(r["s0"] - 1.0) < 1e-3, r
