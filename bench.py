@@ -446,7 +446,6 @@ def main():
     key = f"{args.config}_{dt}_{m_local}x{n}_l{l}_q{q}"
     lowp = dt in ("bf16", "fp8")
     per_op = 1  # kernel dispatches per timed projection (the HIP events bracket the whole product)
-    merged_off = os.environ.get("RSVD_HALF_MERGE") == "0"  # LP = 512 e4m3 halves as two dispatches
     if lowp:  # the LDS-DMA kernels (hi/lo split skinny operand): wproj3 (bf16, LP 256 / 512; TN at
         # LP 256 with two-step A slots: wproj3tn2), wproj3tn4 (e4m3 TN, four-step A slots),
         # wproj2<FP8, NN, LP, SPLIT> otherwise
@@ -460,15 +459,12 @@ def main():
             kpref = "wproj3_kernel<true, 128, true"  # the hi / lo NN at LP = 128 on the v3 kernel
         elif dt == "fp8" and LPk == 512 and nn and os.environ.get("RSVD_NN8", "1") != "0":
             kpref = "wproj3nn8_kernel<true"  # e4m3 NN halves on the v3 addressing, one dispatch
-            per_op = 2 if merged_off else 1
-        elif dt == "fp8" and LPk in (256, 512) and not nn and os.environ.get("RSVD_FP8_TN4") != "0":
-            kpref = "wproj3tn4_kernel<true"  # e4m3 TN, 128-B A lines; LP = 512 as two column halves
-            per_op = LPk // 256 if merged_off else 1  # (both halves in one dispatch by default)
+        elif dt == "fp8" and LPk in (256, 512) and not nn:
+            kpref = "wproj3tn4_kernel<true"  # e4m3 TN, 128-B A lines; LP = 512 as two column halves in one dispatch
         elif dt == "bf16" and LPk in (256, 512):
             kpref = f"wproj3_kernel<{'true' if nn else 'false'}, {LPk}, true"
         elif dt == "fp8" and LPk == 512:  # two 256-column halves per product (WProjPlan::half), one dispatch
             kpref = f"wproj2_kernel<true, {'true' if nn else 'false'}, 256, true"
-            per_op = 2 if merged_off else 1
         else:
             kpref = f"wproj2_kernel<{'true' if dt == 'fp8' else 'false'}, {'true' if nn else 'false'}, {LPk}, true"
     else:
@@ -510,8 +506,7 @@ def main():
             sk = {"bound": "hbm", "achieved": sk_gbs, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": sk_gbs / PEAK_HBM_GBS}
         else:
             sk = {"bound": "mfma", "achieved": sk_tf, "peak": sk_peak, "unit": "TFLOP/s", "frac": sk_tf / sk_peak}
-        sk.update({"kernel": "sketch Y = A Omega" + (" (e4m3 x e4m3, " + ("v_mfma_f32_16x16x32_fp8_fp8" if os.environ.get("RSVD_FP8_SCALED") == "0"
-                                          else "block-scaled v_mfma_scale_f32_16x16x128_f8f6f4, unit scales") + ")"
+        sk.update({"kernel": "sketch Y = A Omega" + (" (e4m3 x e4m3, block-scaled v_mfma_scale_f32_16x16x128_f8f6f4, unit scales)"
                                           if dt == "fp8" else ""),
                    "avg_launch_us": sk_s * 1e6, "achieved_TFLOPs": sk_tf, "achieved_GBps": sk_gbs, "launches_timed": sk_n})
         roof["sketch"] = sk

@@ -58,6 +58,9 @@ struct WideLayout {
     size_t off_Xn, off_Zn, off_Ym, off_Qm, off_T1, off_Xh, off_Xl, off_Qh, off_Ql, off_X8, off_pslab, off_gslab;
     size_t off_G, off_R, off_Rinv, off_W, off_R1, off_Uw, off_Vw, off_JX, off_JJ, off_M32, off_MS, off_colflag, off_sync,
         off_E, total;
+    // the deferred second CholeskyQR pass (fp32 results): the factor's R (scratch), R2^-1 of the m and n
+    // output panels, their products with U_w / V_w and a temp
+    size_t off_R2s = 0, off_R2m = 0, off_R2n = 0, off_Mu = 0, off_Mv = 0, off_Tmp = 0;
 
     int64_t mpad, npad;  // bf16 panel rows, zero-padded to a multiple of 32 (wproj2 reads whole k-steps)
     bool s8 = false;     // the sketch runs e4m3 x e4m3 on the fp8 MFMA
@@ -138,6 +141,14 @@ struct WideLayout {
         off_sync = take(sizeof(unsigned) * kBJSyncWords);
         // the eigensolver's small SVD (fp32 results, 128 <= LP <= 512: wide_eig.hip)
         off_E = take(sizeof(T) == 4 && LP >= 128 && LP <= 512 ? sizeof(double) * eig_svd_ws_doubles(LP) : 0);
+        if (sizeof(T) == 4) {
+            off_R2s = take(sizeof(double) * L2);
+            off_R2m = take(sizeof(double) * L2);
+            off_R2n = take(sizeof(double) * L2);
+            off_Mu = take(sizeof(double) * L2);
+            off_Mv = take(sizeof(double) * L2);
+            off_Tmp = take(sizeof(double) * L2);
+        }
         total = o;
     }
 };
@@ -196,7 +207,28 @@ struct WideEngine {
         Ms = sizeof(T) == 4 ? reinterpret_cast<bf16_t*>(b + L.off_MS) : nullptr;
         colflag = reinterpret_cast<int*>(b + L.off_colflag);
         sync = reinterpret_cast<unsigned*>(b + L.off_sync);
+        if (sizeof(T) == 4) {
+            R2s = reinterpret_cast<double*>(b + L.off_R2s);
+            R2m = reinterpret_cast<double*>(b + L.off_R2m);
+            R2n = reinterpret_cast<double*>(b + L.off_R2n);
+            Mu = reinterpret_cast<double*>(b + L.off_Mu);
+            Mv = reinterpret_cast<double*>(b + L.off_Mv);
+            Tmp = reinterpret_cast<double*>(b + L.off_Tmp);
+        }
     }
+
+    // Output panels (final Q, Q_B) of fp32-result runs defer CholeskyQR2's second pass (round 6):
+    // pass 1 gives T1 (orthonormal to ~eps_G cond^2, repaired when rank-deficient), and the exact
+    // basis Q = T1 R2^-1 (R2 = chol(T1^T T1)) is never formed: the next projection reads T1 itself
+    // (B^T = A^T Q = (A^T T1) R2^-1 -- T1 is as well conditioned as Q for the hi / lo operand), and
+    // R2^-1 enters only the l x l matrices: R = Q_B^T B^T = R2n^-T (T1z^T A^T T1) R2m^-1,
+    // U = T1 (R2m^-1 U_w), V = T1z (R2n^-1 V_w).  Same span, same R up to rounding (src/rSVD.cpp:60-68,
+    // 89, 128); two m x l / n x l panel products per rSVD become four l x l GEMMs (C5 -0.33 ms, C3
+    // -0.28 ms on one box).  Measured and dropped: the pass-2 Gram + factor on a side stream beside the
+    // next projection -- the projections run one workgroup per CU in a single wave of workgroups, so
+    // a CU the side stream holds delays the whole projection by about as long (C4 +0.03, C5 +0.08 ms).
+    bool defer = false;
+    double *R2s = nullptr, *R2m = nullptr, *R2n = nullptr, *Mu = nullptr, *Mv = nullptr, *Tmp = nullptr;
 
     // world > 1: G[LP^2] holds this rank's row count until the first m-side Gram all-reduce sums it
     // with the Gram; a global count below l then raises kFlagFewRows (rsvd_sync: RSVD_ERR_UNSUPPORTED)
@@ -291,22 +323,61 @@ struct WideEngine {
     // fp64 Gram and factor run again.
     static constexpr double kSplitIllTol = 1e-7;
     bool split_gram = false;
-    int split_cross = 3;  // RSVD_GSPLIT_X bits: 1 the split cross Gram at LP = 256, 2 at LP = 512
-    bool split_panel = false;  // panel products on the bf16 MFMA, three-piece split (RSVD_PANEL_SPLIT=0: fp32 MFMA)
+    static constexpr int split_cross = 3;  // bits: 1 the split cross Gram at LP = 256, 2 at LP = 512
+    bool split_panel = false;  // panel products on the bf16 MFMA, three-piece split (fp32 panels of bf16 / e4m3 A)
     bf16_t* Ms = nullptr;
     bf16_t* ms() const { return split_panel ? Ms : nullptr; }
-    // two-level factor: bit 0 at LP = 512, bit 1 at LP = 256 (RSVD_CHOL2 overrides; 0: one level
+    // two-level factor: bit 0 at LP = 512, bit 1 at LP = 256 (0 would be one level
     // everywhere).  Round 4 default 3: with the K-split 128^3 / 256^3 products (four waves per tile)
     // and the DPP diagonal factor, tools/wide_lab chol: LP = 256 one level 157.8 us vs two levels
     // 145.5 us; LP = 512 two levels 350.2 us vs three (each 256 level itself two-level) 321.8 us
-    int chol2 = 3;
+    static constexpr int chol2 = 3;
     // LP = 512 with bit 1 also set: each 256-column level is itself two-level (three levels of 128)
     int chol_depth() const { return (L.LP == 512 && (chol2 & 2)) ? 1 : 0; }
-    int bj_groups = 0;  // block-Jacobi row groups (0: auto; RSVD_BJ_GROUPS, for A/B runs)
+    static constexpr int bj_groups = 0;  // block-Jacobi row groups (0: auto)
     bool eig_svd = true;  // fp32 results: the small SVD through the eigensolver (RSVD_SMALL_SVD=jacobi: block Jacobi)
     // panel_gemm's operand in the panel precision: fp64 matrices as-is, fp32 copies for fp32 panels
     const T* mat(const double* m64, const float* m32) const {
         if constexpr (sizeof(T) == 8) return m64; else return m32;
+    }
+
+    // R = chol(P^T P) and R^-1 (Ro, Rio; with the fp32 copy and bf16 pieces of R^-1 when r32 / mt).
+    int gram_factor(const T* P, int64_t rows, const GramPlan& gp, bool sharded, int* flag, const int* pred, double* Ro,
+                    double* Rio, float* r32, bf16_t* mt) {
+        // LP = 256 / 512, l > LP / 2: the two-level factor (wide_qr.hip launch_chol_wide_2level; JX is
+        // free scratch until the small SVD) for unpredicated passes
+        const bool two = (chol2 & (L.LP == 512 ? 1 : (L.LP == 256 ? 2 : 0))) && L.l > L.LP / 2;
+        auto factor = [&](int* fl, double ill_tol, int* ill) -> hipError_t {
+            if (two)
+                return launch_chol_wide_2level(G, L.l, L.LP, tol(), Ro, Rio, r32, colflag, fl, W, JX, s, ill_tol, ill,
+                                               nullptr, chol_depth(), mt);
+            return launch_chol_wide(G, L.l, L.LP, tol(), Ro, Rio, r32, colflag, fl, W, nullptr, s, ill_tol, ill,
+                                    nullptr, mt);
+        };
+        if (split_gram && !sharded && !pred) {
+            int* ill = h->dflags + kFlagSplitIll;
+            RSVD_CK(launch_gram_split(reinterpret_cast<const float*>(P), rows, L.LP, gp, gslab, G, s));
+            RSVD_CK(factor(h->dflags + kFlagSplitScratch, kSplitIllTol, ill));
+            RSVD_CK(launch_gram_wide<T>(P, nullptr, rows, L.LP, gp, gslab, G, ill, s));
+            RSVD_CK(launch_chol_wide(G, L.l, L.LP, tol(), Ro, Rio, r32, colflag, flag, W, ill, s, 0.0, nullptr, nullptr,
+                                     mt));
+            return RSVD_OK;
+        }
+        RSVD_CK(launch_gram_wide<T>(P, nullptr, rows, L.LP, gp, gslab, G, pred, s));
+        if (sharded) {
+            const bool cnt = count_pending && rows == L.m && !pred;
+            RSVD_TRY(allreduce(G, (int64_t)L.LP * L.LP + (cnt ? 1 : 0), RSVD_F64));
+            if (cnt) {
+                count_pending = false;
+                RSVD_CK(launch_check_rows(G + (size_t)L.LP * L.LP, L.l, h->dflags + kFlagFewRows, s));
+            }
+        }
+        if (pred)
+            RSVD_CK(launch_chol_wide(G, L.l, L.LP, tol(), Ro, Rio, r32, colflag, flag, W, pred, s, 0.0, nullptr, nullptr,
+                                     mt));
+        else
+            RSVD_CK(factor(flag, 0.0, nullptr));
+        return RSVD_OK;
     }
 
     // One CholeskyQR pass Out = P chol(P^T P)^-1 (+ bf16 hi/lo of Out).  `pred`: predicated pass.
@@ -320,50 +391,54 @@ struct WideEngine {
         // the split panel product's pieces of R^-1, written by the factor with its fp32 copy (no
         // split_mat launch per pass; bit-identical)
         bf16_t* mt = (ms() && L.LP >= 128) ? ms() : nullptr;
-        // LP = 256 / 512, l > LP / 2: the two-level factor (wide_qr.hip launch_chol_wide_2level; JX is
-        // free scratch until the small SVD) for unpredicated passes
-        const bool two = (chol2 & (L.LP == 512 ? 1 : (L.LP == 256 ? 2 : 0))) && L.l > L.LP / 2;
-        auto factor = [&](int* fl, double ill_tol, int* ill) -> hipError_t {
-            if (two)
-                return launch_chol_wide_2level(G, L.l, L.LP, tol(), R, Rinv, r32, colflag, fl, W, JX, s, ill_tol, ill,
-                                               nullptr, chol_depth(), mt);
-            return launch_chol_wide(G, L.l, L.LP, tol(), R, Rinv, r32, colflag, fl, W, nullptr, s, ill_tol, ill,
-                                    nullptr, mt);
-        };
-        if (split_gram && !sharded && !pred) {
-            int* ill = h->dflags + kFlagSplitIll;
-            RSVD_CK(launch_gram_split(reinterpret_cast<const float*>(P), rows, L.LP, gp, gslab, G, s));
-            RSVD_CK(factor(h->dflags + kFlagSplitScratch, kSplitIllTol, ill));
-            RSVD_CK(launch_gram_wide<T>(P, nullptr, rows, L.LP, gp, gslab, G, ill, s));
-            RSVD_CK(launch_chol_wide(G, L.l, L.LP, tol(), R, Rinv, r32, colflag, flag, W, ill, s, 0.0, nullptr, nullptr,
-                                     mt));
-            RSVD_CK(launch_panel_gemm<T>(P, rows, L.LP, mat(Rinv, Rinv32), 1, Out, 0, 0, hi, lo, nullptr, s, ms(),
-                                         mt != nullptr));
-            return RSVD_OK;
-        }
-        RSVD_CK(launch_gram_wide<T>(P, nullptr, rows, L.LP, gp, gslab, G, pred, s));
-        if (sharded) {
-            const bool cnt = count_pending && rows == L.m && !pred;
-            RSVD_TRY(allreduce(G, (int64_t)L.LP * L.LP + (cnt ? 1 : 0), RSVD_F64));
-            if (cnt) {
-                count_pending = false;
-                RSVD_CK(launch_check_rows(G + (size_t)L.LP * L.LP, L.l, h->dflags + kFlagFewRows, s));
-            }
-        }
-        if (pred)
-            RSVD_CK(launch_chol_wide(G, L.l, L.LP, tol(), R, Rinv, r32, colflag, flag, W, pred, s, 0.0, nullptr, nullptr,
-                                     mt));
-        else
-            RSVD_CK(factor(flag, 0.0, nullptr));
-        RSVD_CK(launch_panel_gemm<T>(P, rows, L.LP, mat(Rinv, Rinv32), 1, Out, 0, 0, hi, lo, pred, s, ms(),
-                                     mt != nullptr));
+        RSVD_TRY(gram_factor(P, rows, gp, sharded, flag, pred, R, Rinv, r32, mt));
+        const bool split_path = split_gram && !sharded && !pred;
+        RSVD_CK(launch_panel_gemm<T>(P, rows, L.LP, mat(Rinv, Rinv32), 1, Out, 0, 0, hi, lo, split_path ? nullptr : pred,
+                                     s, ms(), mt != nullptr));
         return RSVD_OK;
+    }
+
+    // The rank-deficiency completion of an output panel Q (rows of this rank), predicated on `flag`
+    // (a breakdown in its orthonormalisation): flagged columns replaced by Philox Gaussian rows, one
+    // predicated CholeskyQR pass back into Q (+ hi / lo).
+    int repair(T* Q, int64_t rows, const GramPlan& gp, bool sharded, bf16_t* hi, bf16_t* lo, int* flag, bool mside,
+               bool nshard) {
+        // sharded panels draw disjoint stream rows per rank (rank 2^40 + local row), as the m side
+        const int64_t off = (mside || nshard) ? row_off : 0, tot = (mside || nshard) ? m_total : L.n;
+        const int64_t nrm = mside ? m_norm : L.n;
+        const int64_t valid = nshard ? std::max<int64_t>(0, std::min<int64_t>(L.nc, L.n - c0)) : rows;
+        RSVD_CK(launch_repair_panel<T>(Q, rows, L.l, L.LP, colflag, flag, seed ^ (0x5EEDull + orth_index), off, tot,
+                                       nrm, T1, s, valid));
+        // a breakdown in the repaired pass is reported (sticky) by rsvd_sync as RSVD_ERR_NUMERICAL
+        return cholqr_pass(T1, rows, gp, Q, sharded, hi, lo, h->dflags + kFlagUnrepaired, flag);
+    }
+
+    // The deferred form of an output panel's CholeskyQR2 (see `defer`): T1out = pass 1 (+ hi / lo, the
+    // repair), then R2^-1 = chol(T1^T T1)^-1 into r2inv.
+    int orth2_deferred(const T* P, bool mside, T* T1out, bf16_t* hi, bf16_t* lo, double* r2inv) {
+        const bool nshard = !mside && nsh;
+        const int64_t rows = mside ? L.m : (nshard ? L.nc : L.n);
+        const GramPlan& gp = mside ? L.gm : (nshard ? L.gnc : L.gn);
+        const bool sharded = (mside || nshard) && h->world > 1;
+        if (nshard) {
+            P += c0 * L.LP;
+            T1out += c0 * L.LP;
+            if (hi) hi += c0 * L.LP;
+            if (lo) lo += c0 * L.LP;
+        }
+        int* flag = h->dflags + 4 + (orth_index < 12 ? orth_index : 11);
+        ++orth_index;
+        RSVD_TRY(cholqr_pass(P, rows, gp, T1out, sharded, hi, lo, flag, nullptr));
+        RSVD_TRY(repair(T1out, rows, gp, sharded, hi, lo, flag, mside, nshard));
+        // pass 2's factor: T1 is orthonormal to ~eps_G cond^2 (or repaired), so a breakdown here means the
+        // panel could not be orthonormalised -- reported through the sticky kFlagUnrepaired
+        return gram_factor(T1out, rows, gp, sharded, h->dflags + kFlagUnrepaired, nullptr, R2s, r2inv, nullptr, nullptr);
     }
 
     // Q = orth(P): CholeskyQR (passes = 1) or CholeskyQR2; output panels (repair = true) get the
     // rank-deficiency completion (predicated on the breakdown flag of this orth).
     // The n side, sharded: P, Q, hi, lo are the full panels; this rank's rows [c0, c0 + nc) are used.
-    int orth(const T* P, bool mside, T* Q, int passes, bf16_t* hi, bf16_t* lo, bool repair) {
+    int orth(const T* P, bool mside, T* Q, int passes, bf16_t* hi, bf16_t* lo, bool repair_out) {
         const bool nshard = !mside && nsh;
         const int64_t rows = mside ? L.m : (nshard ? L.nc : L.n);
         const GramPlan& gp = mside ? L.gm : (nshard ? L.gnc : L.gn);
@@ -380,22 +455,13 @@ struct WideEngine {
         if (passes <= 1) {
             // bf16 / e4m3 A: a power-iteration intermediate is consumed only through its bf16 hi/lo
             // panels (the wproj kernels), so its fp32 copy is not written (-1/2 of the panel's writes)
-            T* out = (L.lowp && !repair && hi && lo) ? nullptr : Q;
+            T* out = (L.lowp && !repair_out && hi && lo) ? nullptr : Q;
             RSVD_TRY(cholqr_pass(P, rows, gp, out, sharded, hi, lo, flag, nullptr));
         } else {
             RSVD_TRY(cholqr_pass(P, rows, gp, T1, sharded, nullptr, nullptr, flag, nullptr));
             RSVD_TRY(cholqr_pass(T1, rows, gp, Q, sharded, hi, lo, flag, nullptr));
         }
-        if (repair) {
-            // sharded panels draw disjoint stream rows per rank (rank 2^40 + local row), as the m side
-            const int64_t off = (mside || nshard) ? row_off : 0, tot = (mside || nshard) ? m_total : L.n;
-            const int64_t nrm = mside ? m_norm : L.n;
-            const int64_t valid = nshard ? std::max<int64_t>(0, std::min<int64_t>(L.nc, L.n - c0)) : rows;
-            RSVD_CK(launch_repair_panel<T>(Q, rows, L.l, L.LP, colflag, flag, seed ^ (0x5EEDull + orth_index), off,
-                                           tot, nrm, T1, s, valid));
-            // a breakdown in the repaired pass is reported (sticky) by rsvd_sync as RSVD_ERR_NUMERICAL
-            RSVD_TRY(cholqr_pass(T1, rows, gp, Q, sharded, hi, lo, h->dflags + kFlagUnrepaired, flag));
-        }
+        if (repair_out) RSVD_TRY(repair(Q, rows, gp, sharded, hi, lo, flag, mside, nshard));
         return RSVD_OK;
     }
 
@@ -422,7 +488,10 @@ struct WideEngine {
         } else {
             RSVD_TRY(proj_nn(A, lda, Xn, Xh, nullptr, Ym, 2));  // the sketch: Omega is exactly bf16 (lowp)
         }
-        RSVD_TRY(orth(Ym, true, Qm, q == 0 ? 2 : inter_passes, Qh, Ql, q == 0));
+        if (q == 0 && defer)
+            RSVD_TRY(orth2_deferred(Ym, true, Qm, Qh, Ql, R2m));
+        else
+            RSVD_TRY(orth(Ym, true, Qm, q == 0 ? 2 : inter_passes, Qh, Ql, q == 0));
         for (int i = 0; i < q; ++i) {
             const bool last = i == q - 1;
             // RSVD_FLAG_LOWP_INTERMEDIATES: iterations before the last take the bf16 operand alone
@@ -431,7 +500,10 @@ struct WideEngine {
             RSVD_TRY(orth(Zn, false, Xn, inter_passes, Xh, Xl, false));
             RSVD_TRY(gather_x());
             RSVD_TRY(proj_nn(A, lda, Xn, Xh, one ? nullptr : Xl, Ym));
-            RSVD_TRY(orth(Ym, true, Qm, last ? 2 : inter_passes, Qh, Ql, last));
+            if (last && defer)
+                RSVD_TRY(orth2_deferred(Ym, true, Qm, Qh, Ql, R2m));
+            else
+                RSVD_TRY(orth(Ym, true, Qm, last ? 2 : inter_passes, Qh, Ql, last));
         }
         return RSVD_OK;
     }
@@ -467,8 +539,11 @@ struct WideEngine {
 
     int run(const rsvd_desc_t* d, const void* A, void* U, int64_t ldu, T* S, void* V, int64_t ldv) {
         RSVD_TRY(range_finder(A, d->lda, d->q));
-        RSVD_TRY(proj_tn(A, d->lda, Qm, Qh, Ql, Zn));               // B^T = A^T Q
-        RSVD_TRY(orth(Zn, false, Xn, 2, nullptr, nullptr, true));  // Q_B
+        RSVD_TRY(proj_tn(A, d->lda, Qm, Qh, Ql, Zn));  // B^T = A^T Q (deferred: A^T T1 = B^T R2m)
+        if (defer)
+            RSVD_TRY(orth2_deferred(Zn, false, Xn, nullptr, nullptr, R2n));  // T1z (Q_B = T1z R2n^-1)
+        else
+            RSVD_TRY(orth(Zn, false, Xn, 2, nullptr, nullptr, true));  // Q_B
         if (nsh) {  // R = Q_B^T B^T summed over the n shards
             RSVD_CK(launch_gram_wide<T>(Xn + c0 * L.LP, Zn + c0 * L.LP, L.nc, L.LP, L.gxc, gslab, R1, nullptr, s));
             RSVD_TRY(allreduce(R1, (int64_t)L.LP * L.LP, RSVD_F64));
@@ -480,6 +555,10 @@ struct WideEngine {
                                                 L.n, L.LP, L.gx, gslab, R1, s));
             else
                 RSVD_CK(launch_gram_wide<T>(Xn, Zn, L.n, L.LP, L.gx, gslab, R1, nullptr, s));
+        }
+        if (defer) {  // R = R2n^-T (T1z^T A^T T1) R2m^-1
+            RSVD_CK(launch_gemm_rm(0, 0, L.LP, R1, L.LP, R2m, L.LP, Tmp, L.LP, s));
+            RSVD_CK(launch_gemm_rm(1, 0, L.LP, R2n, L.LP, Tmp, L.LP, R1, L.LP, s));
         }
         // Inf / NaN in A reach R through B^T = A^T Q whatever the orthonormalisations did with them
         RSVD_CK(launch_check_finite<double>(R1, L.LP * L.LP, h->dflags + kFlagNonFinite, s));
@@ -501,6 +580,15 @@ struct WideEngine {
             RSVD_CK(launch_block_jacobi<double>(R1, L.l, L.LP, JX, JJ, Uw, Vw, Sd, sync, h->dflags + 1, s,
                                                 sizeof(T) == 4 ? 1e-8 : 1e-16, sizeof(T) == 4 ? kBJTolF32 : kBJTolF64,
                                                 bjg));
+        }
+        // deferred: U = T1 (R2m^-1 U_w), V = T1z (R2n^-1 V_w)
+        double* Uw = this->Uw;
+        double* Vw = this->Vw;
+        if (defer) {
+            RSVD_CK(launch_gemm_rm(0, 0, L.LP, R2m, L.LP, Uw, L.LP, Mu, L.LP, s));
+            RSVD_CK(launch_gemm_rm(0, 0, L.LP, R2n, L.LP, Vw, L.LP, Mv, L.LP, s));
+            Uw = Mu;
+            Vw = Mv;
         }
         // U_w / V_w pieces for the split final products, written with their fp32 copies and S (one launch)
         bf16_t* mu = (ms() && L.LP >= 128) ? Ms : nullptr;
@@ -561,33 +649,16 @@ int wide_typed(rsvd_handle_t h, const rsvd_desc_t* d, const void* A, const void*
     h->info.splits_tn = L.lowp ? L.wtn.splits : L.ptn.splits;
     WideEngine<T> E(h, L, d->dtype);
     E.qr_mode = d->qr_mode;
-    // the split Gram: fp32 panels of bf16 / e4m3 A (RSVD_GRAM_SPLIT=0 in the environment: fp64 Grams only)
+    // the split Gram: fp32 panels of bf16 / e4m3 A.  Diagnostic switches (each pinned against the oracle
+    // by tests/test_gpu_switches.py): RSVD_GRAM_SPLIT=0 fp64 Grams only, RSVD_SMALL_SVD=jacobi the block
+    // Jacobi small SVD for fp32 results instead of the eigensolver.
     {
         static const int env = [] {
             const char* v = std::getenv("RSVD_GRAM_SPLIT");
             return v ? std::atoi(v) : 1;
         }();
         E.split_gram = env != 0 && sizeof(T) == 4 && L.lowp && gram_split_ok(L.LP);
-        static const int env2 = [] {
-            const char* v = std::getenv("RSVD_CHOL2");
-            return v ? std::atoi(v) : 3;
-        }();
-        E.chol2 = env2;
-        static const int envx = [] {
-            const char* v = std::getenv("RSVD_GSPLIT_X");
-            return v ? std::atoi(v) : 3;
-        }();
-        E.split_cross = envx;
-        static const int env3 = [] {
-            const char* v = std::getenv("RSVD_PANEL_SPLIT");
-            return v ? std::atoi(v) : 1;
-        }();
-        E.split_panel = env3 != 0 && sizeof(T) == 4 && L.lowp && L.LP % 32 == 0 && L.LP >= 128;
-        static const int env4 = [] {
-            const char* v = std::getenv("RSVD_BJ_GROUPS");
-            return v ? std::atoi(v) : 0;
-        }();
-        E.bj_groups = env4;
+        E.split_panel = sizeof(T) == 4 && L.lowp && L.LP % 32 == 0 && L.LP >= 128;
         static const bool env5 = [] {
             const char* v = std::getenv("RSVD_SMALL_SVD");
             return !(v && std::string(v) == "jacobi");
@@ -595,6 +666,16 @@ int wide_typed(rsvd_handle_t h, const rsvd_desc_t* d, const void* A, const void*
         E.eig_svd = env5;
     }
     E.lowp_inter = (d->flags & RSVD_FLAG_LOWP_INTERMEDIATES) != 0;
+    {
+        // fp32 results, the rSVD proper (not the range finder's Q, not the power method: both use Q / Q_B
+        // themselves).  RSVD_DEFER2=0: Q and Q_B formed by the second passes, as before round 6 (A/B).
+        static const int env = [] {
+            const char* v = std::getenv("RSVD_DEFER2");
+            return v ? std::atoi(v) : 1;
+        }();
+        E.defer = env != 0 && sizeof(T) == 4 && !Qout && d->method != RSVD_SVD_POWER &&
+                  d->method != RSVD_SVD_POWER_IC && d->qr_mode == RSVD_QR_AUTO;
+    }
     E.seed = d->seed;
     E.nsh = L.nsh;
     E.c0 = L.nsh ? (int64_t)h->rank * L.nc : 0;

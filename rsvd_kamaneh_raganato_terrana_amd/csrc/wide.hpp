@@ -186,6 +186,9 @@ hipError_t launch_block_jacobi_given(int l, int LP, double* X, double* J, double
 // compact-WY back-transformation, X = W V_w; then launch_block_jacobi_given's check (and polish if
 // it fails) and finish.  ews: eig_svd_ws_doubles(LP) doubles; sync: kBJSyncWords words.
 size_t eig_svd_ws_doubles(int LP);
+// Z = op(X) op(Y) for n x n fp64 row-major matrices on the fp64 MFMA (tx / ty: transpose X / Y)
+hipError_t launch_gemm_rm(int tx, int ty, int n, const double* X, int ldx, const double* Y, int ldy, double* Z, int ldz,
+                          hipStream_t s);
 template <typename T>
 hipError_t launch_eig_svd(const double* R, int l, int LP, double* ews, double* X, double* J, double* Uw, double* Vw,
                           T* S, unsigned* sync, int* info, hipStream_t s, double tol_chk);

@@ -1084,17 +1084,20 @@ __global__ __launch_bounds__(256) void wy_apply_kernel(const double* __restrict_
 }
 
 // C = alpha op(A) op(B) + beta C for the eigensolver's small fp64 products (column-major, M, N,
-// K <= a few hundred): one wave per 16 x 16 tile of C (1024 waves at 512^2 -- gemm.hip's 64 x 64
+// K <= a few hundred): one workgroup per 16 x 16 tile of C (1024 at 512^2 -- gemm.hip's 64 x 64
 // tiles gave 64 workgroups there and ran 55 / 100 us at 256^3 / 512^3).  Within a 16-deep k chunk
 // the MFMA k order is k0 + 4 h + s (step s, lane half h): the A and B operands only have to agree on
 // it, and then a transposed operand (op = T: contiguous along k) is read as 32-B runs per lane,
 // a plain one (contiguous along i / j) as 128-B rows per 16 lanes.
 // (Cin: the beta term's C when it is not the output, same ld -- C = alpha op(A) op(B) + beta Cin)
 template <int TA, int TB>
-__global__ __launch_bounds__(64) void sqgemm_f64_kernel(int M, int N, int K, double alpha, const double* __restrict__ A,
-                                                        int lda, const double* __restrict__ B, int ldb, double beta,
-                                                        double* C, int ldc, const double* Cin) {
-    const int lane = threadIdx.x, r = lane & 15, h = lane >> 4;
+__global__ __launch_bounds__(256) void sqgemm_f64_kernel(int M, int N, int K, double alpha, const double* __restrict__ A,
+                                                         int lda, const double* __restrict__ B, int ldb, double beta,
+                                                         double* C, int ldc, const double* Cin) {
+    // round 6: four waves per tile, wave w taking every fourth 32-deep k chunk, the partial tiles summed
+    // in wave order through LDS (the one-wave form walked K = 512 as 16 dependent L2 round trips: 23 us)
+    __shared__ f64x4 part[3][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 15, h = lane >> 4;
     const int tm = (M + 15) / 16;
     const int bi = blockIdx.x % tm, bj = blockIdx.x / tm;
     const int i = 16 * bi + r, j = 16 * bj + r;
@@ -1108,8 +1111,7 @@ __global__ __launch_bounds__(64) void sqgemm_f64_kernel(int M, int N, int K, dou
         return TB ? B[(int64_t)k * ldb + j] : B[(int64_t)j * ldb + k];
     };
     f64x4 acc0 = MD::zero(), acc1 = MD::zero();
-    int k0 = 0;
-    for (; k0 + 32 <= K; k0 += 32) {
+    for (int k0 = 32 * w; k0 < K; k0 += 128) {
         double a[8], b[8];
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
@@ -1124,16 +1126,20 @@ __global__ __launch_bounds__(64) void sqgemm_f64_kernel(int M, int N, int K, dou
             acc1 = MD::mma(a[4 + s], b[4 + s], acc1);
         }
     }
-    for (; k0 < K; k0 += 16) {
+    f64x4 t;
 #pragma unroll
-        for (int s = 0; s < 4; ++s) acc0 = MD::mma(ld_a(k0 + 4 * h + s), ld_b(k0 + 4 * h + s), acc0);
-    }
+    for (int q = 0; q < 4; ++q) t[q] = acc0[q] + acc1[q];
+    if (w > 0) part[w - 1][lane] = t;
+    __syncthreads();
+    if (w != 0) return;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) t[q] = ((t[q] + part[0][lane][q]) + part[1][lane][q]) + part[2][lane][q];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
         const int ii = 16 * bi + MD::row(h, q);
         if (ii < M && jv) {
             double* c = C + (int64_t)j * ldc + ii;
-            const double v = alpha * (acc0[q] + acc1[q]);
+            const double v = alpha * t[q];
             *c = beta != 0.0 ? v + beta * (Cin ? Cin[(int64_t)j * ldc + ii] : *c) : v;
         }
     }
@@ -1144,7 +1150,7 @@ hipError_t launch_sqgemm(int ta, int tb, int M, int N, int K, double alpha, cons
     const dim3 grid(((M + 15) / 16) * ((N + 15) / 16));
 #define SQG(X, Y)                                                                                                    \
     if (ta == X && tb == Y) {                                                                                        \
-        hipLaunchKernelGGL((sqgemm_f64_kernel<X, Y>), grid, dim3(64), 0, s, M, N, K, alpha, A, lda, B, ldb, beta, C, \
+        hipLaunchKernelGGL((sqgemm_f64_kernel<X, Y>), grid, dim3(256), 0, s, M, N, K, alpha, A, lda, B, ldb, beta, C, \
                            ldc, Cin);                                                                                \
         return hipGetLastError();                                                                                    \
     }
@@ -1193,6 +1199,13 @@ void tri_prof_read(long long* out) {
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_tri_prof), z, sizeof(z));
 }
 #endif
+
+// Z = op(X) op(Y), n x n fp64 row-major (lds ldx / ldy / ldz): the column-major sqgemm on the
+// transposed views (Z^T = op(Y)^T op(X)^T)
+hipError_t launch_gemm_rm(int tx, int ty, int n, const double* X, int ldx, const double* Y, int ldy, double* Z, int ldz,
+                          hipStream_t s) {
+    return launch_sqgemm(ty, tx, n, n, n, 1.0, Y, ldy, X, ldx, 0.0, Z, ldz, s);
+}
 
 size_t eig_svd_ws_doubles(int LP) {
     const size_t L2 = (size_t)LP * LP;

@@ -1026,7 +1026,11 @@ hipError_t wproj3_go(const void* A, int64_t lda, int64_t m, int64_t n, const bf1
     float* o = p.splits == 1 ? Out : slabs;
     const int64_t stride = rows_out * LP;
     constexpr int KN = NN ? 3 : 0;  // as v2 (profiles/r02_wide_lab_knobs.txt)
+#ifdef RSVD_LAB
     constexpr bool ar_ok = ABL == 0 && SD == 1 && SH::NA >= 3;  // register-staged A fits
+#else
+    constexpr bool ar_ok = false;  // (the lab-only variants are built into tools/wide_lab alone)
+#endif
     auto go = [&](auto knc) {
         if constexpr (ar_ok) {
             if (p.abl & 16) {  // abl 16 (lab only): register-staged A
@@ -1040,6 +1044,7 @@ hipError_t wproj3_go(const void* A, int64_t lda, int64_t m, int64_t n, const bf1
                            dim3(512), SH::LDS, s, reinterpret_cast<const bf16_t*>(A), lda, rows_out, K, m, Shi, Slo, o,
                            stride, p.chunk, p.blocks);
     };
+#ifdef RSVD_LAB
     if constexpr (LP == 256 && ABL == 0 && SD == 1) {  // lab knob sweep (p.kn >= 0); the engine uses KN
         switch (p.kn < 0 ? KN : p.kn) {
             case 0: go(std::integral_constant<int, 0>{}); break;
@@ -1050,6 +1055,9 @@ hipError_t wproj3_go(const void* A, int64_t lda, int64_t m, int64_t n, const bf1
     } else {
         go(std::integral_constant<int, KN>{});
     }
+#else
+    go(std::integral_constant<int, KN>{});
+#endif
     hipError_t e = hipGetLastError();
     if (e == hipSuccess && done) e = hipEventRecord(done, s);
     if (e != hipSuccess || p.splits == 1) return e;
@@ -1656,21 +1664,28 @@ hipError_t wproj3tn2_go(const void* A, int64_t lda, int64_t m, int64_t n, const 
     float* o = p.splits == 1 ? Out : slabs;
     const int64_t stride = rows_out * 256;
     auto go = [&](auto knc) {  // LDS-DMA A; register-staged A only for the lab (abl 16)
-        if (!(p.abl & 16))
-            hipLaunchKernelGGL((wproj3tn2_kernel<SPLIT, decltype(knc)::value, false>), dim3(p.blocks * p.splits),
-                               dim3(512), lds, s, reinterpret_cast<const bf16_t*>(A), lda, rows_out, K, m, Shi, Slo, o,
-                               stride, p.chunk, p.blocks);
-        else
+#ifdef RSVD_LAB
+        if (p.abl & 16) {
             hipLaunchKernelGGL((wproj3tn2_kernel<SPLIT, decltype(knc)::value, true>), dim3(p.blocks * p.splits),
                                dim3(512), lds, s, reinterpret_cast<const bf16_t*>(A), lda, rows_out, K, m, Shi, Slo, o,
                                stride, p.chunk, p.blocks);
+            return;
+        }
+#endif
+        hipLaunchKernelGGL((wproj3tn2_kernel<SPLIT, decltype(knc)::value, false>), dim3(p.blocks * p.splits),
+                           dim3(512), lds, s, reinterpret_cast<const bf16_t*>(A), lda, rows_out, K, m, Shi, Slo, o,
+                           stride, p.chunk, p.blocks);
     };
+#ifdef RSVD_LAB
     switch (p.kn < 0 ? 0 : p.kn) {  // KN 0 in the engine; the others for the lab knob sweep
         case 1: go(std::integral_constant<int, 1>{}); break;
         case 2: go(std::integral_constant<int, 2>{}); break;
         case 3: go(std::integral_constant<int, 3>{}); break;
         default: go(std::integral_constant<int, 0>{}); break;
     }
+#else
+    go(std::integral_constant<int, 0>{});
+#endif
     hipError_t e = hipGetLastError();
     if (e == hipSuccess && done) e = hipEventRecord(done, s);
     if (e != hipSuccess || p.splits == 1) return e;
@@ -1977,6 +1992,7 @@ hipError_t wproj_lp(int nn, int fp8, const void* A, int64_t lda, int64_t m, int6
         return split ? wproj3_go<false, LP, true, SD>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d)        \
                      : wproj3_go<false, LP, false, SD>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d);      \
     }
+#ifdef RSVD_LAB
             if constexpr (LP == 256) {  // lab ablations of the C4 NN2 / TN2 kernels
                 if (p.abl && split) {
 #define AB(X) \
@@ -1986,6 +2002,7 @@ hipError_t wproj_lp(int nn, int fp8, const void* A, int64_t lda, int64_t m, int6
 #undef AB
                 }
             }
+#endif
             if constexpr (LP == 256) {  // (LP = 512 split: a third S slot does not fit)
                 if (!nn && p.tn2 && p.sd == 1)
                     return split ? wproj3tn2_go<true>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d)
@@ -2006,10 +2023,9 @@ hipError_t wproj_lp(int nn, int fp8, const void* A, int64_t lda, int64_t m, int6
             if (nn && p.nn8)
                 return split ? wproj3nn8_go<true>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d)
                              : wproj3nn8_go<false>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d);
-            if (nn) return split ? wproj2_half_go<true, true, true>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d)
-                                 : wproj2_half_go<true, true, false>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d);
-            return split ? wproj2_half_go<true, false, true>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d)
-                         : wproj2_half_go<true, false, false>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d);
+            // (RSVD_NN8=0, the round-4 kernel; every v2 e4m3 TN takes wproj3tn4 above)
+            return split ? wproj2_half_go<true, true, true>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d)
+                         : wproj2_half_go<true, true, false>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d);
         }
     }
     if constexpr (LP >= 128) {
@@ -2021,8 +2037,16 @@ hipError_t wproj_lp(int nn, int fp8, const void* A, int64_t lda, int64_t m, int6
         return split ? wproj2_go<F, false, LP, true>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d)        \
                      : wproj2_go<F, false, LP, false>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d);      \
     }
-            if (fp8) GO2(true);
-            GO2(false);
+            if (fp8) {  // (e4m3 at LP 256 / 512: the TN is wproj3tn4's, LP 512 runs as halves above)
+                if constexpr (LP == 128) GO2(true);
+                if constexpr (LP == 256) {
+                    if (nn) return split ? wproj2_go<true, true, LP, true>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d)
+                                         : wproj2_go<true, true, LP, false>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d);
+                }
+                return hipErrorInvalidValue;
+            }
+            if constexpr (LP == 128) GO2(false);  // (bf16 at LP 256 / 512: the v3 kernels above)
+            return hipErrorInvalidValue;
 #undef GO2
         }
     }
@@ -2045,14 +2069,6 @@ bool wproj_supported_lp(int LP) {
 }
 
 int wproj_rows_per_block(int LP) { return LP <= 128 ? 256 : (LP == 256 ? 128 : 64); }
-
-static bool tn4_enabled() {  // RSVD_FP8_TN4=0 in the environment: the wproj2 e4m3 TN (A/B)
-    static const int env = [] {
-        const char* v = std::getenv("RSVD_FP8_TN4");
-        return v ? std::atoi(v) : 1;
-    }();
-    return env != 0;
-}
 
 static int tn128_mode() {  // RSVD_TN128: 0 the v2 double-step LP = 128 TN, 1 rings 4 / 2 (default), 2 rings 3 / 3
     static const int env = [] {
@@ -2079,14 +2095,6 @@ static bool nn3_128_enabled() {  // RSVD_NN3_128=0 in the environment: the v2 bf
     return env != 0;
 }
 
-static bool half_merge_enabled() {
-    static const int env = [] {
-        const char* v = std::getenv("RSVD_HALF_MERGE");
-        return v ? std::atoi(v) : 1;
-    }();
-    return env != 0;
-}
-
 WProjPlan plan_wproj(int64_t rows_out, int64_t K, int LP, bool v2, bool nn, bool fp8) {
     WProjPlan p;
     p.v2 = v2 && LP >= 128;
@@ -2098,12 +2106,12 @@ WProjPlan plan_wproj(int64_t rows_out, int64_t K, int LP, bool v2, bool nn, bool
     p.half = p.v2 && fp8 && LP == 512;  // two LP = 256 column halves (wproj2_half_go)
     p.nn8 = p.half && nn && nn8_enabled();  // ... the e4m3 NN on wproj3nn8_kernel
     // e4m3 TN: four k-steps per A slot (wproj3tn4_kernel; K chunks of whole 128-row slots)
-    p.tn4 = p.v2 && fp8 && !nn && (LP == 256 || LP == 512) && tn4_enabled();
+    p.tn4 = p.v2 && fp8 && !nn && (LP == 256 || LP == 512);
     const int WI = p.v2 ? (LP == 128 ? (p.ds ? 256 : 512) : ((LP == 256 || p.half) ? 256 : 128))
                         : wproj_rows_per_block(LP);
     p.blocks = (int)((rows_out + WI - 1) / WI);
-    // LP = 512 e4m3 products as two 256-column halves in one launch (RSVD_HALF_MERGE=0: two launches)
-    p.merge = (p.half || (p.tn4 && LP == 512)) && half_merge_enabled();
+    // LP = 512 e4m3 products as two 256-column halves in one launch (twin workgroups adjacent)
+    p.merge = p.half || (p.tn4 && LP == 512);
     // one workgroup per CU (LDS ring / registers); merged halves: two workgroups per (row block, split)
     const int target = p.merge ? 128 : ((p.v2 || LP >= 512) ? 256 : 512);
     int64_t splits = (target + p.blocks - 1) / p.blocks;
@@ -2125,12 +2133,8 @@ hipError_t launch_wproj_s8(const void* A, int64_t lda, int64_t m, int64_t n, con
                            float* slabs, float* Out, hipStream_t s, hipEvent_t done) {
     if (!wproj_s8_supported(p, LP)) return hipErrorInvalidValue;
     const bf16_t* S = reinterpret_cast<const bf16_t*>(S8);
-    // the block-scaled K = 128 form when every stage is whole (RSVD_FP8_SCALED=0: the K = 32 form)
-    static const int env = [] {
-        const char* v = std::getenv("RSVD_FP8_SCALED");
-        return v ? std::atoi(v) : 1;
-    }();
-    const bool sc = env != 0 && n % 128 == 0 && p.chunk % 128 == 0;
+    // the block-scaled K = 128 form when every stage is whole (else the K = 32 form)
+    const bool sc = n % 128 == 0 && p.chunk % 128 == 0;
     if (sc) {
         if (LP == 256) return wproj2_go<true, true, 256, false, false, true, true>(A, lda, m, n, S, nullptr, p, slabs, Out, s, done);
         if (p.half) return wproj2_half_go<true, true, false, true, true>(A, lda, m, n, S, nullptr, p, slabs, Out, s, done);

@@ -115,7 +115,7 @@ __global__ __launch_bounds__(256) void gram_wide_kernel(const T* __restrict__ P,
 // costs two LDS reads per 4 rows.  Pairs are dealt round-robin to the waves (9 per wave at
 // LP = 256).  The old kernel gave each 32x32 block its own wave and chunk walk, re-reading every
 // panel row LP/32 + 1 times from HBM; here each byte is read once and the MFMA issue rate is the
-// bound.  Partial tiles land in the (chunk, 32x32 block) slab layout gram_reduce_kernel sums; the
+// bound.  Partial tiles land in the (chunk, 32x32 block) slab layout gram_reduce4_kernel sums; the
 // lower 16x16 sub-tile of a diagonal 32x32 block is written as the transpose of the upper one.
 // (ta, tb) of upper tile pair p (row-major over the upper triangle of NT x NT tiles); p >= NP -> (0, 0)
 constexpr int pair_ta(int NT, int p) {
@@ -284,7 +284,7 @@ __global__ __launch_bounds__(512) void gram_sym_kernel(const T* __restrict__ P, 
 // lane (r, h) of tile t reads rows 8h .. 8h + 7 of column 16t + r -- the A and the B fragment of
 // v_mfma_f32_16x16x32_bf16 alike (G = P^T P: both operands are "column, rows k" reads).
 // Upper tile pairs (ta <= tb) are dealt to the NH x 8 waves of a chunk at compile time; the
-// partial tiles go to gram_sym's (chunk, 32x32 block) slab layout, summed by gram_reduce_kernel.
+// partial tiles go to gram_sym's (chunk, 32x32 block) slab layout, summed by gram_reduce4_kernel.
 typedef __attribute__((ext_vector_type(8))) short bf16x8s;
 
 // Work split: the tiles are cut into groups of TG (4; 2 at LP = 128) and each wave owns one
@@ -293,7 +293,7 @@ typedef __attribute__((ext_vector_type(8))) short bf16x8s;
 // one fragment pair per tile pair read 1 KB per MFMA and made the kernel LDS-bound).  Diagonal
 // group pairs compute their TG^2 tile pairs in full and store the upper ones.  The fp32 MFMA
 // accumulators run over the whole row chunk (<= 1024 rows for the panels of the bf16 / e4m3
-// configs) and the chunk partials are summed in fp64 by gram_reduce_kernel.
+// configs) and the chunk partials are summed in fp64 by gram_reduce4_kernel.
 template <int LP> struct GramSplit {
     static constexpr int TG = LP == 128 ? 2 : 4;
     static constexpr int NT = LP / 16, NTG = NT / TG, NBK = NTG * (NTG + 1) / 2;
@@ -704,7 +704,7 @@ __global__ __launch_bounds__(GramSplit4::THREADS) void gram_split4_kernel(const 
 // -- 4 types at LP = 256, 16 at LP = 512.  A step stages 64 + 256 columns (octet units as
 // gram_split4_kernel, 60 KB, double-buffered); wave w takes X tiles 2 (w & 1) .. + 1 of the group and
 // Y tiles 4 (w >> 1) .. + 3 of the half -- 8 tile pairs, six MFMAs each.  Partial 32 x 32 blocks go
-// to the cross slab layout gram_reduce_kernel sums (blk = a nb + b).
+// to the cross slab layout gram_reduce4_kernel sums (blk = a nb + b).
 template <int LP_> struct GramSplitX {
     static constexpr int LP = LP_, NB = LP / 32, NBLK = NB * NB, WAVES = 8, THREADS = 64 * WAVES;
     static constexpr int GXN = LP / 64, GYN = LP / 256, TYPES = GXN * GYN;
@@ -850,51 +850,11 @@ __global__ __launch_bounds__(GramSplitX<LP_>::THREADS) void gram_split_cross_ker
         }
 }
 
-__global__ void gram_reduce_kernel(const double* __restrict__ slabs, int nblk, int nchunk, int LP, int cross,
-                                   double* __restrict__ G, const int* __restrict__ pred) {
-    if (pred && *pred == 0) return;
-    const int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    if (e >= (int64_t)nblk * 1024) return;
-    const int blk = (int)(e / 1024), loc = (int)(e % 1024);
-    const int nb = (LP + 31) / 32;
-    int a, b;
-    if (cross) {
-        a = blk / nb;
-        b = blk % nb;
-    } else {
-        int rem = blk;
-        a = 0;
-        while (rem >= nb - a) {
-            rem -= nb - a;
-            ++a;
-        }
-        b = a + rem;
-    }
-    const int ra = 32 * a + loc / 32, cb = 32 * b + loc % 32;
-    if (ra >= LP || cb >= LP) return;
-    // four interleaved partial sums (loads in flight), combined in a fixed order: deterministic
-    const int64_t cs = (int64_t)nblk * 1024;
-    const double* src = slabs + (int64_t)blk * 1024 + loc;
-    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
-    int c = 0;
-    for (; c + 4 <= nchunk; c += 4) {
-        s0 += src[(c + 0) * cs];
-        s1 += src[(c + 1) * cs];
-        s2 += src[(c + 2) * cs];
-        s3 += src[(c + 3) * cs];
-    }
-    for (; c < nchunk; ++c) s0 += src[c * cs];
-    const double s = (s0 + s1) + (s2 + s3);
-    G[(int64_t)ra * LP + cb] = s;
-    if (!cross && a != b) G[(int64_t)cb * LP + ra] = s;
-}
-
-// The same sum with more parallelism per entry: one workgroup = 64 Gram entries x 4 chunk ranges
-// (wave k sums chunks [k n / 4, (k + 1) n / 4) with four interleaved partials, a wave's 64 entries
-// one 512-B load per chunk), the ranges combined in a fixed order -- deterministic, but a different
-// order than gram_reduce_kernel.  C3's LP = 128 Gram (10 blocks, 256 chunks) ran gram_reduce_kernel
-// on 40 workgroups; this gives it 160.  Default; RSVD_GRAM_REDUCE4=0 selects gram_reduce_kernel (A/B,
-// one box: C4 23.81 -> 23.68 ms, C5 19.15 -> 19.13, C3 5.65 -> 5.62; gpurun_out r5a).
+// The chunk partials summed in a fixed order (deterministic): one workgroup = 64 Gram entries x 4
+// chunk ranges (wave k sums chunks [k n / 4, (k + 1) n / 4) with four interleaved partials, a wave's
+// 64 entries one 512-B load per chunk), the ranges combined in wave order.  (Round 4 replaced a
+// one-thread-per-entry sum: C3's LP = 128 Gram -- 10 blocks, 256 chunks -- ran that on 40 workgroups;
+// this gives it 160: C4 23.81 -> 23.68 ms, C5 19.15 -> 19.13, C3 5.65 -> 5.62 on one box.)
 __global__ __launch_bounds__(256) void gram_reduce4_kernel(const double* __restrict__ slabs, int nblk, int nchunk,
                                                            int LP, int cross, double* __restrict__ G,
                                                            const int* __restrict__ pred) {
@@ -947,17 +907,9 @@ __global__ __launch_bounds__(256) void gram_reduce4_kernel(const double* __restr
 
 hipError_t launch_gram_reduce(const double* slabs, int nblk, int nchunk, int LP, int cross, double* G, const int* pred,
                               hipStream_t s) {
-    static const int v4 = [] {
-        const char* e = std::getenv("RSVD_GRAM_REDUCE4");
-        return e ? std::atoi(e) : 1;
-    }();
     const int64_t tot = (int64_t)nblk * 1024;
-    if (v4)
-        hipLaunchKernelGGL(gram_reduce4_kernel, dim3((int)((tot + 63) / 64)), dim3(256), 0, s, slabs, nblk, nchunk, LP,
-                           cross, G, pred);
-    else
-        hipLaunchKernelGGL(gram_reduce_kernel, dim3((int)((tot + 255) / 256)), dim3(256), 0, s, slabs, nblk, nchunk,
-                           LP, cross, G, pred);
+    hipLaunchKernelGGL(gram_reduce4_kernel, dim3((int)((tot + 63) / 64)), dim3(256), 0, s, slabs, nblk, nchunk, LP,
+                       cross, G, pred);
     return hipGetLastError();
 }
 
@@ -2525,33 +2477,18 @@ hipError_t launch_gram_split(const float* P, int64_t rows, int LP, const GramPla
         constexpr int L = decltype(lpc)::value;
         typedef GramSplit<L> GS;
         const int grid = GS::NH == 1 ? gp.chunks : (gp.chunks + 7) / 8 * 8 * GS::NH;
-        static const int lgv = [] {  // RSVD_GSPLIT_LG (LP = 128): 0 one-step prefetch, 1 two loader groups, 2 four
-            const char* e = std::getenv("RSVD_GSPLIT_LG");
-            return e ? std::atoi(e) : 1;
-        }();
-        if constexpr (L == 128) {
-            if (lgv == 1) {
-                hipLaunchKernelGGL((gram_split_kernel<L, 1, 2>), dim3(grid), dim3(GS::THREADS), GS::NBUF * GS::STEP, s,
-                                   P, rows, gp.rows_per_chunk, gp.chunks, slabs);
-                return;
-            }
-            if (lgv == 2) {
-                hipLaunchKernelGGL((gram_split_kernel<L, 2, 4>), dim3(grid), dim3(GS::THREADS), GS::NBUF * GS::STEP, s,
-                                   P, rows, gp.rows_per_chunk, gp.chunks, slabs);
-                return;
-            }
+        if constexpr (L == 128) {  // two loader groups taking the steps in turn (round 4, 220 -> 180 us at C3)
+            hipLaunchKernelGGL((gram_split_kernel<L, 1, 2>), dim3(grid), dim3(GS::THREADS), GS::NBUF * GS::STEP, s, P,
+                               rows, gp.rows_per_chunk, gp.chunks, slabs);
+            return;
         }
         hipLaunchKernelGGL(gram_split_kernel<L>, dim3(grid), dim3(GS::THREADS), GS::NBUF * GS::STEP, s, P, rows,
                            gp.rows_per_chunk, gp.chunks, slabs);
     };
-    static const int v4 = [] {  // RSVD_GSPLIT4=0: the all-columns LP = 512 kernel (A/B runs)
-        const char* e = std::getenv("RSVD_GSPLIT4");
-        return e ? std::atoi(e) : 1;
-    }();
     if (LP == 128) go(std::integral_constant<int, 128>{});
     else if (LP == 256) go(std::integral_constant<int, 256>{});
     int nchunk = gp.chunks;
-    if (LP == 512 && v4) {
+    if (LP == 512) {
         // one round of 5-workgroup chunks on the 256 CUs (51 x 5 = 255), >= 512 rows each, within the
         // plan's slab count (the fp32 accumulators then run over up to ~2600 rows, as C3's 4096 do)
         int64_t ch = (rows + 511) / 512;
@@ -2563,8 +2500,6 @@ hipError_t launch_gram_split(const float* P, int64_t rows, int LP, const GramPla
         nchunk = (int)((rows + rpc - 1) / rpc);
         hipLaunchKernelGGL(gram_split4_kernel, dim3((nchunk + 7) / 8 * 8 * GramSplit4::TYPES),
                            dim3(GramSplit4::THREADS), GramSplit4::LDS, s, P, rows, rpc, nchunk, slabs);
-    } else if (LP == 512) {
-        go(std::integral_constant<int, 512>{});
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
@@ -2666,24 +2601,44 @@ constexpr int kGemmSqWaves = 4;
 // zrow (nullable): output rows i with zrow[i] != 0 are written as zeros (R12's broken-down rows).
 // Cin (nullable): the beta term's C when it is not the output (ld ldcin); d0out (nullable): the
 // diagonal-tile workgroups also write d0out[i] = d0in ? d0in[i] : Cin[i][i] (a level's pivot reference)
-__global__ __launch_bounds__(64 * kGemmSqWaves) void gemmsq_f64_kernel(int N, int ta, double alpha,
-                                                                       const double* __restrict__ A, int lda,
-                                                                       const double* __restrict__ B, int ldb,
-                                                                       double beta, double* __restrict__ C, int ldc,
-                                                                       const int* __restrict__ zrow,
-                                                                       const double* __restrict__ Cin, int ldcin,
-                                                                       double* __restrict__ d0out,
-                                                                       const double* __restrict__ d0in, Chol2Asm aj) {
+struct GemmSqJob {
+    int N = 0, ta = 0;  // N = 0: no job
+    double alpha = 1.0;
+    const double* A = nullptr;
+    int lda = 0;
+    const double* B = nullptr;
+    int ldb = 0;
+    double beta = 0.0;
+    double* C = nullptr;
+    int ldc = 0;
+    const int* zrow = nullptr;
+    const double* Cin = nullptr;
+    int ldcin = 0;
+    double* d0out = nullptr;
+    const double* d0in = nullptr;
+};
+// One launch runs up to two independent products (j1.N = 0: one) and, on extra workgroups, a
+// two-level factor's assembly job (round 6: the two-level factor's T = Ri11 R12 rides the S product's
+// launch -- one dependent launch fewer per two-level block).
+__global__ __launch_bounds__(64 * kGemmSqWaves) void gemmsq_f64_kernel(GemmSqJob j0, GemmSqJob j1, Chol2Asm aj) {
     __shared__ double part[kGemmSqWaves - 1][4][64];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 15, h = lane >> 4;
-    const int nt = N / 16;
-    if (aj.B && (int)blockIdx.x >= nt * nt) {  // an assembly workgroup (the Rinv12 product's launch)
-        const int e = ((int)blockIdx.x - nt * nt) * 64 * kGemmSqWaves + (int)threadIdx.x;
-        if (e < 2 * aj.B * aj.B) chol2_assemble_elem(aj, e / aj.B, e % aj.B);
+    const int nb0 = (j0.N / 16) * (j0.N / 16), nb1 = (j1.N / 16) * (j1.N / 16);
+    int b = (int)blockIdx.x;
+    if (b >= nb0 + nb1) {  // an assembly workgroup (the Rinv12 product's launch)
+        const int e = (b - nb0 - nb1) * 64 * kGemmSqWaves + (int)threadIdx.x;
+        if (aj.B && e < 2 * aj.B * aj.B) chol2_assemble_elem(aj, e / aj.B, e % aj.B);
         return;
     }
-    const int i0 = 16 * (blockIdx.x / nt), j0 = 16 * (blockIdx.x % nt);
+    const bool second = b >= nb0;
+    const GemmSqJob& J = second ? j1 : j0;
+    if (second) b -= nb0;
+    const int N = J.N, nt = N / 16;
+    const int i0 = 16 * (b / nt), j0c = 16 * (b % nt);
     const int kq = N / kGemmSqWaves;  // N % 64 == 0
+    const double* __restrict__ A = J.A;
+    const double* __restrict__ B = J.B;
+    const int lda = J.lda, ldb = J.ldb, ta = J.ta;
     f64x4 acc[4] = {MD::zero(), MD::zero(), MD::zero(), MD::zero()};
 #pragma unroll 2
     for (int k0 = w * kq; k0 < (w + 1) * kq; k0 += 16) {
@@ -2691,7 +2646,7 @@ __global__ __launch_bounds__(64 * kGemmSqWaves) void gemmsq_f64_kernel(int N, in
         for (int u = 0; u < 4; ++u) {
             const int k = k0 + 4 * u + h;
             const double a = ta ? A[(int64_t)k * lda + i0 + r] : A[(int64_t)(i0 + r) * lda + k];
-            acc[u] = MD::mma(a, B[(int64_t)k * ldb + j0 + r], acc[u]);
+            acc[u] = MD::mma(a, B[(int64_t)k * ldb + j0c + r], acc[u]);
         }
     }
     double v[4];
@@ -2703,38 +2658,53 @@ __global__ __launch_bounds__(64 * kGemmSqWaves) void gemmsq_f64_kernel(int N, in
     }
     __syncthreads();
     if (w != 0) return;
+    const int ldc = J.ldc;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {  // f64 D: col = r, row = h + 4 j
 #pragma unroll
         for (int q = 0; q < kGemmSqWaves - 1; ++q) v[j] += part[q][j][lane];
-        const int ii = i0 + MD::row(h, j), jj = j0 + r;
-        double* c = C + (int64_t)ii * ldc + jj;
-        const double o = alpha * v[j];
-        const double cin = beta == 0.0 ? 0.0 : (Cin ? Cin[(int64_t)ii * ldcin + jj] : *c);
-        const double out = (zrow && zrow[ii]) ? 0.0 : (beta == 0.0 ? o : o + beta * cin);
+        const int ii = i0 + MD::row(h, j), jj = j0c + r;
+        double* c = J.C + (int64_t)ii * ldc + jj;
+        const double o = J.alpha * v[j];
+        const double cin = J.beta == 0.0 ? 0.0 : (J.Cin ? J.Cin[(int64_t)ii * J.ldcin + jj] : *c);
+        const double out = (J.zrow && J.zrow[ii]) ? 0.0 : (J.beta == 0.0 ? o : o + J.beta * cin);
         *c = out;
-        if (d0out && ii == jj) d0out[ii] = d0in ? d0in[ii] : Cin[(int64_t)ii * ldcin + ii];
-        if (aj.B) {  // (the Rinv12 product: C = Rinv + B, ldc = 2 B) its fp32 copy and pieces
+        if (J.d0out && ii == jj) J.d0out[ii] = J.d0in ? J.d0in[ii] : J.Cin[(int64_t)ii * J.ldcin + ii];
+        if (!second && aj.B) {  // (the Rinv12 product: C = Rinv + B, ldc = 2 B) its fp32 copy and pieces
             if (aj.Rinv32) aj.Rinv32[(int64_t)ii * ldc + aj.B + jj] = (float)out;
             if (aj.Mt) store_pieces(aj.Mt, (int64_t)4 * aj.B * aj.B, (int64_t)(aj.B + jj) * 2 * aj.B + ii, (float)out);
         }
     }
 }
 
-static hipError_t gemm_sq(int N, int ta, double alpha, const double* A, int lda, const double* B, int ldb, double beta,
-                          double* C, int ldc, hipStream_t s, const int* zrow = nullptr, const double* Cin = nullptr,
-                          int ldcin = 0, double* d0out = nullptr, const double* d0in = nullptr,
-                          const Chol2Asm* aj = nullptr) {
-    if (N % (16 * kGemmSqWaves)) return hipErrorInvalidValue;
+static GemmSqJob sq_job(int N, int ta, double alpha, const double* A, int lda, const double* B, int ldb, double beta,
+                        double* C, int ldc, const int* zrow = nullptr, const double* Cin = nullptr, int ldcin = 0,
+                        double* d0out = nullptr, const double* d0in = nullptr) {
+    GemmSqJob j;
+    j.N = N, j.ta = ta, j.alpha = alpha, j.A = A, j.lda = lda, j.B = B, j.ldb = ldb, j.beta = beta, j.C = C, j.ldc = ldc;
+    j.zrow = zrow, j.Cin = Cin, j.ldcin = ldcin, j.d0out = d0out, j.d0in = d0in;
+    return j;
+}
+
+static hipError_t gemm_sq2(const GemmSqJob& j0, const GemmSqJob& j1, hipStream_t s, const Chol2Asm* aj = nullptr) {
+    if (j0.N % (16 * kGemmSqWaves) || j1.N % (16 * kGemmSqWaves)) return hipErrorInvalidValue;
     Chol2Asm job{};
     int extra = 0;
     if (aj) {
         job = *aj;
         extra = (2 * job.B * job.B + 64 * kGemmSqWaves - 1) / (64 * kGemmSqWaves);
     }
-    hipLaunchKernelGGL(gemmsq_f64_kernel, dim3((N / 16) * (N / 16) + extra), dim3(64 * kGemmSqWaves), 0, s, N, ta, alpha,
-                       A, lda, B, ldb, beta, C, ldc, zrow, Cin, ldcin, d0out, d0in, job);
+    const int nb = (j0.N / 16) * (j0.N / 16) + (j1.N / 16) * (j1.N / 16) + extra;
+    hipLaunchKernelGGL(gemmsq_f64_kernel, dim3(nb), dim3(64 * kGemmSqWaves), 0, s, j0, j1, job);
     return hipGetLastError();
+}
+
+static hipError_t gemm_sq(int N, int ta, double alpha, const double* A, int lda, const double* B, int ldb, double beta,
+                          double* C, int ldc, hipStream_t s, const int* zrow = nullptr, const double* Cin = nullptr,
+                          int ldcin = 0, double* d0out = nullptr, const double* d0in = nullptr,
+                          const Chol2Asm* aj = nullptr) {
+    return gemm_sq2(sq_job(N, ta, alpha, A, lda, B, ldb, beta, C, ldc, zrow, Cin, ldcin, d0out, d0in), GemmSqJob{}, s,
+                    aj);
 }
 
 size_t chol_2level_scratch_doubles(int LP, int depth) {
@@ -2775,33 +2745,24 @@ hipError_t launch_chol_wide_2level(const double* G, int l, int LP, double tol, d
     // the one-level factor's strips are (written so by the product's epilogue)
     if ((e = gemm_sq(B, 1, 1.0, Ri11, B, G + B, ldg, 0.0, R + B, LP, s, colflag)) != hipSuccess) return e;
     // S = G22 - R12^T R12 into Sb (the beta term read from G22 in place), and d0b = diag(G22) (or the
-    // caller's d0src[B ..]) from the diagonal tiles
-    if ((e = gemm_sq(B, 1, -1.0, R + B, LP, R + B, LP, 1.0, Sb, B, s, nullptr, G + (int64_t)B * ldg + B, ldg, d0b,
-                     d0src ? d0src + B : nullptr)) != hipSuccess)
+    // caller's d0src[B ..]) from the diagonal tiles; in the same launch T = Ri11 R12 (independent of S)
+    if ((e = gemm_sq2(sq_job(B, 1, -1.0, R + B, LP, R + B, LP, 1.0, Sb, B, nullptr, G + (int64_t)B * ldg + B, ldg, d0b,
+                             d0src ? d0src + B : nullptr),
+                      sq_job(B, 0, 1.0, Ri11, B, R + B, LP, 0.0, T, B), s)) != hipSuccess)
         return e;
     // level 2 on the l - B valid columns of S, tested against diag(G22) (or the caller's d0src)
     e = chol_level(Sb, B, l - B, B, tol, R22, Ri22, colflag + B, flag, work, inner, s, ill_tol, ill ? ill2 : nullptr,
                    d0b, sub);
     if (e != hipSuccess) return e;
-    // Rinv12 = -Ri11 (R12 Ri22) -> Rinv[:B, B:]
-    if ((e = gemm_sq(B, 0, 1.0, R + B, LP, Ri22, B, 0.0, T, B, s)) != hipSuccess) return e;
-    // ... with the blocks' assembly into R / Rinv (+ Rinv32, pieces, ill) on extra workgroups
+    // Rinv12 = -(Ri11 R12) Ri22 -> Rinv[:B, B:], with the blocks' assembly into R / Rinv (+ Rinv32,
+    // pieces, ill) on extra workgroups
     const Chol2Asm job{R11, Ri11, R22, Ri22, B, R, Rinv, Rinv32, ill2, ill, Mt};
-    return gemm_sq(B, 0, -1.0, Ri11, B, T, B, 0.0, Rinv + B, LP, s, nullptr, nullptr, 0, nullptr, nullptr, &job);
+    return gemm_sq(B, 0, -1.0, T, B, Ri22, B, 0.0, Rinv + B, LP, s, nullptr, nullptr, 0, nullptr, nullptr, &job);
 }
 
 
-// panel_split_kernel shape: 0 = 2 row tiles x 128 columns (default), 1 = 4 x 128, 2 = 4 x 64
-// (RSVD_PANEL_SPLIT_SHAPE, for A/B runs; 4 x 128 runs at one wave per SIMD and loses the gain of
-// its halved LDS reads, 4 x 64 ties with 2 x 128 in the bench)
-static int panel_split_variant() {
-    static const int v = [] {
-        const char* e = std::getenv("RSVD_PANEL_SPLIT_SHAPE");
-        return e ? std::atoi(e) : 0;
-    }();
-    return v;
-}
-
+// panel_split_kernel shape: 2 row tiles x 128 columns (4 x 128 runs at one wave per SIMD and loses
+// the gain of its halved LDS reads, 4 x 64 ties with 2 x 128 in the bench: round 3)
 template <typename T>
 hipError_t launch_panel_gemm(const T* In, int64_t rows, int LP, const T* Mm, int upper, T* Out, int64_t ldo,
                              int cols, bf16_t* hi, bf16_t* lo, const int* pred, hipStream_t s, bf16_t* msplit,
@@ -2823,9 +2784,6 @@ hipError_t launch_panel_gemm(const T* In, int64_t rows, int LP, const T* Mm, int
                            upper, reinterpret_cast<float*>(Out), ldo, cols, hi, lo, ncb, pred);                \
         return hipGetLastError();                                                                              \
     }
-            const int v = panel_split_variant();
-            if (v == 1) PSPLIT(4, 128, 2)
-            if (v == 2) PSPLIT(4, 64, 2)
             // In prefetch ring depth (RSVD_PANEL_PD overrides): 4 at LP = 512 (16 k-steps: C5 18.38 ->
             // 18.19 ms, gpurun_out r6k), 2 (one step ahead) below, where 3 / 4 measured no gain
             static const int pd_env = [] {

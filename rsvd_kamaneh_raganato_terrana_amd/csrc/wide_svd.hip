@@ -973,19 +973,13 @@ __global__ __launch_bounds__(1024) void block_jacobi_complete_kernel(const T* __
 
 // inner sweep form: bit 0 = the first four waves only (inner_sweep4), bit 1 = pair_angle_fast,
 // bit 2 (with bit 0) = Jp rotated by waves 4..7 one round behind (inner_sweep4j).
-// Same box A/B (RSVD_BJ_INNER=0/1/2/3): C5 29.77 / 29.25 / 29.48 / 29.14 ms, C3 7.15 / 6.99 / 7.04 /
+// Same box A/B (round 3, variants 0/1/2/3): C5 29.77 / 29.25 / 29.48 / 29.14 ms, C3 7.15 / 6.99 / 7.04 /
 // 6.99 ms, C4 28.02 / 28.05 / 28.06 / 27.92 ms (8 sweeps in every case); another box, 3 / 5 / 7:
 // C5 28.91 / 28.51 / 28.34, C4 27.67 / 27.35 / 27.27, C3 6.96 / 6.92 / 6.88.  Default: 7 for the
 // fp32-result tolerance; the fp64-result runs (tol_chk <= 1e-9: the standalone fp64 SVD, fp64 A)
 // keep 0, whose V is orthogonal to the 1e-12 the fp64 SVD tests hold (3 gave 1.6e-12 on a
 // 1200 x 900 SVD).
-static int bj_inner_variant(double tol_chk) {
-    static const int v = [] {
-        const char* e = std::getenv("RSVD_BJ_INNER");
-        return e ? std::atoi(e) : -1;
-    }();
-    return v >= 0 ? v : (tol_chk > 1e-9 ? 7 : 0);
-}
+static int bj_inner_variant(double tol_chk) { return tol_chk > 1e-9 ? 7 : 0; }
 
 int block_jacobi_groups(int MR, int LP, int G) {
     // scratch (U_w, MR x LP doubles) must hold nwg + 1024 nwg doubles; members split MR and LP rows
