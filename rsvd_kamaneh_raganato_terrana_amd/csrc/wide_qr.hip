@@ -2516,12 +2516,10 @@ hipError_t launch_chol_wide(const double* G, int l, int LP, double tol, double* 
     // LP = 256: chol_wide_kernel (its wave-0 look-ahead overlaps the diagonal factor with the other waves'
     // updates; the register-resident kernel spills there, 174 vs 161 us measured); LP <= 128: chol_reg_kernel
     // (LP = 128: 63 vs 71 us, LP = 64: 31 vs 37 us, tools/wide_lab chol)
-    // RSVD_CHOL_RINV_FUSED=0: R^-1 on its own rinv_wide launch after the register-resident factor too
-    static const int fused_env = [] {
-        const char* e = std::getenv("RSVD_CHOL_RINV_FUSED");
-        return e ? std::atoi(e) : 1;
-    }();
-    const int fuse = (fused_env && chol_variant >= 1 && (LP == 128 || LP == 64)) ? 1 : 0;
+    // R^-1 by the triangular inverse in the same launch after the register-resident factor (round 6 tried
+    // eliminating [G | I] in the factor's own sweep instead: 256 VGPRs + 112 B/lane scratch at NP = 8,
+    // +6 us per launch measured; DESIGN.md §9c dead end 17)
+    const int fuse = (chol_variant >= 1 && (LP == 128 || LP == 64)) ? 1 : 0;
     if (chol_variant >= 1 && LP == 128)
         hipLaunchKernelGGL(chol_reg_kernel<8>, dim3(1), dim3(64 * kCholRegWaves),
                            std::max(CholReg<8>::lds_bytes, fuse ? CholRegInv<8>::lds_bytes : 0), s, G, l, tol, R, Rinv,

@@ -10,7 +10,7 @@ for c in $cfgs; do
   for knobs in "$@"; do
     out=$R/gpurun_out/trace_${tag}_${c}_$i
     mkdir -p $out
-    (cd /tmp && env $knobs timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $out -o run -- python3 $R/bench.py --cpu-budget 0 --config $c --steps 3 --warmup 1 > $out.log 2>&1) || { tail -5 $out.log; exit 1; }
+    (cd /tmp && env $knobs timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $out -o run -- python3 $R/bench.py --cpu-budget 0 --config $c --steps 3 --warmup 1 ${BENCH_EXTRA:-} > $out.log 2>&1) || { tail -5 $out.log; exit 1; }
     echo "$c $i: $knobs" >> $R/gpurun_out/trace_${tag}.idx
     i=$((i+1))
   done
