@@ -68,6 +68,8 @@ constexpr int kFlagGramTimeout = 2, kFlagJacobiTimeout = 3, kFlagUnrepaired = 20
               kFlagFewRows = 22;
 // the split-Gram fallback test (wide.cpp cholqr_pass) and its factor's breakdown count (never read)
 constexpr int kFlagSplitIll = 24, kFlagSplitScratch = 25;
+// the deferred second pass's G^-1/2 series (wide.cpp orth2_deferred): [0] series applies, [1] the Cholesky runs
+constexpr int kFlagIsqrt = 26;
 
 // Per-run reset of the non-sticky flag words ([0..1] and [4..19]; the sticky words stay).
 inline hipError_t reset_run_flags(int* dflags, hipStream_t s) {

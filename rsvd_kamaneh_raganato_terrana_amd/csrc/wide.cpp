@@ -227,7 +227,11 @@ struct WideEngine {
     // -0.28 ms on one box).  Measured and dropped: the pass-2 Gram + factor on a side stream beside the
     // next projection -- the projections run one workgroup per CU in a single wave of workgroups, so
     // a CU the side stream holds delays the whole projection by about as long (C4 +0.03, C5 +0.08 ms).
-    bool defer = false;
+    // R2^-1 need not be triangular: any M with (T1 M)^T (T1 M) = I will do, and G = T1^T T1 = I + E is
+    // near the identity, so M = G^-1/2 by its series (wide_eig.hip launch_isqrt_near_identity: four
+    // l^3 MFMA products instead of the factor's pivot chain; the Cholesky factor, predicated, when
+    // |E|_F > 0.1).  RSVD_ISQRT=0: the Cholesky factor always (A/B).
+    bool defer = false, isqrt = true;
     double *R2s = nullptr, *R2m = nullptr, *R2n = nullptr, *Mu = nullptr, *Mv = nullptr, *Tmp = nullptr;
 
     // world > 1: G[LP^2] holds this rank's row count until the first m-side Gram all-reduce sums it
@@ -341,6 +345,14 @@ struct WideEngine {
         if constexpr (sizeof(T) == 8) return m64; else return m32;
     }
 
+    // The split Gram runs on unpredicated passes of one rank (RSVD_GRAM_SPLIT_SHARDED=1: of every rank).
+    // Priced at world 8 from the per-rank kernels (bench.py --emulate-world 8, round 6): C5 -0.40 ms,
+    // C4 -0.05 ms of kernel time per rSVD, but its predicated fallback Gram has to be summed whether or
+    // not it runs -- eight more LP^2 all-reduces per rSVD, ~+0.42 / +0.34 ms at the model's RCCL cost
+    // (tools/model8.py) -- so sharded passes keep the fp64 Gram.
+    bool split_sharded = false;
+    bool split_path(bool sharded, const int* pred) const { return split_gram && !pred && (!sharded || split_sharded); }
+
     // R = chol(P^T P) and R^-1 (Ro, Rio; with the fp32 copy and bf16 pieces of R^-1 when r32 / mt).
     int gram_factor(const T* P, int64_t rows, const GramPlan& gp, bool sharded, int* flag, const int* pred, double* Ro,
                     double* Rio, float* r32, bf16_t* mt) {
@@ -354,24 +366,33 @@ struct WideEngine {
             return launch_chol_wide(G, L.l, L.LP, tol(), Ro, Rio, r32, colflag, fl, W, nullptr, s, ill_tol, ill,
                                     nullptr, mt);
         };
-        if (split_gram && !sharded && !pred) {
-            int* ill = h->dflags + kFlagSplitIll;
-            RSVD_CK(launch_gram_split(reinterpret_cast<const float*>(P), rows, L.LP, gp, gslab, G, s));
-            RSVD_CK(factor(h->dflags + kFlagSplitScratch, kSplitIllTol, ill));
-            RSVD_CK(launch_gram_wide<T>(P, nullptr, rows, L.LP, gp, gslab, G, ill, s));
-            RSVD_CK(launch_chol_wide(G, L.l, L.LP, tol(), Ro, Rio, r32, colflag, flag, W, ill, s, 0.0, nullptr, nullptr,
-                                     mt));
-            return RSVD_OK;
-        }
-        RSVD_CK(launch_gram_wide<T>(P, nullptr, rows, L.LP, gp, gslab, G, pred, s));
-        if (sharded) {
+        // sharded: the rank's Gram summed over the ranks (the first m-side sum carries the global row count)
+        auto sum_ranks = [&]() -> int {
+            if (!sharded) return RSVD_OK;
             const bool cnt = count_pending && rows == L.m && !pred;
             RSVD_TRY(allreduce(G, (int64_t)L.LP * L.LP + (cnt ? 1 : 0), RSVD_F64));
             if (cnt) {
                 count_pending = false;
                 RSVD_CK(launch_check_rows(G + (size_t)L.LP * L.LP, L.l, h->dflags + kFlagFewRows, s));
             }
+            return RSVD_OK;
+        };
+        if (split_path(sharded, pred)) {
+            int* ill = h->dflags + kFlagSplitIll;
+            RSVD_CK(launch_gram_split(reinterpret_cast<const float*>(P), rows, L.LP, gp, gslab, G, s));
+            RSVD_TRY(sum_ranks());
+            RSVD_CK(factor(h->dflags + kFlagSplitScratch, kSplitIllTol, ill));
+            RSVD_CK(launch_gram_wide<T>(P, nullptr, rows, L.LP, gp, gslab, G, ill, s));
+            // sharded: the fallback Gram's sum is issued whether or not `ill` is raised (a device word the
+            // host does not read; every rank factors the same summed G, so the ranks' words agree).  When
+            // it is clear, G is dead and so is this sum.
+            RSVD_TRY(sum_ranks());
+            RSVD_CK(launch_chol_wide(G, L.l, L.LP, tol(), Ro, Rio, r32, colflag, flag, W, ill, s, 0.0, nullptr, nullptr,
+                                     mt));
+            return RSVD_OK;
         }
+        RSVD_CK(launch_gram_wide<T>(P, nullptr, rows, L.LP, gp, gslab, G, pred, s));
+        RSVD_TRY(sum_ranks());
         if (pred)
             RSVD_CK(launch_chol_wide(G, L.l, L.LP, tol(), Ro, Rio, r32, colflag, flag, W, pred, s, 0.0, nullptr, nullptr,
                                      mt));
@@ -381,7 +402,7 @@ struct WideEngine {
     }
 
     // One CholeskyQR pass Out = P chol(P^T P)^-1 (+ bf16 hi/lo of Out).  `pred`: predicated pass.
-    // fp32 panels of bf16 / e4m3 A (one rank, unpredicated passes): the Gram by the three-piece bf16
+    // fp32 panels of bf16 / e4m3 A (unpredicated passes, any world size): the Gram by the three-piece bf16
     // split (wide_qr.hip gram_split_kernel, |dG| ~ 1e-8 |G|); when a pivot of its factor falls below
     // kSplitIllTol of its diagonal (cond(P) beyond ~1e3, or a breakdown) the fp64 Gram and factor
     // run again, predicated on that test (h->dflags[kFlagSplitIll]), and their R / R^-1 / flags stand.
@@ -392,8 +413,8 @@ struct WideEngine {
         // split_mat launch per pass; bit-identical)
         bf16_t* mt = (ms() && L.LP >= 128) ? ms() : nullptr;
         RSVD_TRY(gram_factor(P, rows, gp, sharded, flag, pred, R, Rinv, r32, mt));
-        const bool split_path = split_gram && !sharded && !pred;
-        RSVD_CK(launch_panel_gemm<T>(P, rows, L.LP, mat(Rinv, Rinv32), 1, Out, 0, 0, hi, lo, split_path ? nullptr : pred,
+        const bool split_p = split_path(sharded, pred);
+        RSVD_CK(launch_panel_gemm<T>(P, rows, L.LP, mat(Rinv, Rinv32), 1, Out, 0, 0, hi, lo, split_p ? nullptr : pred,
                                      s, ms(), mt != nullptr));
         return RSVD_OK;
     }
@@ -432,7 +453,21 @@ struct WideEngine {
         RSVD_TRY(repair(T1out, rows, gp, sharded, hi, lo, flag, mside, nshard));
         // pass 2's factor: T1 is orthonormal to ~eps_G cond^2 (or repaired), so a breakdown here means the
         // panel could not be orthonormalised -- reported through the sticky kFlagUnrepaired
-        return gram_factor(T1out, rows, gp, sharded, h->dflags + kFlagUnrepaired, nullptr, R2s, r2inv, nullptr, nullptr);
+        if (!isqrt)
+            return gram_factor(T1out, rows, gp, sharded, h->dflags + kFlagUnrepaired, nullptr, R2s, r2inv, nullptr,
+                               nullptr);
+        // G = T1^T T1 (split Gram: its ~3e-8 entry error is what the factor of that Gram carried too)
+        if (split_gram) RSVD_CK(launch_gram_split(reinterpret_cast<const float*>(T1out), rows, L.LP, gp, gslab, G, s));
+        else RSVD_CK(launch_gram_wide<T>(T1out, nullptr, rows, L.LP, gp, gslab, G, nullptr, s));
+        if (sharded) RSVD_TRY(allreduce(G, (int64_t)L.LP * L.LP, RSVD_F64));
+        int* fl = h->dflags + kFlagIsqrt;
+        // E = G - I and the cut-off test; past it the Cholesky factor (predicated), then G is scratch
+        RSVD_CK(launch_isqrt_near_identity(G, L.l, L.LP, Mu, nullptr, nullptr, nullptr, nullptr, nullptr, fl, s, true,
+                                           false));
+        RSVD_CK(launch_chol_wide(G, L.l, L.LP, tol(), R2s, r2inv, nullptr, colflag, h->dflags + kFlagUnrepaired, W,
+                                 fl + 1, s, 0.0, nullptr, nullptr, nullptr));
+        RSVD_CK(launch_isqrt_near_identity(nullptr, L.l, L.LP, Mu, Mv, Tmp, R2s, G, r2inv, fl, s, false, true));
+        return RSVD_OK;
     }
 
     // Q = orth(P): CholeskyQR (passes = 1) or CholeskyQR2; output panels (repair = true) get the
@@ -659,6 +694,11 @@ int wide_typed(rsvd_handle_t h, const rsvd_desc_t* d, const void* A, const void*
         }();
         E.split_gram = env != 0 && sizeof(T) == 4 && L.lowp && gram_split_ok(L.LP);
         E.split_panel = sizeof(T) == 4 && L.lowp && L.LP % 32 == 0 && L.LP >= 128;
+        static const int env6 = [] {
+            const char* v = std::getenv("RSVD_GRAM_SPLIT_SHARDED");
+            return v ? std::atoi(v) : 0;
+        }();
+        E.split_sharded = env6 != 0;
         static const bool env5 = [] {
             const char* v = std::getenv("RSVD_SMALL_SVD");
             return !(v && std::string(v) == "jacobi");
@@ -675,6 +715,11 @@ int wide_typed(rsvd_handle_t h, const rsvd_desc_t* d, const void* A, const void*
         }();
         E.defer = env != 0 && sizeof(T) == 4 && !Qout && d->method != RSVD_SVD_POWER &&
                   d->method != RSVD_SVD_POWER_IC && d->qr_mode == RSVD_QR_AUTO;
+        static const int env2 = [] {
+            const char* v = std::getenv("RSVD_ISQRT");
+            return v ? std::atoi(v) : 1;
+        }();
+        E.isqrt = env2 != 0;
     }
     E.seed = d->seed;
     E.nsh = L.nsh;

@@ -189,6 +189,11 @@ size_t eig_svd_ws_doubles(int LP);
 // Z = op(X) op(Y) for n x n fp64 row-major matrices on the fp64 MFMA (tx / ty: transpose X / Y)
 hipError_t launch_gemm_rm(int tx, int ty, int n, const double* X, int ldx, const double* Y, int ldy, double* Z, int ldz,
                           hipStream_t s);
+// M = G^-1/2 for a Gram near the identity (|G - I|_F <= 0.1: flags[0] = 1, M into `out`; else flags[1] = 1
+// and `out` is left alone).  prep_only: E = G - I and the flags; series_only: the rest (G no longer read).
+hipError_t launch_isqrt_near_identity(const double* G, int l, int LP, double* E, double* E2, double* E3, double* B,
+                                      double* T, double* out, int* flags, hipStream_t s, bool prep_only,
+                                      bool series_only);
 template <typename T>
 hipError_t launch_eig_svd(const double* R, int l, int LP, double* ews, double* X, double* J, double* Uw, double* Vw,
                           T* S, unsigned* sync, int* info, hipStream_t s, double tol_chk);

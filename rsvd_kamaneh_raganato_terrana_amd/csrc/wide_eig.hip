@@ -1111,19 +1111,29 @@ __global__ __launch_bounds__(256) void sqgemm_f64_kernel(int M, int N, int K, do
         return TB ? B[(int64_t)k * ldb + j] : B[(int64_t)j * ldb + k];
     };
     f64x4 acc0 = MD::zero(), acc1 = MD::zero();
-    for (int k0 = 32 * w; k0 < K; k0 += 128) {
-        double a[8], b[8];
+    // (round 6: the loads of up to four of the wave's chunks -- K = 512 whole -- are issued before
+    // their MFMAs, one L2 round trip instead of four; the same products in the same order)
+    for (int kb = 32 * w; kb < K; kb += 512) {
+        double a[4][8], b[4][8];
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            a[s] = ld_a(k0 + 4 * h + s);
-            b[s] = ld_b(k0 + 4 * h + s);
-            a[4 + s] = ld_a(k0 + 16 + 4 * h + s);
-            b[4 + s] = ld_b(k0 + 16 + 4 * h + s);
+        for (int it = 0; it < 4; ++it) {
+            const int k0 = kb + 128 * it;
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                a[it][s] = ld_a(k0 + 4 * h + s);
+                b[it][s] = ld_b(k0 + 4 * h + s);
+                a[it][4 + s] = ld_a(k0 + 16 + 4 * h + s);
+                b[it][4 + s] = ld_b(k0 + 16 + 4 * h + s);
+            }
         }
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            acc0 = MD::mma(a[s], b[s], acc0);
-            acc1 = MD::mma(a[4 + s], b[4 + s], acc1);
+        for (int it = 0; it < 4; ++it) {
+            if (kb + 128 * it >= K) break;
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                acc0 = MD::mma(a[it][s], b[it][s], acc0);
+                acc1 = MD::mma(a[it][4 + s], b[it][4 + s], acc1);
+            }
         }
     }
     f64x4 t;
@@ -1199,6 +1209,87 @@ void tri_prof_read(long long* out) {
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_tri_prof), z, sizeof(z));
 }
 #endif
+
+// ---- G^-1/2 of a Gram near the identity (round 6; the deferred second CholeskyQR pass, wide.cpp) ----
+// The second pass's Gram G = T1^T T1 of an already orthonormalised panel is I + E with |E|_F <~ 0.03
+// (the split Gram's entry error times cond(P)^2, bounded by its fallback test).  Any M with
+// (T1 M)^T (T1 M) = I serves the deferred algebra (it only needs span(T1 M) = span(T1)), and
+// M = G^-1/2 = sum_k binom(-1/2, k) E^k converges fast there: to degree 8 the remainder is below
+// 0.19 |E|^9 (2e-10 at |E|_F = 0.1, the cut-off).  Paterson-Stockmeyer on E, E^2, E^3:
+//     M = B0 + E^3 (B1 + E^3 B2),   B_i = c_{3i} I + c_{3i+1} E + c_{3i+2} E^2
+// -- four l^3 products on the MFMA and three element-wise passes, against the Cholesky factor's
+// dependent pivot chain (C5: ~285 us per LP = 512 factor).  Past the cut-off (or a non-finite E)
+// flags[1] is raised and the caller's predicated Cholesky factor runs instead.
+constexpr double kIsqrtCut = 0.1;
+constexpr double kIsqrtC[9] = {1.0,          -0.5,         0.375,         -0.3125,           0.2734375,
+                               -0.24609375, 0.2255859375, -0.20947265625, 0.196380615234375};
+
+// E = G - I on the l x l block, 0 outside; flags[0] = |E|_F <= cut (finite), flags[1] = !flags[0]
+__global__ __launch_bounds__(1024) void isqrt_prep_kernel(const double* __restrict__ G, int l, int LP,
+                                                          double* __restrict__ E, int* __restrict__ flags) {
+    __shared__ double part[16];
+    const int tid = threadIdx.x;
+    double ss = 0.0;
+    for (int e = tid; e < LP * LP; e += 1024) {
+        const int i = e / LP, j = e - i * LP;
+        const double v = (i < l && j < l) ? G[e] - (i == j ? 1.0 : 0.0) : 0.0;
+        E[e] = v;
+        ss = fma(v, v, ss);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o);
+    if ((tid & 63) == 0) part[tid >> 6] = ss;
+    __syncthreads();
+    if (tid == 0) {
+        double t = 0.0;
+        for (int w = 0; w < 16; ++w) t += part[w];
+        const int small = (t <= kIsqrtCut * kIsqrtCut) ? 1 : 0;  // NaN: not small
+        flags[0] = small;
+        flags[1] = 1 - small;
+    }
+}
+
+// out = a I + b E + c E2 (+ X) on the l x l block; outside it the identity (`pad_id`) or 0
+__global__ __launch_bounds__(256) void isqrt_poly_kernel(double* __restrict__ out, const double* __restrict__ E,
+                                                         const double* __restrict__ E2, const double* __restrict__ X,
+                                                         double a, double b, double c, int l, int LP, int pad_id,
+                                                         const int* __restrict__ pred) {
+    if (pred && *pred == 0) return;
+    const int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (e >= (int64_t)LP * LP) return;
+    const int i = (int)(e / LP), j = (int)(e - (int64_t)i * LP);
+    double v;
+    if (i < l && j < l) {
+        v = fma(c, E2[e], fma(b, E[e], i == j ? a : 0.0));
+        if (X) v += X[e];
+    } else {
+        v = (pad_id && i == j) ? 1.0 : 0.0;
+    }
+    out[e] = v;
+}
+
+// M = G^-1/2 into `out` (pred flags[0]); scratch: E, E2, E3, B, T (LP x LP each, T may be G itself once
+// the caller's predicated fallback has read it).  The l x l products run on the sqgemm (column-major:
+// every operand is a polynomial in the symmetric E, so the layout does not matter).
+hipError_t launch_isqrt_near_identity(const double* G, int l, int LP, double* E, double* E2, double* E3, double* B,
+                                      double* T, double* out, int* flags, hipStream_t s, bool prep_only,
+                                      bool series_only) {
+    hipError_t er;
+    if (!series_only) {
+        hipLaunchKernelGGL(isqrt_prep_kernel, dim3(1), dim3(1024), 0, s, G, l, LP, E, flags);
+        if ((er = hipGetLastError()) != hipSuccess || prep_only) return er;
+    }
+    const double* c = kIsqrtC;
+    const dim3 grid((unsigned)(((int64_t)LP * LP + 255) / 256));
+    if ((er = launch_sqgemm(0, 0, l, l, l, 1.0, E, LP, E, LP, 0.0, E2, LP, s)) != hipSuccess) return er;
+    if ((er = launch_sqgemm(0, 0, l, l, l, 1.0, E2, LP, E, LP, 0.0, E3, LP, s)) != hipSuccess) return er;
+    hipLaunchKernelGGL(isqrt_poly_kernel, grid, dim3(256), 0, s, B, E, E2, nullptr, c[6], c[7], c[8], l, LP, 0, nullptr);
+    if ((er = launch_sqgemm(0, 0, l, l, l, 1.0, E3, LP, B, LP, 0.0, T, LP, s)) != hipSuccess) return er;
+    hipLaunchKernelGGL(isqrt_poly_kernel, grid, dim3(256), 0, s, B, E, E2, T, c[3], c[4], c[5], l, LP, 0, nullptr);
+    if ((er = launch_sqgemm(0, 0, l, l, l, 1.0, E3, LP, B, LP, 0.0, T, LP, s)) != hipSuccess) return er;
+    hipLaunchKernelGGL(isqrt_poly_kernel, grid, dim3(256), 0, s, out, E, E2, T, c[0], c[1], c[2], l, LP, 1, flags);
+    return hipGetLastError();
+}
 
 // Z = op(X) op(Y), n x n fp64 row-major (lds ldx / ldy / ldz): the column-major sqgemm on the
 // transposed views (Z^T = op(Y)^T op(X)^T)

@@ -2496,8 +2496,8 @@ hipError_t launch_gram_split(const float* P, int64_t rows, int LP, const GramPla
         if (ch > gp.chunks) ch = gp.chunks;
         if (ch < 1) ch = 1;
         int64_t rpc = (rows + ch - 1) / ch;
-        rpc = (rpc + 31) / 32 * 32;
-        nchunk = (int)((rows + rpc - 1) / rpc);
+        rpc = rpc < 32 ? 32 : (rpc + 31) / 32 * 32;  // (a rank's shard may hold no rows: one empty chunk)
+        nchunk = rows > 0 ? (int)((rows + rpc - 1) / rpc) : 1;
         hipLaunchKernelGGL(gram_split4_kernel, dim3((nchunk + 7) / 8 * 8 * GramSplit4::TYPES),
                            dim3(GramSplit4::THREADS), GramSplit4::LDS, s, P, rows, rpc, nchunk, slabs);
     }

@@ -203,6 +203,15 @@ def test_row_sharded_world8_matches_oracle(case):
     _check_world2(case, True, world=8)
 
 
+@pytest.mark.parametrize("case", [(8191, 4000, 256, 2, "bf16"), (8192, 2000, 512, 2, "e4m3")])
+def test_row_sharded_world8_split_gram_sharded(case, monkeypatch):
+    """RSVD_GRAM_SPLIT_SHARDED=1 (opt-in, round 6): the three-piece split Gram on sharded passes too --
+    the rank's split Gram all-reduced and factored, the predicated fp64 fallback Gram summed whether
+    or not it runs (DESIGN.md §5 prices it).  The world-8 cases above, against the oracle at 1e-4."""
+    monkeypatch.setenv("RSVD_GRAM_SPLIT_SHARDED", "1")  # read once per process: the spawned ranks see it
+    _check_world2(case, True, world=8)
+
+
 @pytest.mark.parametrize("case", [(1600, 1000, 768, 1, "f32"), (2001, 1200, 640, 1, "bf16")])
 def test_row_sharded_world2_l_past_512(case):
     """rSVD() past the wide engine's 512 sketch columns on two ranks: the

@@ -8,7 +8,7 @@ one-GPU box, so they carry stated assumptions: a reduce-scatter / all-gather of 
 (N-1)/N V over the ring at RING_GBS per GPU, an all-reduce of V bytes costs 2 (N-1)/N V at that rate, and
 every collective launch costs LAT_US.
 
-usage: python tools/model8.py <kernel_stats.csv> <config c4|c5> [N]
+usage: python tools/model8.py <kernel_stats.csv> <config c4|c5> [N] [extra all-reduces]
 """
 import csv
 import sys
@@ -30,6 +30,9 @@ CFG = {"c4": (65536, 65536, 256, 2, 2), "c5": (131072, 8192, 512, 2, 1)}  # m, n
 def main():
     path, cfg = sys.argv[1], sys.argv[2]
     N = int(sys.argv[3]) if len(sys.argv) > 3 else 8
+    # extra LP^2 all-reduces per rSVD: RSVD_GRAM_SPLIT_SHARDED=1 sums each split pass's predicated fp64
+    # fallback Gram whether or not it runs (8 per rSVD at q = 2)
+    extra = int(sys.argv[4]) if len(sys.argv) > 4 else 0
     m, n, l, q, _ = CFG[cfg]
     rows = list(csv.DictReader(open(path)))
     nr = max(int(r["Calls"]) for r in rows if "tridiag_bisect_kernel" in r["Name"] or "small_svd_kernel" in r["Name"])
@@ -48,7 +51,7 @@ def main():
     # q - 1 intermediates, the output panel's two passes) and its repair pass, n side the same, the cross
     # Gram R -- 2 q + 7; reduce-scatters of A^T Q (q + 1); all-gathers of the hi / lo X panels (q, two
     # each) and of V
-    ar_small = 2 * q + 7
+    ar_small = 2 * q + 7 + extra
     b_lp2 = LP * LP * 8
     rs = (q + 1) * N * nc * LP * 4
     ag = q * 2 * N * nc * LP * 2 + N * nc * LP * 4
