@@ -462,7 +462,7 @@ struct WideEngine {
         if (sharded) RSVD_TRY(allreduce(G, (int64_t)L.LP * L.LP, RSVD_F64));
         int* fl = h->dflags + kFlagIsqrt;
         // E = G - I and the cut-off test; past it the Cholesky factor (predicated), then G is scratch
-        RSVD_CK(launch_isqrt_near_identity(G, L.l, L.LP, Mu, nullptr, nullptr, nullptr, nullptr, nullptr, fl, s, true,
+        RSVD_CK(launch_isqrt_near_identity(G, L.l, L.LP, Mu, Mv, nullptr, nullptr, nullptr, nullptr, fl, s, true,
                                            false));
         RSVD_CK(launch_chol_wide(G, L.l, L.LP, tol(), R2s, r2inv, nullptr, colflag, h->dflags + kFlagUnrepaired, W,
                                  fl + 1, s, 0.0, nullptr, nullptr, nullptr));

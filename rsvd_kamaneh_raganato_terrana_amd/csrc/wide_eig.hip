@@ -1111,29 +1111,19 @@ __global__ __launch_bounds__(256) void sqgemm_f64_kernel(int M, int N, int K, do
         return TB ? B[(int64_t)k * ldb + j] : B[(int64_t)j * ldb + k];
     };
     f64x4 acc0 = MD::zero(), acc1 = MD::zero();
-    // (round 6: the loads of up to four of the wave's chunks -- K = 512 whole -- are issued before
-    // their MFMAs, one L2 round trip instead of four; the same products in the same order)
-    for (int kb = 32 * w; kb < K; kb += 512) {
-        double a[4][8], b[4][8];
+    for (int k0 = 32 * w; k0 < K; k0 += 128) {
+        double a[8], b[8];
 #pragma unroll
-        for (int it = 0; it < 4; ++it) {
-            const int k0 = kb + 128 * it;
-#pragma unroll
-            for (int s = 0; s < 4; ++s) {
-                a[it][s] = ld_a(k0 + 4 * h + s);
-                b[it][s] = ld_b(k0 + 4 * h + s);
-                a[it][4 + s] = ld_a(k0 + 16 + 4 * h + s);
-                b[it][4 + s] = ld_b(k0 + 16 + 4 * h + s);
-            }
+        for (int s = 0; s < 4; ++s) {
+            a[s] = ld_a(k0 + 4 * h + s);
+            b[s] = ld_b(k0 + 4 * h + s);
+            a[4 + s] = ld_a(k0 + 16 + 4 * h + s);
+            b[4 + s] = ld_b(k0 + 16 + 4 * h + s);
         }
 #pragma unroll
-        for (int it = 0; it < 4; ++it) {
-            if (kb + 128 * it >= K) break;
-#pragma unroll
-            for (int s = 0; s < 4; ++s) {
-                acc0 = MD::mma(a[it][s], b[it][s], acc0);
-                acc1 = MD::mma(a[it][4 + s], b[it][4 + s], acc1);
-            }
+        for (int s = 0; s < 4; ++s) {
+            acc0 = MD::mma(a[s], b[s], acc0);
+            acc1 = MD::mma(a[4 + s], b[4 + s], acc1);
         }
     }
     f64x4 t;
@@ -1155,14 +1145,119 @@ __global__ __launch_bounds__(256) void sqgemm_f64_kernel(int M, int N, int K, do
     }
 }
 
+// Round 6: 32 x 32 tiles of C (2 x 2 MFMA tiles per wave), K split in four contiguous ranges over the
+// waves, partials summed in wave order.  Per 16-deep chunk a wave issues 8 + 8 loads for 16 MFMAs
+// (the 16 x 16 form: 8 + 8 for 4), a k-contiguous operand as 32-B vector loads; the L2 reads of A and
+// B halve (each tile row / column is read by half as many workgroups).
+template <int TA, int TB>
+__global__ __launch_bounds__(256) void sqgemm2_f64_kernel(int M, int N, int K, double alpha,
+                                                          const double* __restrict__ A, int lda,
+                                                          const double* __restrict__ B, int ldb, double beta,
+                                                          double* C, int ldc, const double* Cin) {
+    __shared__ f64x4 part[3][4][64];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6, r = lane & 15, h = lane >> 4;
+    const int tm = (M + 31) / 32;
+    const int i0 = 32 * (blockIdx.x % tm), j0 = 32 * (blockIdx.x / tm);
+    const int kper = (K + 63) / 64 * 16;  // each wave's K range: a multiple of 16
+    const int kb = w * kper, ke = min(K, kb + kper);
+    // op(A)(i, k0 .. k0 + 3) and op(B)(k0 .. k0 + 3, j) (zero outside the matrix and the wave's range)
+    auto ld_a4 = [&](int i, int k0, double (&v)[4]) {
+        if (TA && i < M && k0 + 3 < ke && ((lda | k0) & 1) == 0) {
+            const double2 x = *reinterpret_cast<const double2*>(A + (int64_t)i * lda + k0);
+            const double2 y = *reinterpret_cast<const double2*>(A + (int64_t)i * lda + k0 + 2);
+            v[0] = x.x; v[1] = x.y; v[2] = y.x; v[3] = y.y;
+            return;
+        }
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const int k = k0 + s;
+            v[s] = (i < M && k < ke) ? (TA ? A[(int64_t)i * lda + k] : A[(int64_t)k * lda + i]) : 0.0;
+        }
+    };
+    auto ld_b4 = [&](int j, int k0, double (&v)[4]) {
+        if (!TB && j < N && k0 + 3 < ke && ((ldb | k0) & 1) == 0) {
+            const double2 x = *reinterpret_cast<const double2*>(B + (int64_t)j * ldb + k0);
+            const double2 y = *reinterpret_cast<const double2*>(B + (int64_t)j * ldb + k0 + 2);
+            v[0] = x.x; v[1] = x.y; v[2] = y.x; v[3] = y.y;
+            return;
+        }
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const int k = k0 + s;
+            v[s] = (j < N && k < ke) ? (TB ? B[(int64_t)k * ldb + j] : B[(int64_t)j * ldb + k]) : 0.0;
+        }
+    };
+    f64x4 acc[2][2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b) acc[a][b] = MD::zero();
+    // the next chunk's operands are loaded while this chunk's MFMAs run
+    double av[2][4], bv[2][4];
+    auto load = [&](int kc) {
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            ld_a4(i0 + 16 * t + r, kc + 4 * h, av[t]);
+            ld_b4(j0 + 16 * t + r, kc + 4 * h, bv[t]);
+        }
+    };
+    if (kb < ke) load(kb);
+    for (int kc = kb; kc < ke; kc += 16) {
+        double ac[2][4], bc[2][4];
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                ac[t][s] = av[t][s];
+                bc[t][s] = bv[t][s];
+            }
+        if (kc + 16 < ke) load(kc + 16);
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int b = 0; b < 2; ++b) acc[a][b] = MD::mma(ac[a][s], bc[b][s], acc[a][b]);
+    }
+    if (w > 0) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) part[w - 1][t][lane] = acc[t >> 1][t & 1];
+    }
+    __syncthreads();
+    if (w != 0) return;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        f64x4 v = acc[t >> 1][t & 1];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) v[q] = ((v[q] + part[0][t][lane][q]) + part[1][t][lane][q]) + part[2][t][lane][q];
+        const int j = j0 + 16 * (t & 1) + r;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int ii = i0 + 16 * (t >> 1) + MD::row(h, q);
+            if (ii < M && j < N) {
+                double* c = C + (int64_t)j * ldc + ii;
+                const double x = alpha * v[q];
+                *c = beta != 0.0 ? x + beta * (Cin ? Cin[(int64_t)j * ldc + ii] : *c) : x;
+            }
+        }
+    }
+}
+
 hipError_t launch_sqgemm(int ta, int tb, int M, int N, int K, double alpha, const double* A, int lda, const double* B,
                          int ldb, double beta, double* C, int ldc, hipStream_t s, const double* Cin = nullptr) {
-    const dim3 grid(((M + 15) / 16) * ((N + 15) / 16));
-#define SQG(X, Y)                                                                                                    \
-    if (ta == X && tb == Y) {                                                                                        \
-        hipLaunchKernelGGL((sqgemm_f64_kernel<X, Y>), grid, dim3(256), 0, s, M, N, K, alpha, A, lda, B, ldb, beta, C, \
-                           ldc, Cin);                                                                                \
-        return hipGetLastError();                                                                                    \
+    // 32 x 32 tiles from 384 x 384 up (LP = 512: 23 -> 15 us per 512^3 product); below, the 16 x 16 tiles
+    // keep more workgroups in flight (LP = 256: 6.2 us against 9.9 us on 64 tiles of 32 x 32)
+    const bool big = M >= 384 && N >= 384;
+    const dim3 grid(big ? ((M + 31) / 32) * ((N + 31) / 32) : ((M + 15) / 16) * ((N + 15) / 16));
+#define SQG(X, Y)                                                                                                      \
+    if (ta == X && tb == Y) {                                                                                          \
+        if (big)                                                                                                       \
+            hipLaunchKernelGGL((sqgemm2_f64_kernel<X, Y>), grid, dim3(256), 0, s, M, N, K, alpha, A, lda, B, ldb, beta, \
+                               C, ldc, Cin);                                                                           \
+        else                                                                                                           \
+            hipLaunchKernelGGL((sqgemm_f64_kernel<X, Y>), grid, dim3(256), 0, s, M, N, K, alpha, A, lda, B, ldb, beta,  \
+                               C, ldc, Cin);                                                                           \
+        return hipGetLastError();                                                                                      \
     }
     SQG(0, 0) SQG(0, 1) SQG(1, 0) SQG(1, 1)
 #undef SQG
@@ -1224,25 +1319,36 @@ constexpr double kIsqrtCut = 0.1;
 constexpr double kIsqrtC[9] = {1.0,          -0.5,         0.375,         -0.3125,           0.2734375,
                                -0.24609375, 0.2255859375, -0.20947265625, 0.196380615234375};
 
-// E = G - I on the l x l block, 0 outside; flags[0] = |E|_F <= cut (finite), flags[1] = !flags[0]
-__global__ __launch_bounds__(1024) void isqrt_prep_kernel(const double* __restrict__ G, int l, int LP,
-                                                          double* __restrict__ E, int* __restrict__ flags) {
-    __shared__ double part[16];
-    const int tid = threadIdx.x;
-    double ss = 0.0;
-    for (int e = tid; e < LP * LP; e += 1024) {
-        const int i = e / LP, j = e - i * LP;
-        const double v = (i < l && j < l) ? G[e] - (i == j ? 1.0 : 0.0) : 0.0;
+// E = G - I on the l x l block, 0 outside, 256 entries per workgroup; part[b] = the block's sum of squares
+__global__ __launch_bounds__(256) void isqrt_prep_kernel(const double* __restrict__ G, int l, int LP,
+                                                         double* __restrict__ E, double* __restrict__ part) {
+    __shared__ double red[4];
+    const int64_t e = blockIdx.x * 256 + threadIdx.x;
+    double v = 0.0;
+    if (e < (int64_t)LP * LP) {
+        const int i = (int)(e / LP), j = (int)(e - (int64_t)i * LP);
+        v = (i < l && j < l) ? G[e] - (i == j ? 1.0 : 0.0) : 0.0;
         E[e] = v;
-        ss = fma(v, v, ss);
     }
+    double ss = v * v;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o);
-    if ((tid & 63) == 0) part[tid >> 6] = ss;
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
     __syncthreads();
-    if (tid == 0) {
-        double t = 0.0;
-        for (int w = 0; w < 16; ++w) t += part[w];
+    if (threadIdx.x == 0) part[blockIdx.x] = ((red[0] + red[1]) + red[2]) + red[3];
+}
+// flags[0] = |E|_F <= cut (finite), flags[1] = !flags[0] from the nb block sums (fixed order)
+__global__ __launch_bounds__(256) void isqrt_flags_kernel(const double* __restrict__ part, int nb,
+                                                          int* __restrict__ flags) {
+    __shared__ double red[4];
+    double ss = 0.0;
+    for (int b = threadIdx.x; b < nb; b += 256) ss += part[b];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const double t = ((red[0] + red[1]) + red[2]) + red[3];
         const int small = (t <= kIsqrtCut * kIsqrtCut) ? 1 : 0;  // NaN: not small
         flags[0] = small;
         flags[1] = 1 - small;
@@ -1275,12 +1381,13 @@ hipError_t launch_isqrt_near_identity(const double* G, int l, int LP, double* E,
                                       double* T, double* out, int* flags, hipStream_t s, bool prep_only,
                                       bool series_only) {
     hipError_t er;
-    if (!series_only) {
-        hipLaunchKernelGGL(isqrt_prep_kernel, dim3(1), dim3(1024), 0, s, G, l, LP, E, flags);
+    const dim3 grid((unsigned)(((int64_t)LP * LP + 255) / 256));
+    if (!series_only) {  // (the block sums in E2, free until the series)
+        hipLaunchKernelGGL(isqrt_prep_kernel, grid, dim3(256), 0, s, G, l, LP, E, E2);
+        hipLaunchKernelGGL(isqrt_flags_kernel, dim3(1), dim3(256), 0, s, E2, (int)grid.x, flags);
         if ((er = hipGetLastError()) != hipSuccess || prep_only) return er;
     }
     const double* c = kIsqrtC;
-    const dim3 grid((unsigned)(((int64_t)LP * LP + 255) / 256));
     if ((er = launch_sqgemm(0, 0, l, l, l, 1.0, E, LP, E, LP, 0.0, E2, LP, s)) != hipSuccess) return er;
     if ((er = launch_sqgemm(0, 0, l, l, l, 1.0, E2, LP, E, LP, 0.0, E3, LP, s)) != hipSuccess) return er;
     hipLaunchKernelGGL(isqrt_poly_kernel, grid, dim3(256), 0, s, B, E, E2, nullptr, c[6], c[7], c[8], l, LP, 0, nullptr);
