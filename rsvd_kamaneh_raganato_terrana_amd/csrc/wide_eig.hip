@@ -1339,7 +1339,7 @@ __global__ __launch_bounds__(256) void isqrt_prep_kernel(const double* __restric
 }
 // flags[0] = |E|_F <= cut (finite), flags[1] = !flags[0] from the nb block sums (fixed order)
 __global__ __launch_bounds__(256) void isqrt_flags_kernel(const double* __restrict__ part, int nb,
-                                                          int* __restrict__ flags) {
+                                                          int* __restrict__ flags, double cut) {
     __shared__ double red[4];
     double ss = 0.0;
     for (int b = threadIdx.x; b < nb; b += 256) ss += part[b];
@@ -1349,7 +1349,7 @@ __global__ __launch_bounds__(256) void isqrt_flags_kernel(const double* __restri
     __syncthreads();
     if (threadIdx.x == 0) {
         const double t = ((red[0] + red[1]) + red[2]) + red[3];
-        const int small = (t <= kIsqrtCut * kIsqrtCut) ? 1 : 0;  // NaN: not small
+        const int small = (t <= cut * cut) ? 1 : 0;  // NaN: not small
         flags[0] = small;
         flags[1] = 1 - small;
     }
@@ -1384,7 +1384,13 @@ hipError_t launch_isqrt_near_identity(const double* G, int l, int LP, double* E,
     const dim3 grid((unsigned)(((int64_t)LP * LP + 255) / 256));
     if (!series_only) {  // (the block sums in E2, free until the series)
         hipLaunchKernelGGL(isqrt_prep_kernel, grid, dim3(256), 0, s, G, l, LP, E, E2);
-        hipLaunchKernelGGL(isqrt_flags_kernel, dim3(1), dim3(256), 0, s, E2, (int)grid.x, flags);
+        // RSVD_ISQRT_CUT (debugging, tests/test_gpu_switches.py): another cut-off; 0 sends every second pass
+        // to the predicated Cholesky factor
+        static const double cut = [] {
+            const char* v = std::getenv("RSVD_ISQRT_CUT");
+            return v ? std::atof(v) : kIsqrtCut;
+        }();
+        hipLaunchKernelGGL(isqrt_flags_kernel, dim3(1), dim3(256), 0, s, E2, (int)grid.x, flags, cut);
         if ((er = hipGetLastError()) != hipSuccess || prep_only) return er;
     }
     const double* c = kIsqrtC;
