@@ -34,7 +34,6 @@ struct WProjPlan {
     bool nn3 = false;  // bf16 NN at LP = 128 on wproj3_kernel (RSVD_NN3_128=0: the v2 kernel)
     bool nn8 = false;  // e4m3 NN halves on the v3-style wproj3nn8_kernel (RSVD_NN8=0: the v2 kernel)
     bool v3 = false; // v2 with launch-constant LDS read bases (bf16 A, LP 256 / 512; wide_proj.hip)
-    int sd = 1;       // v3: S-panel prefetch distance in k-steps (1 or 2; A runs as far ahead as LDS allows)
     bool tn2 = false; // v3 TN at LP = 256 with two k-steps per A slot (128-B A lines)
     bool half = false; // e4m3 A at LP = 512: two LP = 256 column-half launches (256-row tiles)
     bool tn4 = false;  // e4m3 TN at LP 256 / 512: four k-steps per A slot (128-B A lines, wproj3tn4_kernel)

@@ -739,7 +739,8 @@ struct W3Shape {
     static constexpr int GL = NS * SPW + APW;                  // glds per thread per step
     static constexpr size_t LDS = (size_t)SBASE + (size_t)NSS * SSLOT;
     static_assert(SPC % 8 == 0 && APC % 8 == 0, "v3 piece split");
-    static_assert(DA >= SD && LDS <= 163840, "v3 rings");
+    // DA > SD: A(st) must be issued before S(st) -- the steady-state wait counts only what follows S(st)
+    static_assert(DA > SD && LDS <= 163840, "v3 rings");
     static_assert((NS - 1) * SIMG + 32 * G < 65536, "immediate offsets");
 };
 
@@ -2003,11 +2004,12 @@ hipError_t wproj_lp(int nn, int fp8, const void* A, int64_t lda, int64_t m, int6
                 }
             }
 #endif
-            if constexpr (LP == 256) {  // (LP = 512 split: a third S slot does not fit)
-                if (!nn && p.tn2 && p.sd == 1)
+            if constexpr (LP == 256) {
+                // (round 6: the S panel two steps ahead instead of one -- sketch 1977 -> 2003 us at C4;
+                // profiles/r06_deadends.txt 22 -- so every v3 product keeps SD = 1)
+                if (!nn && p.tn2)
                     return split ? wproj3tn2_go<true>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d)
                                  : wproj3tn2_go<false>(A, lda, m, n, Shi, Slo, p, slabs, Out, s, d);
-                if (p.sd == 2) GO3(2);
             }
             GO3(1);
 #undef GO3
