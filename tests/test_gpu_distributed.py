@@ -203,6 +203,14 @@ def test_row_sharded_world8_matches_oracle(case):
     _check_world2(case, True, world=8)
 
 
+@pytest.mark.parametrize("case", [(32768, 2048, 256, 2, "bf16"), (32768, 2048, 512, 2, "e4m3")])
+def test_row_sharded_world8_larger_shards(case):
+    """the world > 1 kernel choices (fp64 Grams of the sharded passes, the per-shard
+    n-side passes, the deferred second pass's split Gram + G^-1/2 series) pinned at 4096 rows per rank --
+    half of C4's 8-GPU shard and a quarter of C5's -- against the oracle on the same A and Omega, 1e-4."""
+    _check_world2(case, True, world=8)
+
+
 @pytest.mark.parametrize("case", [(8191, 4000, 256, 2, "bf16"), (8192, 2000, 512, 2, "e4m3")])
 def test_row_sharded_world8_split_gram_sharded(case, monkeypatch):
     """RSVD_GRAM_SPLIT_SHARDED=1 (opt-in, round 6): the three-piece split Gram on sharded passes too --
