@@ -1868,7 +1868,7 @@ __global__ __launch_bounds__(512) void wproj3tn128_kernel(const bf16_t* __restri
         }
 }
 
-// ring depths (A slots, S slots): 4 / 2 in the engine; 3 / 3 for the lab (p.tn3 = 2)
+// ring depths (A slots, S slots): 4 / 2 in the engine; 3 / 3 in the lab only (p.tn3 = 2, RSVD_LAB builds)
 template <bool SPLIT>
 hipError_t wproj3tn128_go(const void* A, int64_t lda, int64_t m, int64_t n, const bf16_t* Shi, const bf16_t* Slo,
                           const WProjPlan& p, float* slabs, float* Out, hipStream_t s, hipEvent_t done) {
@@ -1876,11 +1876,13 @@ hipError_t wproj3tn128_go(const void* A, int64_t lda, int64_t m, int64_t n, cons
     const int64_t rows_out = n, K = m;
     float* o = p.splits == 1 ? Out : slabs;
     const int64_t stride = rows_out * 128;
+#ifdef RSVD_LAB
     if (p.tn3 == 2)
         hipLaunchKernelGGL((wproj3tn128_kernel<SPLIT, 3, 3>), dim3(p.blocks * p.splits), dim3(512),
                            (Tn128Shape<3, 3>::lds(NS)), s, reinterpret_cast<const bf16_t*>(A), lda, rows_out, K, m, Shi,
                            Slo, o, stride, p.chunk, p.blocks);
     else
+#endif
         hipLaunchKernelGGL((wproj3tn128_kernel<SPLIT, 4, 2>), dim3(p.blocks * p.splits), dim3(512),
                            (Tn128Shape<4, 2>::lds(NS)), s, reinterpret_cast<const bf16_t*>(A), lda, rows_out, K, m, Shi,
                            Slo, o, stride, p.chunk, p.blocks);
@@ -2072,11 +2074,11 @@ bool wproj_supported_lp(int LP) {
 
 int wproj_rows_per_block(int LP) { return LP <= 128 ? 256 : (LP == 256 ? 128 : 64); }
 
-static int tn128_mode() {  // RSVD_TN128: 0 the v2 double-step LP = 128 TN, 1 rings 4 / 2 (default), 2 rings 3 / 3
+static int tn128_mode() {  // RSVD_TN128: 0 the v2 double-step LP = 128 TN, 1 rings 4 / 2 (default)
     static const int env = [] {
         const char* v = std::getenv("RSVD_TN128");
         const int x = v ? std::atoi(v) : 1;
-        return x < 0 || x > 2 ? 1 : x;
+        return x == 0 ? 0 : 1;
     }();
     return env;
 }

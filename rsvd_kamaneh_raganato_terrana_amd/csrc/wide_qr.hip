@@ -2528,9 +2528,11 @@ hipError_t launch_chol_wide(const double* G, int l, int LP, double tol, double* 
         hipLaunchKernelGGL(chol_reg_kernel<4>, dim3(1), dim3(64 * kCholRegWaves),
                            std::max(CholReg<4>::lds_bytes, fuse ? CholRegInv<4>::lds_bytes : 0), s, G, l, tol, R, Rinv,
                            colflag, flag, pred, ill_tol, ill, d0src, ldg, Rinv32, Mt, fuse);
-    else if (chol_variant == 2 && LP == 256)  // lab only
+#ifdef RSVD_LAB
+    else if (chol_variant == 2 && LP == 256)  // the lab's register-resident LP = 256 factor (it spills)
         hipLaunchKernelGGL(chol_reg_kernel<16>, dim3(1), dim3(64 * kCholRegWaves), CholReg<16>::lds_bytes, s, G, l,
                            tol, R, Rinv, colflag, flag, pred, ill_tol, ill, d0src, ldg, Rinv32, Mt, 0);
+#endif
     else
         hipLaunchKernelGGL((chol_wide_kernel<kCholThreads, kCholBatch>), dim3(1), dim3(kCholThreads), chol_lds_bytes(LP),
                            s, G, l, LP, tol, work, R, Rinv, colflag, flag, pred, ill_tol, ill, d0src, ldg);

@@ -3,7 +3,7 @@
 # bench (RSVD_CHOL_PROF) compiled in.  Run after `make -C rsvd_kamaneh_raganato_terrana_amd/csrc all`.
 set -e
 cd "$(dirname "$0")/../rsvd_kamaneh_raganato_terrana_amd/csrc"
-F="--offload-arch=gfx950 -O3 -fPIC -std=c++17 -Wno-unused-result -DRSVD_CHOL_PROF"
+F="--offload-arch=gfx950 -O3 -fPIC -std=c++17 -Wno-unused-result -DRSVD_CHOL_PROF -DRSVD_LAB"
 T=$(mktemp -d)
 /opt/rocm/bin/hipcc $F -c wide_qr.hip -o $T/wide_qr.o
 /opt/rocm/bin/hipcc $F -I. -c ../../tools/wide_lab.cpp -o $T/wide_lab.o
