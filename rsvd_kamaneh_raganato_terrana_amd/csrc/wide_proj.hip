@@ -854,6 +854,20 @@ __global__ __launch_bounds__(512) void wproj3_kernel(const bf16_t* __restrict__ 
 #pragma unroll
         for (int t = 0; t < SH::APW; ++t) glds16<(KN & 1) ? 2 : 0>(asrc(st, t), slot + (t * 8 + w) * SH::APITCH);
     };
+    // KN bit 2 (IL): the step's LDS-DMA one piece per column group inside the MFMA loop (the same
+    // issue order as the burst after the barrier, so the waits count the same)
+    constexpr bool IL = (KN & 4) != 0 && !AR && ABL == 0;
+    constexpr int NSP = NS * SH::SPW;
+    static_assert(!IL || NSP + SH::APW <= G, "interleaved DMA: one piece per column group");
+    auto issueS_piece = [&](int st, int i) {
+        char* slot = smem_raw + SH::SBASE + (st % NSS) * SH::SSLOT;
+        const int a = i / SH::SPW, t = i % SH::SPW;
+        const bf16_t* S = (a ? Slo : Shi) + (kbeg + (int64_t)st * KS) * LP;
+        glds16(S + soff[t], slot + a * SH::SIMG + (t * 8 + w) * SImg::PITCH);
+    };
+    auto issueA_piece = [&](int st, int t) {
+        glds16<(KN & 1) ? 2 : 0>(asrc(st, t), smem_raw + (st % NA) * SH::AIMG + (t * 8 + w) * SH::APITCH);
+    };
     // AR: A through registers instead of LDS-DMA -- global_load_dwordx4 four steps ahead,
     // ds_write_b128 of the same 16 B to the same LDS address two steps ahead; S stays on the DMA.
     // Loads and writes are inline asm: the compiler's waitcnt pass cannot count the in-flight DMA
@@ -930,9 +944,12 @@ __global__ __launch_bounds__(512) void wproj3_kernel(const bf16_t* __restrict__ 
                 else wait_vm<0>();
                 __builtin_amdgcn_s_barrier();
             }
-            if (st + SD < nsteps) issueS(st + SD);
-            if (st + DA < nsteps) issueA(st + DA);
+            if constexpr (!IL) {
+                if (st + SD < nsteps) issueS(st + SD);
+                if (st + DA < nsteps) issueA(st + DA);
+            }
         }
+        const bool il_s = st + SD < nsteps, il_a = st + DA < nsteps;
         const uint32_t sS = lds0 + SH::SBASE + (uint32_t)((st % NSS) * SH::SSLOT);
         const uint32_t sA = lds0 + (uint32_t)((st % NA) * SH::AIMG);
         const uint32_t bS1 = sS + lS1, bS2 = sS + lS2, bA1 = sA + lA1, bA2 = sA + lA2;
@@ -982,6 +999,13 @@ __global__ __launch_bounds__(512) void wproj3_kernel(const bf16_t* __restrict__ 
         auto gstep = [&](auto gc) {
             constexpr int g = decltype(gc)::value;
             if constexpr (g + 1 < G) bread(std::integral_constant<int, g + 1>{}, bb[(g + 1) & 1]);
+            if constexpr (IL) {
+                if constexpr (g < NSP) {
+                    if (il_s) issueS_piece(st + SD, g);
+                } else if constexpr (g < NSP + SH::APW) {
+                    if (il_a) issueA_piece(st + DA, g - NSP);
+                }
+            }
             __builtin_amdgcn_sched_barrier(0);  // the next tile's reads go out before this tile's MFMAs
             const i32x2* b = bb[g & 1];
             const bf16x8_t bh = join2(b[0], b[1]);
@@ -1026,7 +1050,9 @@ hipError_t wproj3_go(const void* A, int64_t lda, int64_t m, int64_t n, const bf1
     const int64_t rows_out = NN ? m : n, K = NN ? n : m;
     float* o = p.splits == 1 ? Out : slabs;
     const int64_t stride = rows_out * LP;
-    constexpr int KN = NN ? 3 : 0;  // as v2 (profiles/r02_wide_lab_knobs.txt)
+    // as v2 (profiles/r02_wide_lab_knobs.txt), plus the interleaved DMA (bit 2, round 6) for the LP = 256 NN
+    // (C4 -0.23 ms on one box, bit-identical; the LP = 128 NN measured 4.99 -> 5.01 ms at C3 with it)
+    constexpr int KN = NN ? ((LP == 256 && ABL == 0) ? 7 : 3) : 0;
 #ifdef RSVD_LAB
     constexpr bool ar_ok = ABL == 0 && SD == 1 && SH::NA >= 3;  // register-staged A fits
 #else
@@ -1051,7 +1077,8 @@ hipError_t wproj3_go(const void* A, int64_t lda, int64_t m, int64_t n, const bf1
             case 0: go(std::integral_constant<int, 0>{}); break;
             case 1: go(std::integral_constant<int, 1>{}); break;
             case 2: go(std::integral_constant<int, 2>{}); break;
-            default: go(std::integral_constant<int, 3>{}); break;
+            case 3: go(std::integral_constant<int, 3>{}); break;
+            default: go(std::integral_constant<int, KN>{}); break;
         }
     } else {
         go(std::integral_constant<int, KN>{});
@@ -1135,6 +1162,22 @@ __global__ __launch_bounds__(512) void wproj3tn2_kernel(const bf16_t* __restrict
 #pragma unroll
         for (int t = 0; t < APW2; ++t) glds16<(KN & 1) ? 2 : 0>(asrc(d, t), slot + (t * 8 + w) * 1024);
     };
+    // KN bit 2 (IL): the step's LDS-DMA goes out one piece per column group inside the MFMA loop
+    // instead of as a burst of NS SPW + APW2 right after the barrier (the same issue order, so the
+    // waits count the same).  Piece i < NS SPW: S(st + 1) image i / SPW, piece i % SPW; the next APW2:
+    // the A slot's pieces.
+    constexpr bool IL = (KN & 4) != 0;
+    constexpr int NSP = NS * SH::SPW;
+    static_assert(!IL || NSP + APW2 <= G, "interleaved DMA: one piece per column group");
+    auto issueS_piece = [&](int st, int i) {
+        char* slot = smem_raw + SBASE + (st & 1) * SH::SSLOT;
+        const int a = i / SH::SPW, t = i % SH::SPW;
+        const bf16_t* S = (a ? Slo : Shi) + (kbeg + (int64_t)st * KS) * LP;
+        glds16(S + soff[t], slot + a * SH::SIMG + (t * 8 + w) * SImg::PITCH);
+    };
+    auto issueA_piece = [&](int d, int t) {
+        glds16<(KN & 1) ? 2 : 0>(asrc(d, t), smem_raw + (d & 1) * ASLOT + (t * 8 + w) * 1024);
+    };
     // AR: A(d + 1) is ds_written at step 2d from registers loaded at step 2d - 2 (one A buffer: the
     // write of A(d + 1) precedes the load of A(d + 2) in the same step); see wproj3_kernel.
     i32x4 areg[APW2];
@@ -1184,10 +1227,11 @@ __global__ __launch_bounds__(512) void wproj3tn2_kernel(const bf16_t* __restrict
             if (hs == 0 && d + 1 < nd) writeA(d + 1);
             if (st + 1 < nsteps) issueS(st + 1);
             if (hs == 0 && d + 2 < nd) loadA(d + 2);
-        } else {
+        } else if constexpr (!IL) {
             if (st + 1 < nsteps) issueS(st + 1);
             if (hs == 0 && d + 1 < nd) issueA(d + 1);
         }
+        const bool il_s = st + 1 < nsteps, il_a = hs == 0 && d + 1 < nd;
         const uint32_t sS = lds0 + SBASE + (uint32_t)((st & 1) * SH::SSLOT);
         const uint32_t sA = lds0 + (uint32_t)((d & 1) * ASLOT);
         const uint32_t bS1 = sS + lS1, bS2 = sS + lS2, bA = sA + (hs ? lA1 : lA0);
@@ -1222,6 +1266,13 @@ __global__ __launch_bounds__(512) void wproj3tn2_kernel(const bf16_t* __restrict
         auto gstep = [&](auto gc) {
             constexpr int g = decltype(gc)::value;
             if constexpr (g + 1 < G) bread(std::integral_constant<int, g + 1>{}, bb[(g + 1) & 1]);
+            if constexpr (IL && !AR) {
+                if constexpr (g < NSP) {
+                    if (il_s) issueS_piece(st + 1, g);
+                } else if constexpr (g < NSP + APW2) {
+                    if (il_a) issueA_piece(d + 1, g - NSP);
+                }
+            }
             __builtin_amdgcn_sched_barrier(0);
             const i32x2* b = bb[g & 1];
             const bf16x8_t bh = join2(b[0], b[1]);
@@ -1437,7 +1488,7 @@ __global__ __launch_bounds__(512) void wproj3tn4_kernel(const uint8_t* __restric
 // fixed for the launch; one v_add each per step).  A lane's fragment is ds_read_b64_tr_b8 of k rows
 // 8 h .. 8 h + 7 of its column, widened to bf16 exactly.  Rings: A NA x 8 KiB (read DA = NA - 1
 // steps ahead), S 2 x (hi + lo) images.  Same k order and MFMA order as v2: bit-identical.
-template <bool SPLIT>
+template <bool SPLIT, bool IL = false>
 __global__ __launch_bounds__(512) void wproj3nn8_kernel(const uint8_t* __restrict__ A, int64_t lda, int64_t rows_out,
                                                         int64_t K, int64_t arows, const bf16_t* __restrict__ Shi,
                                                         const bf16_t* __restrict__ Slo, float* __restrict__ out,
@@ -1518,14 +1569,29 @@ __global__ __launch_bounds__(512) void wproj3nn8_kernel(const uint8_t* __restric
         if (i == -1 && nsteps > 0) issueS(0);
         if (i + DA < nsteps) issueA(i + DA);
     }
+    // IL (round 6, the engine's form): the step's LDS-DMA one piece per column group inside the MFMA
+    // loop instead of a burst after the barrier, the same issue order (the waits count the same);
+    // bit-identical, C5 17.16 -> 17.07 ms on one box.  (The e4m3 TN measured slower with it: its A
+    // slot spans four steps, 1639 -> 1678 us.)
+    constexpr int NSP = NS * SH::SPW;
+    static_assert(!IL || NSP + 1 <= G, "interleaved DMA: one piece per column group");
+    auto issueS_piece = [&](int st, int i) {
+        char* slot = smem_raw + SBASE + (st & 1) * SH::SSLOT;
+        const int a = i / SH::SPW, t = i % SH::SPW;
+        const bf16_t* S = (a ? Slo : Shi) + (kbeg + (int64_t)st * KS) * s_pitch;
+        glds16(S + soff[t], slot + a * SH::SIMG + (t * 8 + w) * SImg::PITCH);
+    };
     const uint32_t lds0 = lds_addr(smem_raw);
     for (int st = 0; st < nsteps; ++st) {
         // S(st) and A(st) have landed once at most A(st - 1 + DA), issued behind S(st), is in flight
         if (st - 1 + DA < nsteps) wait_vm<1>();
         else wait_vm<0>();
         __builtin_amdgcn_s_barrier();
-        if (st + 1 < nsteps) issueS(st + 1);
-        if (st + DA < nsteps) issueA(st + DA);
+        if constexpr (!IL) {
+            if (st + 1 < nsteps) issueS(st + 1);
+            if (st + DA < nsteps) issueA(st + DA);
+        }
+        const bool il_s = st + 1 < nsteps, il_a = st + DA < nsteps;
         const uint32_t sS = lds0 + SBASE + (uint32_t)((st & 1) * SH::SSLOT);
         const uint32_t sA = lds0 + (uint32_t)((st % NA) * AIMG);
         const uint32_t bS1 = sS + lS1, bS2 = sS + lS2;
@@ -1557,6 +1623,13 @@ __global__ __launch_bounds__(512) void wproj3nn8_kernel(const uint8_t* __restric
         auto gstep = [&](auto gc) {
             constexpr int g = decltype(gc)::value;
             if constexpr (g + 1 < G) bread(std::integral_constant<int, g + 1>{}, bb[(g + 1) & 1]);
+            if constexpr (IL) {
+                if constexpr (g < NSP) {
+                    if (il_s) issueS_piece(st + 1, g);
+                } else if constexpr (g == NSP) {
+                    if (il_a) issueA(st + DA);
+                }
+            }
             __builtin_amdgcn_sched_barrier(0);
             const i32x2* b = bb[g & 1];
             const bf16x8_t bh = join2(b[0], b[1]);
@@ -1603,14 +1676,14 @@ hipError_t wproj3nn8_go(const void* A, int64_t lda, int64_t m, int64_t n, const 
     float* o = p.splits == 1 ? Out : slabs;
     const int64_t stride = rows_out * 512;
     if (p.merge) {
-        hipLaunchKernelGGL((wproj3nn8_kernel<SPLIT>), dim3(2 * p.blocks * p.splits), dim3(512), lds, s,
+        hipLaunchKernelGGL((wproj3nn8_kernel<SPLIT, true>), dim3(2 * p.blocks * p.splits), dim3(512), lds, s,
                            reinterpret_cast<const uint8_t*>(A), lda, rows_out, K, m, Shi, Slo, o, stride, p.chunk,
                            p.blocks, 512, 512, 2);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
     } else {
         for (int hf = 0; hf < 2; ++hf) {
-            hipLaunchKernelGGL((wproj3nn8_kernel<SPLIT>), dim3(p.blocks * p.splits), dim3(512), lds, s,
+            hipLaunchKernelGGL((wproj3nn8_kernel<SPLIT, true>), dim3(p.blocks * p.splits), dim3(512), lds, s,
                                reinterpret_cast<const uint8_t*>(A), lda, rows_out, K, m, Shi + 256 * hf,
                                Slo ? Slo + 256 * hf : nullptr, o + 256 * hf, stride, p.chunk, p.blocks, 512, 512, 1);
             hipError_t e = hipGetLastError();
@@ -1678,14 +1751,15 @@ hipError_t wproj3tn2_go(const void* A, int64_t lda, int64_t m, int64_t n, const 
                            stride, p.chunk, p.blocks);
     };
 #ifdef RSVD_LAB
-    switch (p.kn < 0 ? 0 : p.kn) {  // KN 0 in the engine; the others for the lab knob sweep
+    switch (p.kn < 0 ? 4 : p.kn) {  // KN 4 (interleaved DMA) in the engine; the others for the lab knob sweep
+        case 0: go(std::integral_constant<int, 0>{}); break;
         case 1: go(std::integral_constant<int, 1>{}); break;
         case 2: go(std::integral_constant<int, 2>{}); break;
         case 3: go(std::integral_constant<int, 3>{}); break;
-        default: go(std::integral_constant<int, 0>{}); break;
+        default: go(std::integral_constant<int, 4>{}); break;
     }
 #else
-    go(std::integral_constant<int, 0>{});
+    go(std::integral_constant<int, 4>{});  // interleaved DMA (KN bit 2, round 6)
 #endif
     hipError_t e = hipGetLastError();
     if (e == hipSuccess && done) e = hipEventRecord(done, s);
