@@ -136,8 +136,11 @@ def pmc_traffic(key, kernel_prefix):
 def pmc_mfma_busy(key, kernel_prefix):
     """MFMA pipe occupancy of the kernel from the committed rocprofv3 pass for this workload
     (profiles/*_mfma_busy.json, tools/pmc_mfma.sh + tools/mfma_busy.py: SQ_VALU_MFMA_BUSY_CYCLES over
-    the SIMD-cycles at the clock the kernel actually ran, GRBM_GUI_ACTIVE).  Passes whose clock
-    estimate exceeds the 2.4 GHz peak are not evidence and are skipped.  None when absent."""
+    the SIMD-cycles at the clock the kernel actually ran, GRBM_GUI_ACTIVE).  A clock estimate above
+    the 2.4 GHz peak means GUI_ACTIVE also counted the dispatch overhead of a short kernel (C2's
+    ~27-us projections): there the busy cycles are priced against the dispatch duration at 2.4 GHz
+    instead -- a lower bound of the busy fraction, since the chip ran at most that clock -- and the
+    entry says so.  None when absent."""
     import glob
     import re
 
@@ -153,8 +156,16 @@ def pmc_mfma_busy(key, kernel_prefix):
         if d.get("workload") != key:
             continue
         for k, v in d.get("kernels", {}).items():
-            if k.startswith(kernel_prefix) and 0 < v.get("clock_GHz_est", 9.9) <= 2.4:
-                best = {"frac": v["mfma_busy_frac"], "clock_GHz": v["clock_GHz_est"], "source": os.path.relpath(f, REPO)}
+            if not k.startswith(kernel_prefix):
+                continue
+            clk = v.get("clock_GHz_est", 0.0)
+            if 0 < clk <= 2.4:
+                best = {"frac": v["mfma_busy_frac"], "clock_GHz": clk, "source": os.path.relpath(f, REPO)}
+            elif clk > 2.4:  # busy / (1024 SIMDs x duration x 2.4 GHz), duration = GUI_ACTIVE / 8 / clk
+                best = {"frac": v["mfma_busy_frac"] * clk / 2.4, "clock_GHz": None, "bound": "lower",
+                        "note": "short dispatch: GUI_ACTIVE includes dispatch overhead (clock estimate "
+                                f"{clk:.2f} GHz); busy cycles priced at the 2.4 GHz peak over the dispatch",
+                        "source": os.path.relpath(f, REPO)}
     return best
 
 

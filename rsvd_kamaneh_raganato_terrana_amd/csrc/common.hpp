@@ -66,18 +66,22 @@ template <> struct Vec16<double> {
     static __device__ __forceinline__ double get(const double2& v, int t) { return t == 0 ? v.x : v.y; }
 };
 
-// Launch of a persistent grid whose workgroups wait on each other (grid barriers, spin hand-offs):
-// a cooperative launch, so co-residency is the runtime's guarantee -- the launch fails when the
-// grid cannot be resident at once (e.g. CUs held by another process's kernels) -- instead of an
-// assumption the kernel's bounded spins can only report after the fact.
-// RSVD_COOP=0 in the environment launches them plainly (the same kernel; for profiling runs that
-// need a clean exit: under rocprofv3 7.2 --kernel-trace ANY process that made a cooperative launch
-// segfaults in the HIP runtime's exit-time teardown, after the trace is written -- reproduced without
-// this library by tools/coop_repro.hip, see profiles/r04_exit_segv/README.md).
+// Launch of a persistent grid whose workgroups wait on each other (grid barriers, spin hand-offs).
+// Residency comes from the grid size alone (plain, cooperative and graph launches of one grid are
+// equally resident, MI355X_MICROARCH.md coop-launch row): launch_coresident checks the grid against
+// the occupancy query x CU count itself -- the check hipLaunchCooperativeKernel would make -- refuses
+// an oversize grid, and every spin in these kernels is bounded.  Round 6: the launch is PLAIN by
+// default.  The cooperative launch bought nothing beyond that check and cost wall time in the rSVD
+// loop: same box, alternating (gpurun_out ab_coop_*, profiles/r06_coop_ab.txt) C4 22.73 / 22.74 ->
+// 22.44 / 22.54 ms, C5 17.00 / 17.01 -> 16.72 / 16.76 ms per rSVD, with one or two persistent
+// launches per rSVD (tridiagonalisation phase 1, block Jacobi).  RSVD_COOP=1 selects
+// hipLaunchCooperativeKernel (under rocprofv3 7.2 --kernel-trace ANY process that made a cooperative
+// launch segfaults in the HIP runtime's exit-time teardown, after the trace is written --
+// reproduced without this library by tools/coop_repro.hip, profiles/r04_exit_segv/README.md).
 inline bool coop_launch_enabled() {
     static const int env = [] {
         const char* v = std::getenv("RSVD_COOP");
-        return v ? std::atoi(v) : 1;
+        return v ? std::atoi(v) : 0;
     }();
     return env != 0;
 }

@@ -11,7 +11,7 @@ against the fp64 oracle on the same A and Omega:
 * RSVD_DEFER2=0       output panels' CholeskyQR2 with Q and Q_B formed (the pre-round-6 order)
 * RSVD_ISQRT=0        the deferred second pass's R2^-1 by the Cholesky factor instead of the G^-1/2 series
 * RSVD_ISQRT_CUT=0    the series' cut-off at 0: its predicated Cholesky fallback runs on every second pass
-* RSVD_COOP=0         plain launches of the persistent kernels (profiling runs)
+* RSVD_COOP=1         cooperative launches of the persistent kernels (plain is the default since round 6)
 """
 import json
 import os
@@ -49,7 +49,7 @@ eng.close()
 
 @pytest.mark.parametrize("env", [{"RSVD_GRAM_SPLIT": "0"}, {"RSVD_SMALL_SVD": "jacobi"}, {"RSVD_DEFER2": "0"},
                                  {"RSVD_ISQRT": "0"}, {"RSVD_ISQRT_CUT": "0"},
-                                 {"RSVD_COOP": "0"}, {}])
+                                 {"RSVD_COOP": "1"}, {}])
 def test_switch_matches_oracle(env, tmp_path):
     m, n, l = 2048, 1200, 256  # l > 192: the eigensolver's multi-workgroup (persistent) phase runs
     A = gapped_matrix(m, n, 2 * l, decay=0.985, seed=12)
