@@ -295,6 +295,9 @@ def main():
     ap.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
                     help="N > 1: torch.distributed backend (nccl = RCCL; gloo with --comm torch runs the whole "
                          "multi-rank path with every rank on one GPU, for the one-GPU test box)")
+    ap.add_argument("--lda-pad", type=int, default=0,
+                    help="diagnostics: store A column-major with leading dimension m + PAD (elements) instead of "
+                         "m -- the caller's layout choice; the headline line keeps lda = m (Eigen's layout)")
     ap.add_argument("--emulate-world", type=int, default=0,
                     help="diagnostics, one process: run rank 0 of an N-rank strong-scaled job alone (its rows of A, "
                          "its n shard, the sharded-panel kernels) with no-op collectives -- prices the per-rank "
@@ -355,6 +358,11 @@ def main():
             return float(t.item())
 
         A, a_scale = make_A(torch, m_local, n, row0, dt, amax_reduce=amax_all)
+        if args.lda_pad > 0:  # the same A in a buffer whose column pitch is m + pad (BLAS lda > m)
+            Ap = R.empty_colmajor(m_local, n, A.dtype, A.device, pad=args.lda_pad)
+            Ap.copy_(A)
+            del A
+            A = Ap
     eng = R.Engine(dev)
     if world > 1:
         if args.comm == "library":  # rsvd_comm_init: RCCL owned by the C ABI, rank 0's id broadcast
@@ -559,6 +567,7 @@ def main():
             "config": {
                 "workload": label + (f"; {m_global}x{n} global, {m_local} rows/GPU" if world > 1 else ""),
                 "m": m_global, "n": n, "l": l, "q": q, "m_per_gpu": m_local,
+                "lda": int(A.stride(1)) if A.dim() == 2 else m_local,
                 "parallelism": par,
                 "algorithmic_tflop_per_step": f_total / 1e12,
             },

@@ -59,9 +59,14 @@ def colmajor(t):
     return c, max(1, c.shape[0])
 
 
-def empty_colmajor(rows: int, cols: int, dtype, device):
+def empty_colmajor(rows: int, cols: int, dtype, device, pad: int = 0):
+    """An uninitialised column-major rows x cols matrix; pad > 0 gives it the leading dimension
+    rows + pad.  For a tall A whose row count is a large power of two, a pad of 64 elements keeps the
+    columns of one k-step off a common HBM address pattern: C3's A^T Q 0.66 -> 0.54 ms per launch
+    (profiles/r06_ldapad_ab.txt; no effect at C4 / C5).  Eigen callers pass lda = m."""
     torch = _torch()
-    return torch.empty((cols, rows), dtype=dtype, device=device).t()
+    buf = torch.empty((cols, rows + max(0, pad)), dtype=dtype, device=device)
+    return buf[:, :rows].t()
 
 
 def make_allreduce_hook(get_buffer, group=None):
