@@ -100,3 +100,50 @@ def test_bench_c5_family_matches_oracle(engine):
     16384 rows: the fp8 x fp8 block-scaled sketch, the four-step e4m3 TN halves, the LP = 512 split
     Grams and three-level factors, the LP = 512 eigensolver."""
     _pin(engine, "c5", 16384, 8192, 512, 2, "fp8")
+
+
+@pytest.mark.timeout(900)
+def test_bench_c3_fullsize_matches_oracle(engine):
+    """C3 at its full BASELINE size (configs[2]: 2^20 x 1024 bf16, l = 128, q = 1) against the fp64
+    oracle on the same bf16 A and Omega (the full-size configs were held by
+    property checks only).  The oracle's 1.1 TFLOP of fp64 work takes about a minute on the box's
+    host cores; C4 / C5 at full size would take several minutes each and stay property-checked
+    (tests/test_gpu_fullsize.py) with their families pinned above."""
+    _pin(engine, "c3", 1 << 20, 1024, 128, 1, "bf16")
+
+
+def test_padded_lda_is_bit_identical(engine):
+    """The caller's column pitch (bench.py --lda-pad, empty_colmajor(pad=)) changes only addresses:
+    C3's family with lda = m + 64 (and m + 256) gives the same U, S, V bit for bit as lda = m -- the
+    LP = 128 kernels (separate-ring TN, hi / lo NN, split Gram) read A through lda."""
+    import torch
+
+    sys.path.insert(0, REPO)
+    import bench
+    import rsvd_kamaneh_raganato_terrana_amd as R
+
+    m, n, l, seed = 131072, 1024, 128, 0x5EED0002
+    A, _ = bench.make_A(torch, m, n, 0, "bf16")
+    ref = [x.clone() for x in engine.rsvd(A, l, q=1, seed=seed)]
+    for pad in (64, 256):
+        Ap = R.empty_colmajor(m, n, A.dtype, A.device, pad=pad)
+        Ap.copy_(A)
+        assert Ap.stride(1) == m + pad
+        out = engine.rsvd(Ap, l, q=1, seed=seed)
+        torch.cuda.synchronize()
+        for a, b in zip(ref, out):
+            assert torch.equal(a, b), pad
+        del Ap
+
+
+_FULL = os.environ.get("RSVD_FULLSIZE_PINS", "0") == "1"
+
+
+@pytest.mark.skipif(not _FULL, reason="RSVD_FULLSIZE_PINS=1: minutes of fp64 oracle work per config")
+@pytest.mark.timeout(1100)
+@pytest.mark.parametrize("cfg,m,n,l,q,dt", [("c5", 131072, 8192, 512, 2, "fp8"), ("c4", 65536, 65536, 256, 2, "bf16")])
+def test_bench_fullsize_matches_oracle(engine, cfg, m, n, l, q, dt):
+    """C5 and C4 at their full BASELINE sizes against the fp64 oracle (same A, Omega, scale).  The
+    oracle needs ~7 (C5) and ~13 (C4) TFLOP of fp64 work -- several minutes each on the box's host
+    cores -- so the default suite skips them; the committed run is profiles/r06_fullsize_pins.txt."""
+    _pin(engine, cfg, m, n, l, q, dt)
