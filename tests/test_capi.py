@@ -119,3 +119,20 @@ def test_no_cpu_fallback_without_gpu(lib):
     assert lib.rsvd_create(0, ctypes.byref(h)) == 4  # RSVD_ERR_NO_DEVICE
     with pytest.raises(R.RSVDError):
         R.rSVD(np.eye(8), 4)
+
+
+def test_empty_colmajor_padded_pitch():
+    """empty_colmajor(pad=) (INTEGRATION.md "Layout"): a column-major view whose leading dimension is
+    rows + pad -- what Engine.desc() passes as lda (max(stride(1), rows))."""
+    import torch
+
+    import rsvd_kamaneh_raganato_terrana_amd as R
+
+    for pad in (0, 64):
+        A = R.empty_colmajor(7, 3, torch.float32, "cpu", pad=pad)
+        assert A.shape == (7, 3) and A.stride() == (1, 7 + pad)
+        B = torch.arange(21, dtype=torch.float32).reshape(7, 3)
+        A.copy_(B)
+        assert torch.equal(A, B)
+        C, ld = R.colmajor(A)
+        assert C.data_ptr() == A.data_ptr() and ld == 7 + pad  # no copy: the padded view is accepted as is
